@@ -1,0 +1,109 @@
+/*
+ * hiprag.h -- C ABI of libhiprag.so, the MI355X-native vector index behind
+ * youtu-rag's KB-search plugin interfaces.
+ *
+ * Every entry point replaces one numeric call of the reference's vector store
+ * (paths relative to the youtu-rag tree; the store is a BaseVectorStore,
+ * utu/rag/base.py:187-232):
+ *
+ *   hr_index_create    ChromaVectorStore.__init__ / FAISSVectorStore.__init__
+ *                        (chroma_store.py:25-62 get_or_create_collection with hnsw:space;
+ *                         faiss_store.py:31-58 IndexFlatIP/IndexFlatL2 choice :102-105)
+ *   hr_index_add       add_chunks -> collection.add / normalize_L2 + index.add
+ *                        (chroma_store.py:64-88, faiss_store.py:89-127)
+ *   hr_index_remove    delete / delete_by_document_id (row tombstones)
+ *                        (chroma_store.py:150-183, faiss_store.py:201-254)
+ *   hr_index_search    search -> collection.query(n_results=top_k, where=...)
+ *                        (chroma_store.py:90-148; exact semantics of faiss_store.py:129-199)
+ *   hr_index_search_device  the same on device-resident queries/results (batched
+ *                        VectorRetriever.batch_retrieve, base_retriever.py:82-99)
+ *   hr_index_size      count (chroma_store.py:249-255, faiss_store.py:283-289)
+ *   hr_index_get_rows  get_by_id's stored embedding (chroma_store.py:224-247)
+ *   hr_index_save/load PersistentClient dir / faiss write_index+pickle
+ *                        (chroma_store.py:41-44, faiss_store.py:61-87)
+ *   hr_index_search_shard / hr_index_search_shard_collect / hr_merge_candidates
+ *                      row-sharded multi-GPU search (no reference counterpart: the
+ *                      reference is single-process)
+ *   hr_pool_normalize  the embedding server's masked mean-pool + F.normalize
+ *                        (docs/content/docs/en/youtu-embedding/deploying-locally.mdx:75-79, :98-115)
+ *
+ * Conventions: every int-returning call returns 0 on success or a negative
+ * HR_E_* code; hr_last_error() then holds a thread-local message.  Handles are
+ * opaque; calls on one handle are serialised by an internal mutex.  Host
+ * pointers are caller-owned; "_device"/"_shard"/merge calls take device pointers
+ * and run on the given hipStream_t (NULL = the null stream, which is also
+ * PyTorch's default stream); host-pointer calls use the handle's own stream and
+ * return after synchronising it.  Scores follow the
+ * reference's similarity convention (cosine/dot: inner product).  Result order:
+ * score descending, then row ascending; unfilled slots hold score -inf, row -1.
+ */
+#ifndef HIPRAG_H
+#define HIPRAG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hr_index hr_index;
+
+enum { HR_F32 = 0, HR_BF16 = 1, HR_F16 = 2 };         /* storage dtype */
+enum { HR_COSINE = 0, HR_IP = 1, HR_L2 = 2 };         /* distance metric (L2: not yet on the GPU path) */
+enum {
+    HR_OK = 0,
+    HR_E_INVALID = -1,   /* bad argument -> Python ValueError */
+    HR_E_HIP = -2,       /* HIP runtime error -> RuntimeError */
+    HR_E_UNSUPPORTED = -3,
+    HR_E_OVERFLOW = -4,  /* candidate buffer overflow in the exact fallback */
+    HR_E_IO = -5
+};
+
+#define HR_MAX_K 32            /* top-k served by the fast path */
+
+int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);
+int hr_index_reserve(hr_index* h, int64_t capacity_rows);
+int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* first_row_out);
+int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global_row0, int64_t n, int64_t* first_row_out);
+int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n);
+int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
+                    int64_t* rows_out);
+int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const uint64_t* row_mask_dev,
+                           float* scores_out_dev, int64_t* rows_out_dev, void* stream);
+int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out);
+int hr_index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out);
+int hr_index_save(hr_index* h, const char* path);
+int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr_index** out);
+void hr_index_destroy(hr_index* h);
+
+/* Row-sharded search pieces (one process per GPU; RCCL moves the candidates).
+ * Candidate record = {double exact_score; int64 global_row} (16 bytes).
+ * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_K).             */
+int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
+                          int64_t row_offset, void* cand_out_dev /* B*kc records */,
+                          double* bound_out_dev /* B */, void* stream);
+int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev /* B */,
+                                  int cap, const uint64_t* row_mask_dev, int64_t row_offset,
+                                  void* cand_out_dev /* B*cap records */, double* bound_out_dev, void* stream);
+int hr_merge_candidates(int device, const void* cand_dev /* G*B*kc records */, const double* bounds_dev /* G*B */,
+                        int G, int B, int kc, int k, float* scores_out_dev, int64_t* rows_out_dev,
+                        double* kth_out_dev, int32_t* fail_out_dev, void* stream);
+
+/* K7: masked mean-pool of the first-dim hidden states with the first n_instr
+ * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */
+int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,
+                      float* out_dev, void* stream);
+
+/* Timing of the most recent scan launch on this handle (ms, HIP events). */
+int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms);
+int hr_device_count(int* n_out);
+/* Diagnostics: approximate MFMA scores of every row (B <= 64; approx_out B×n) and the
+ * per-query error bound E_q that the exactness guard uses (e_out, B). */
+int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out);
+const char* hr_last_error(void);
+int hr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPRAG_H */

@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "youtu-rag_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libhiprag.so on the device)")
+    config.addinivalue_line("markers", "slow: long-running (full-size) checks")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

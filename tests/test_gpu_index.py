@@ -1,0 +1,288 @@
+"""GPU parity tests: libhiprag.so (through its C ABI) against the CPU oracle and the
+golden vectors produced by the reference's own VectorRetriever (tests/golden/).
+
+Bar: returned rows identical (bit-exact, including the (score desc, row asc) tie
+order); scores identical to the oracle's fp64 canonical scores cast to fp32, and
+within 1e-5 of the golden fp64 scores (north_star tolerance).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import ref_numpy as R
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def native():
+    from hiprag import _native
+
+    _native.load_library()
+    assert _native.device_count() >= 1, "no HIP device visible"
+    return _native
+
+
+def _stored_as_f32(stored, dtype):
+    return R.dequantize(stored, dtype)
+
+
+def _planted_queries(corpus_rows_f32, B, rng, noise=0.05):
+    n, dim = corpus_rows_f32.shape
+    idx = rng.choice(n, B, replace=False)
+    base = corpus_rows_f32[idx] / np.linalg.norm(corpus_rows_f32[idx], axis=1, keepdims=True)
+    eps = rng.standard_normal((B, dim)).astype(np.float32)
+    eps /= np.linalg.norm(eps, axis=1, keepdims=True)
+    return (base + noise * eps).astype(np.float32)
+
+
+def _check(s_gpu, r_gpu, s_ref, r_ref):
+    np.testing.assert_array_equal(r_gpu, r_ref)
+    valid = r_ref >= 0
+    np.testing.assert_array_equal(s_gpu[valid], s_ref[valid].astype(np.float32))
+    assert np.all(np.isneginf(s_gpu[~valid]))
+
+
+# ---------------------------------------------------------------- K1+K2 storage
+@pytest.mark.parametrize("dim,dtype,metric", [(128, "bf16", "cosine"), (768, "bf16", "cosine"), (1024, "bf16", "cosine"),
+                                              (1024, "f16", "cosine"), (1024, "f32", "cosine"), (100, "bf16", "cosine"),
+                                              (128, "bf16", "ip")])
+def test_store_bit_exact(native, dim, dtype, metric, golden_dir):
+    n = 4096 if dim >= 768 else 1000
+    idx = native.NativeIndex(dim, dtype, metric)
+    idx.add_synthetic(0, 0, n)
+    got = idx.get_rows(np.arange(n))
+    ref = _stored_as_f32(oracle.c_build_synthetic(0, 0, n, dim, dtype, metric), dtype)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    sha = json.load(open(os.path.join(golden_dir, "corpus_sha256.json")))
+    key = f"seed0_rows{n}_dim{dim}_{dtype}_{metric}"
+    if key in sha:
+        st = R.quantize(got, dtype)
+        assert hashlib.sha256(st.tobytes()).hexdigest() == sha[key]
+    # explicit fp32 rows go through the same K1+K2 path
+    idx2 = native.NativeIndex(dim, dtype, metric)
+    idx2.add(R.gen_rows(0, 0, n, dim))
+    np.testing.assert_array_equal(idx2.get_rows(np.arange(n)).view(np.uint32), ref.view(np.uint32))
+
+
+# ---------------------------------------------------------------- golden vectors
+def test_c1_golden(native, golden_dir):
+    d = np.load(os.path.join(golden_dir, "c1_retrieval.npz"))
+    meta = json.load(open(os.path.join(golden_dir, "c1_retrieval.json")))
+    idx = native.NativeIndex(128, "f32", "cosine")
+    idx.add(d["corpus"])
+    s, r = idx.search(d["queries"], 5)
+    for b, res in enumerate(meta["results"]["thr0"]):
+        assert [f"chunk_{x}" for x in r[b]] == [e["chunk_id"] for e in res]
+        np.testing.assert_allclose(s[b], [e["score"] for e in res], atol=SCORE_TOL, rtol=0)
+    allowed = np.array([m["group"] == "g1" for m in meta["metas"]])
+    s, r = idx.search(d["queries"], 5, oracle.mask_from_bool(allowed))
+    for b, res in enumerate(meta["results"]["filtered_g1"]):
+        assert [f"chunk_{x}" for x in r[b] if x >= 0] == [e["chunk_id"] for e in res]
+        np.testing.assert_allclose(s[b][: len(res)], [e["score"] for e in res], atol=SCORE_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_ties_golden(native, golden_dir, dtype):
+    d = np.load(os.path.join(golden_dir, "ties.npz"))
+    meta = json.load(open(os.path.join(golden_dir, "ties.json")))
+    corpus = R.gen_rows(7, 0, 20000, 256)
+    for s_, dst in zip(d["dup_src"], d["dup_dst"]):
+        corpus[dst] = corpus[s_]
+    idx = native.NativeIndex(256, dtype, "cosine")
+    idx.add(corpus)
+    s, r = idx.search(d["queries"], 10)
+    stored = R.process_rows(corpus, "cosine", dtype)
+    s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(d["queries"], "cosine"), 10)
+    _check(s, r, s_ref, r_ref)
+    if dtype == "f32":  # the golden vectors were produced on the fp32 store
+        for b, res in enumerate(meta["results"]):
+            assert [f"chunk_{x}" for x in r[b]] == [e["chunk_id"] for e in res]
+            np.testing.assert_allclose(s[b], [e["score"] for e in res], atol=SCORE_TOL, rtol=0)
+
+
+# ---------------------------------------------------------------- random sweeps vs the oracle
+CASES = [
+    (64, "bf16", 2000, 1, 10), (128, "bf16", 5000, 16, 5), (384, "bf16", 20000, 33, 10), (768, "bf16", 30000, 64, 10),
+    (1024, "bf16", 30000, 64, 32), (1024, "bf16", 7000, 100, 10), (768, "f16", 20000, 64, 10),
+    (1024, "f32", 20000, 48, 10), (200, "f32", 3000, 7, 3), (2048, "bf16", 5000, 40, 10), (96, "f16", 777, 5, 32),
+]
+
+
+@pytest.mark.parametrize("dim,dtype,n,B,k", CASES)
+def test_random_vs_oracle(native, dim, dtype, n, B, k):
+    rng = np.random.default_rng(dim * 7 + B)
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    idx.add_synthetic(3, 0, n)
+    raw = R.gen_rows(3, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+    s, r = idx.search(q, k)
+    stored = oracle.c_build_synthetic(3, 0, n, dim, dtype, "cosine")
+    s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, "cosine"), k)
+    _check(s, r, s_ref, r_ref)
+
+
+def test_ip_metric(native):
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((3000, 128)).astype(np.float32) * rng.uniform(0.1, 3.0, (3000, 1)).astype(np.float32)
+    q = rng.standard_normal((9, 128)).astype(np.float32)
+    idx = native.NativeIndex(128, "bf16", "ip")
+    idx.add(x)
+    s, r = idx.search(q, 10)
+    s_ref, r_ref = oracle.c_search(R.process_rows(x, "ip", "bf16"), "bf16", q, 10)
+    _check(s, r, s_ref, r_ref)
+
+
+def test_mask_remove_and_incremental_add(native):
+    rng = np.random.default_rng(11)
+    dim, n = 256, 9000
+    raw = R.gen_rows(5, 0, n, dim)
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw[:4000])
+    idx.add(raw[4000:7001])
+    idx.add(raw[7001:])
+    gone = rng.choice(n, 700, replace=False)
+    idx.remove(gone)
+    assert idx.size() == (n, n - 700)
+    allowed = rng.random(n) < 0.4
+    q = _planted_queries(raw, 20, rng)
+    s, r = idx.search(q, 10, oracle.mask_from_bool(allowed))
+    eff = allowed.copy()
+    eff[gone] = False
+    stored = R.process_rows(raw, "cosine", "bf16")
+    s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10, oracle.mask_from_bool(eff))
+    _check(s, r, s_ref, r_ref)
+
+
+def test_empty_small_and_ragged(native):
+    idx = native.NativeIndex(64, "bf16", "cosine")
+    q = np.ones((2, 64), np.float32)
+    s, r = idx.search(q, 5)
+    assert (r == -1).all() and np.isneginf(s).all()
+    raw = R.gen_rows(1, 0, 3, 64)
+    idx.add(raw)
+    s, r = idx.search(q, 5)
+    s_ref, r_ref = oracle.c_search(R.process_rows(raw, "cosine", "bf16"), "bf16", R.process_queries(q, "cosine"), 5)
+    _check(s, r, s_ref, r_ref)
+    assert (r[:, 3:] == -1).all()
+    idx.remove([0, 1, 2])
+    s, r = idx.search(q, 5)
+    assert (r == -1).all()
+    with pytest.raises(ValueError):
+        idx.search(q, 33)
+    with pytest.raises(ValueError):
+        idx.search(np.ones((1, 63), np.float32), 5)
+
+
+def test_massive_ties_use_exact_fallback(native):
+    """100 identical rows (> kc = 32 candidates): the guard fails and the collect pass
+    must return the 10 lowest duplicate rows."""
+    dim, n = 128, 5000
+    raw = R.gen_rows(9, 0, n, dim)
+    dups = np.sort(np.random.default_rng(2).choice(n, 100, replace=False))
+    raw[dups] = raw[dups[0]]
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    q = raw[dups[:1]].copy()
+    s, r = idx.search(q, 10)
+    s_ref, r_ref = oracle.c_search(R.process_rows(raw, "cosine", "bf16"), "bf16", R.process_queries(q, "cosine"), 10)
+    _check(s, r, s_ref, r_ref)
+    np.testing.assert_array_equal(r[0], dups[:10])
+
+
+def test_save_load_roundtrip(native, tmp_path):
+    raw = R.gen_rows(4, 0, 1500, 192)
+    idx = native.NativeIndex(192, "f16", "cosine")
+    idx.add(raw)
+    idx.remove([3, 77])
+    p = str(tmp_path / "x.hri")
+    idx.save(p)
+    idx2 = native.NativeIndex.load(p, dim=192, dtype="f16", metric="cosine")
+    assert idx2.size() == (1500, 1498)
+    q = raw[:4] + 0.01
+    np.testing.assert_array_equal(idx.search(q, 8)[1], idx2.search(q, 8)[1])
+
+
+# ---------------------------------------------------------------- device + shard paths
+def test_device_and_sharded_merge(native):
+    torch = pytest.importorskip("torch")
+    dim, n, B, k, kc = 512, 12000, 24, 10, 32
+    raw = R.gen_rows(8, 0, n, dim)
+    full = native.NativeIndex(dim, "bf16", "cosine")
+    full.add(raw)
+    rng = np.random.default_rng(3)
+    q = _planted_queries(raw, B, rng)
+    s_host, r_host = full.search(q, k)
+    qd = torch.from_numpy(q).cuda()
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    rd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    full.search_device(qd.data_ptr(), B, k, sd.data_ptr(), rd.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rd.cpu().numpy(), r_host)
+    np.testing.assert_array_equal(sd.cpu().numpy(), s_host)
+    # two row shards + device merge == one index
+    cut = 5003
+    shards = [native.NativeIndex(dim, "bf16", "cosine") for _ in range(2)]
+    shards[0].add(raw[:cut])
+    shards[1].add(raw[cut:])
+    cand = torch.empty((2, B, kc, 2), dtype=torch.float64, device="cuda")
+    bounds = torch.empty((2, B), dtype=torch.float64, device="cuda")
+    for g, (sh, off) in enumerate(zip(shards, [0, cut])):
+        sh.search_shard(qd.data_ptr(), B, k, kc, off, cand[g].data_ptr(), bounds[g].data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    kth = torch.empty(B, dtype=torch.float64, device="cuda")
+    fail = torch.empty(B, dtype=torch.int32, device="cuda")
+    native.merge_candidates(0, cand.data_ptr(), bounds.data_ptr(), 2, B, kc, k, sd.data_ptr(), rd.data_ptr(),
+                            kth.data_ptr(), fail.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert fail.sum().item() == 0
+    np.testing.assert_array_equal(rd.cpu().numpy(), r_host)
+    np.testing.assert_array_equal(sd.cpu().numpy(), s_host)
+
+
+def test_pool_normalize_matches_torch(native):
+    torch = pytest.importorskip("torch")
+    B, T, H, n_instr = 5, 37, 768, 6
+    g = torch.Generator().manual_seed(0)
+    hidden = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    mask = torch.ones(B, T, dtype=torch.int32)
+    mask[1, 20:] = 0
+    mask[3, 9:] = 0
+    ref_mask = mask.clone()
+    ref_mask[:, :n_instr] = 0
+    s = torch.sum(hidden.float() * ref_mask.unsqueeze(-1).float(), dim=1)
+    d = ref_mask.sum(dim=1, keepdim=True).float()
+    ref = torch.nn.functional.normalize(s / d, dim=-1)
+    hd, md = hidden.cuda(), mask.cuda()
+    out = torch.empty(B, H, device="cuda")
+    native.pool_normalize(hd.data_ptr(), "bf16", md.data_ptr(), B, T, H, n_instr, out.data_ptr(),
+                          stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-5, rtol=1e-5)
+
+
+# ---------------------------------------------------------------- guard rigor
+@pytest.mark.parametrize("dim,dtype,B", [(128, "bf16", 16), (200, "f32", 7), (1024, "f32", 48), (1024, "bf16", 64),
+                                         (768, "f16", 40)])
+def test_approx_error_within_guard_bound(native, dim, dtype, B):
+    """Every row's approximate MFMA score lies within E_q of its exact canonical score --
+    the premise of the exactness guard (DESIGN.md "Exactness guard")."""
+    n = 3000
+    rng = np.random.default_rng(dim + B)
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    idx.add_synthetic(3, 0, n)
+    raw = R.gen_rows(3, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+    approx, E = idx.debug_approx(q)
+    stored = oracle.c_build_synthetic(3, 0, n, dim, dtype, "cosine")
+    exact = R.exact_scores(stored, dtype, R.process_queries(q, "cosine"))
+    err = np.abs(approx.astype(np.float64) - exact).max(axis=1)
+    print(f"{dim}/{dtype}: max |approx-exact| = {err.max():.3e}, min E = {E.min():.3e}")
+    assert np.all(err <= E), (err, E)

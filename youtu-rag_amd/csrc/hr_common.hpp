@@ -1,0 +1,102 @@
+// hr_common.hpp -- types and bit-exact scalar helpers shared by the hiprag kernels.
+// The conversion and generator recipes are identical to oracle/hr_oracle.c (the checker).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hr {
+
+enum { F32 = 0, BF16 = 1, F16 = 2 };
+enum { COSINE = 0, IP = 1, L2 = 2 };
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Cand {  // exact candidate record exchanged between shards (16 B)
+    double score;
+    int64_t row;
+};
+
+// ---------------------------------------------------------------- scalar helpers
+__device__ __host__ inline uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __host__ inline float bf16_to_f32(uint16_t h) { return __builtin_bit_cast(float, (uint32_t)h << 16); }
+
+__device__ __host__ inline uint16_t f32_to_f16_rne(float f) {  // same bit recipe as oracle hro_f32_to_f16
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    uint32_t sign = (u >> 16) & 0x8000u;
+    uint32_t a = u & 0x7FFFFFFFu;
+    if (a >= 0x7F800000u) return (uint16_t)(sign | 0x7C00u | (a > 0x7F800000u ? 0x200u : 0u));
+    if (a >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);
+    if (a < 0x38800000u) {
+        int e = (int)(a >> 23);
+        if (e < 102) return (uint16_t)sign;
+        uint32_t m = (a & 0x7FFFFFu) | 0x800000u;
+        int shift = 126 - e;
+        uint32_t q = m >> shift;
+        uint32_t rem = m & ((1u << shift) - 1u);
+        uint32_t half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (q & 1u))) q++;
+        return (uint16_t)(sign | q);
+    }
+    uint32_t r = a - 0x38000000u;
+    r += 0xFFFu + ((r >> 13) & 1u);
+    return (uint16_t)(sign | (r >> 13));
+}
+__device__ __host__ inline float f16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+template <int MT>
+__device__ inline uint16_t quant_mt(float f) {
+    return MT == BF16 ? f32_to_bf16_rne(f) : f32_to_f16_rne(f);
+}
+template <int MT>
+__device__ inline float dequant_mt(uint16_t h) {
+    return MT == BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+
+// order-preserving float <-> uint32 key (larger key = larger float)
+__device__ __host__ inline uint32_t f2key(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __host__ inline float key2f(uint32_t k) {
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return __builtin_bit_cast(float, u);
+}
+#define HR_KEY_NEG_INF 0x007FFFFFu  // f2key(-inf)
+
+__device__ __host__ inline uint64_t d2key(double d) {
+    uint64_t u = __builtin_bit_cast(uint64_t, d);
+    return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ inline float gen_elem(uint64_t seed, int64_t row, int dim, int d) {
+    uint64_t z = mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)row * (uint64_t)dim + (uint64_t)d);
+    int64_t v = (int64_t)(z & 0xFFFF) + (int64_t)((z >> 16) & 0xFFFF) + (int64_t)((z >> 32) & 0xFFFF) +
+                (int64_t)(z >> 48) - 131070;
+    return (float)v;
+}
+
+__device__ inline double wave_butterfly_sum(double p) {  // canonical: p[i] + p[i ^ off], off = 32..1
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        double o = __shfl_xor(p, off, 64);
+        int lane = threadIdx.x & 63;
+        p = (lane & off) ? (o + p) : (p + o);  // keep p[i] + p[i+off] operand order for i < off
+    }
+    return p;
+}
+
+}  // namespace hr

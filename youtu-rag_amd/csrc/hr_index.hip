@@ -1,0 +1,834 @@
+// hr_index.hip -- host side of libhiprag.so: index handles, launch plumbing, C ABI.
+// Declarations and the reference call each entry replaces: include/hiprag.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hiprag.h"
+#include "hr_kernels.hpp"
+
+using namespace hr;
+
+// ---------------------------------------------------------------- errors
+static thread_local std::string g_err;
+static int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_err(HR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// ---------------------------------------------------------------- device buffers
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+static constexpr int kCap = 8192;       // candidate buffer per query (scan FILTER mode)
+static constexpr int kScanThreads = 512;
+
+struct hr_index {
+    int dim = 0, dpad = 0, S = 0, dtype = BF16, metric = COSINE, device = 0;
+    int64_t n = 0, cap = 0, n_live = 0;
+    double max_norm2 = 0.0;
+    uint8_t* rows = nullptr;        // tiled corpus
+    uint32_t* live = nullptr;       // one word per tile
+    std::vector<uint32_t> live_host;
+    unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    float last_sample_ms = 0.f, last_filter_ms = 0.f;
+    int n_cu = 256;
+    std::mutex mu;
+    // search workspace
+    DevBuf q_in, q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, cand, bound,
+        kth, fail, fb_cand, fb_bound, stage;
+    std::vector<float> floor_host;
+};
+
+static size_t tile_bytes(const hr_index* h) { return (size_t)h->S * (h->dtype == F32 ? 2048 : 1024); }
+
+static int set_device(hr_index* h) {
+    HIP_TRY(hipSetDevice(h->device));
+    return HR_OK;
+}
+
+// ---------------------------------------------------------------- dispatch helpers
+template <class F>
+static int dispatch_dt(int dt, F&& f) {
+    switch (dt) {
+        case F32: return f(std::integral_constant<int, F32>{});
+        case BF16: return f(std::integral_constant<int, BF16>{});
+        case F16: return f(std::integral_constant<int, F16>{});
+    }
+    return set_err(HR_E_INVALID, "unknown dtype");
+}
+
+// MFMA operand type: f16 corpora use the f16 MFMA, bf16 and fp32 corpora the bf16 one
+static int mfma_type(int dtype) { return dtype == F16 ? F16 : BF16; }
+
+// ---------------------------------------------------------------- create / grow
+extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
+    if (!out) return set_err(HR_E_INVALID, "out is null");
+    *out = nullptr;
+    if (dim <= 0 || dim > 4096) return set_err(HR_E_INVALID, "dim must be in [1, 4096]");
+    if (dtype < F32 || dtype > F16) return set_err(HR_E_INVALID, "dtype must be HR_F32, HR_BF16 or HR_F16");
+    if (metric == L2) return set_err(HR_E_UNSUPPORTED, "metric 'euclidean' (L2) is not implemented on the HIP path yet");
+    if (metric != COSINE && metric != IP) return set_err(HR_E_INVALID, "unknown metric");
+    if (n_dev != 1) return set_err(HR_E_UNSUPPORTED, "one device per handle (shard across processes for multi-GPU)");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    int dev = dev_ids ? dev_ids[0] : 0;
+    if (dev < 0 || dev >= ndev) return set_err(HR_E_INVALID, "device id out of range");
+    hr_index* h = new hr_index();
+    h->dim = dim;
+    h->dpad = (dim + 63) / 64 * 64;
+    h->S = h->dpad / 16;
+    h->dtype = dtype;
+    h->metric = metric;
+    h->device = dev;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
+    if (e == hipSuccess) e = hipMalloc(&h->norm_bits, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(h->norm_bits, 0, sizeof(unsigned long long));
+    hipDeviceProp_t prop;
+    if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) {
+        hr_index_destroy(h);
+        return set_err(HR_E_HIP, std::string("hr_index_create: ") + hipGetErrorString(e));
+    }
+    h->n_cu = prop.multiProcessorCount;
+    *out = h;
+    return HR_OK;
+}
+
+static int grow(hr_index* h, int64_t need_rows) {
+    if (need_rows <= h->cap) return HR_OK;
+    int64_t new_cap = std::max<int64_t>({need_rows, h->cap + h->cap / 2, 1024});
+    new_cap = (new_cap + 31) / 32 * 32;
+    const size_t tb = tile_bytes(h);
+    uint8_t* nr = nullptr;
+    uint32_t* nl = nullptr;
+    HIP_TRY(hipMalloc(&nr, (size_t)(new_cap / 32) * tb));
+    HIP_TRY(hipMemsetAsync(nr, 0, (size_t)(new_cap / 32) * tb, h->stream));
+    HIP_TRY(hipMalloc(&nl, (size_t)(new_cap / 32) * 4));
+    HIP_TRY(hipMemsetAsync(nl, 0, (size_t)(new_cap / 32) * 4, h->stream));
+    if (h->rows) {
+        HIP_TRY(hipMemcpyAsync(nr, h->rows, (size_t)(h->cap / 32) * tb, hipMemcpyDeviceToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(nl, h->live, (size_t)(h->cap / 32) * 4, hipMemcpyDeviceToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipFree(h->rows));
+        HIP_TRY(hipFree(h->live));
+    }
+    h->rows = nr;
+    h->live = nl;
+    h->cap = new_cap;
+    h->live_host.resize((size_t)(new_cap / 32), 0u);
+    return HR_OK;
+}
+
+extern "C" int hr_index_reserve(hr_index* h, int64_t capacity_rows) {
+    if (!h || capacity_rows < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    return grow(h, capacity_rows);
+}
+
+static int mark_live(hr_index* h, int64_t r0, int64_t n) {
+    if (n <= 0) return HR_OK;
+    for (int64_t r = r0; r < r0 + n; ++r) h->live_host[(size_t)(r >> 5)] |= 1u << (r & 31);
+    const int64_t w0 = r0 >> 5, w1 = (r0 + n - 1) >> 5;
+    HIP_TRY(hipMemcpyAsync(h->live + w0, h->live_host.data() + w0, (size_t)(w1 - w0 + 1) * 4, hipMemcpyHostToDevice,
+                           h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // live_host may be modified again by the caller's next call
+    h->n_live += n;
+    return HR_OK;
+}
+
+static int finish_add(hr_index* h) {
+    unsigned long long bits = 0;
+    HIP_TRY(hipMemcpyAsync(&bits, h->norm_bits, sizeof(bits), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    double v;
+    std::memcpy(&v, &bits, 8);
+    h->max_norm2 = std::max(h->max_norm2, v);
+    return HR_OK;
+}
+
+template <bool SYNTH>
+static int add_impl(hr_index* h, const float* rows_host, uint64_t seed, int64_t grow0, int64_t n, int64_t* first) {
+    if (int rc = set_device(h)) return rc;
+    if (int rc = grow(h, h->n + n)) return rc;
+    const int64_t r0 = h->n;
+    const int64_t chunk = SYNTH ? (int64_t)1 << 22 : std::max<int64_t>(1, ((int64_t)64 << 20) / (4 * h->dim));
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t m = std::min(chunk, n - off);
+        const float* src = nullptr;
+        if (!SYNTH) {
+            HIP_TRY(h->stage.ensure((size_t)m * h->dim * 4));
+            HIP_TRY(hipMemcpyAsync(h->stage.p, rows_host + off * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice,
+                                   h->stream));
+            src = h->stage.as<float>();
+        }
+        const dim3 grid((unsigned)((m + 3) / 4));
+        int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+            hipLaunchKernelGGL((k_store<decltype(dt)::value, SYNTH>), grid, dim3(256), 0, h->stream, src, seed,
+                               grow0 + off, m, h->dim, h->S, h->metric, r0 + off, h->rows, h->norm_bits);
+            HIP_TRY(hipGetLastError());
+            return HR_OK;
+        });
+        if (rc) return rc;
+    }
+    h->n = r0 + n;
+    if (int rc = mark_live(h, r0, n)) return rc;
+    if (int rc = finish_add(h)) return rc;
+    if (first) *first = r0;
+    return HR_OK;
+}
+
+extern "C" int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* first_row_out) {
+    if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (n == 0) {
+        if (first_row_out) *first_row_out = h->n;
+        return HR_OK;
+    }
+    return add_impl<false>(h, rows, 0, 0, n, first_row_out);
+}
+
+extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global_row0, int64_t n,
+                                      int64_t* first_row_out) {
+    if (!h || n < 0 || global_row0 < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (n == 0) {
+        if (first_row_out) *first_row_out = h->n;
+        return HR_OK;
+    }
+    return add_impl<true>(h, nullptr, seed, global_row0, n, first_row_out);
+}
+
+extern "C" int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n) {
+    if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    int64_t lo = INT64_MAX, hi = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = rows[i];
+        if (r < 0 || r >= h->n) return set_err(HR_E_INVALID, "row out of range");
+        uint32_t& w = h->live_host[(size_t)(r >> 5)];
+        const uint32_t bit = 1u << (r & 31);
+        if (w & bit) {
+            w &= ~bit;
+            h->n_live--;
+        }
+        lo = std::min(lo, r >> 5);
+        hi = std::max(hi, r >> 5);
+    }
+    if (hi >= 0) {
+        HIP_TRY(hipMemcpyAsync(h->live + lo, h->live_host.data() + lo, (size_t)(hi - lo + 1) * 4,
+                               hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return HR_OK;
+}
+
+extern "C" int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (n_out) *n_out = h->n;
+    if (n_live_out) *n_live_out = h->n_live;
+    return HR_OK;
+}
+
+// ---------------------------------------------------------------- search pieces
+struct Plan {
+    int QB, Bp, P;
+};
+
+static int scan_lds_bytes(const hr_index* h, int QB) { return h->S * QB * 1024; }
+
+static int make_plan(const hr_index* h, int B, Plan* p) {
+    const int QB = (B > 32 && scan_lds_bytes(h, 2) <= 160 * 1024) ? 2 : 1;
+    if (scan_lds_bytes(h, QB) > 160 * 1024)
+        return set_err(HR_E_UNSUPPORTED, "dim too large for the LDS-resident query tile (max 2560)");
+    p->QB = QB;
+    p->Bp = QB * 32;
+    // ring depth: deepest prefetch that compiles without spills (see `make resource`)
+    const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : (QB == 2 ? 8 : 16);
+    p->P = (h->S % 16 == 0 && pmax >= 16) ? 16 : (h->S % 8 == 0 && pmax >= 8 ? 8 : 4);
+    return HR_OK;
+}
+
+template <int MT, int DT, int QB, int P, bool FILTER>
+static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds) {
+    auto kern = k_scan<MT, DT, QB, P, FILTER>;
+    static std::mutex attr_mu;
+    static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
+    static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown)
+    const int dev = h->device & 63;
+    const int bucket = lds <= 40 * 1024 ? 0 : lds <= 80 * 1024 ? 1 : lds <= 120 * 1024 ? 2 : 3;
+    int per_cu;
+    {
+        std::lock_guard<std::mutex> lk(attr_mu);
+        if (attr_lds[dev] < 160 * 1024) {
+            HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr_lds[dev] = 160 * 1024;
+        }
+        if (!occ[dev][bucket]) {
+            int o = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kScanThreads, lds));
+            occ[dev][bucket] = std::max(1, o);
+        }
+        per_cu = occ[dev][bucket];
+    }
+    int64_t waves_needed = a.n_units;
+    int64_t blocks = std::min<int64_t>((int64_t)h->n_cu * per_cu, (waves_needed + 7) / 8);
+    blocks = std::max<int64_t>(blocks, 1);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kScanThreads), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    return HR_OK;
+}
+
+template <int MT, int DT, bool FILTER>
+static int launch_scan_p(hr_index* h, const Plan& pl, const ScanArgs& a, hipStream_t st) {
+    const int lds = scan_lds_bytes(h, pl.QB);
+#define HR_SCAN_CASE(QBv, Pv) \
+    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, FILTER>(h, a, st, lds);
+    if constexpr (DT == F32) {
+        HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
+    } else {
+        HR_SCAN_CASE(1, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(2, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
+    }
+#undef HR_SCAN_CASE
+    return set_err(HR_E_INVALID, "no scan variant for this plan");
+}
+
+static int launch_scan(hr_index* h, const Plan& pl, const ScanArgs& a, bool filter, hipStream_t st) {
+    return dispatch_dt(h->dtype, [&](auto dt) -> int {
+        constexpr int DT = decltype(dt)::value;
+        constexpr int MT = DT == F16 ? F16 : BF16;
+        return filter ? launch_scan_p<MT, DT, true>(h, pl, a, st) : launch_scan_p<MT, DT, false>(h, pl, a, st);
+    });
+}
+
+// error-bound constants for the approximate (MFMA) scores, see DESIGN.md "Exactness guard"
+static double acc_gamma(const hr_index* h) { return (double)(h->dpad + 64) * std::ldexp(1.0, -23); }
+static double storage_u(const hr_index* h) {
+    if (h->dtype != F32) return 0.0;
+    return mfma_type(h->dtype) == BF16 ? std::ldexp(1.0, -8) : std::ldexp(1.0, -11);
+}
+
+// One chunk of <= Bp queries on this shard.  mode 0: top-kc via SAMPLE+FILTER(groups);
+// mode 1: collect every row with approx >= floor (exact fallback).
+static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
+                       const double* kth_dev_host /* mode 1: host array of kth, B */, int mode, int cap_out,
+                       Cand* cand_out, double* bound_out, hipStream_t st) {
+    Plan pl;
+    if (int rc = make_plan(h, B, &pl)) return rc;
+    const int Bp = pl.Bp;
+    HIP_TRY(h->q32.ensure((size_t)Bp * h->dpad * 4));
+    HIP_TRY(h->qfrag.ensure((size_t)h->S * pl.QB * 1024));
+    HIP_TRY(h->qerr.ensure((size_t)Bp * 2 * 8));
+    HIP_TRY(h->mkeys.ensure((size_t)Bp * 32 * 4));
+    HIP_TRY(h->floor_q.ensure((size_t)Bp * 4));
+    HIP_TRY(h->cnt.ensure((size_t)Bp * 4));
+    HIP_TRY(h->buf.ensure((size_t)Bp * kCap * 8));
+    HIP_TRY(h->sel_rows.ensure((size_t)Bp * std::max(kc, cap_out) * 4));
+    HIP_TRY(h->sel_cnt.ensure((size_t)Bp * 4));
+    HIP_TRY(h->bound_approx.ensure((size_t)Bp * 4));
+    HIP_TRY(h->overflow.ensure((size_t)Bp * 4));
+
+    const int MT = mfma_type(h->dtype);
+    if (MT == BF16)
+        hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad,
+                           h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+    else
+        hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
+                           pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+    HIP_TRY(hipGetLastError());
+
+    // floors: padded queries never collect; mode 1 uses kth - E (computed on the host from qerr)
+    h->floor_host.assign((size_t)Bp, -INFINITY);
+    for (int b = B; b < Bp; ++b) h->floor_host[(size_t)b] = INFINITY;
+    const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
+    if (mode == 1) {
+        std::vector<double> qerr((size_t)Bp * 2);
+        HIP_TRY(hipMemcpyAsync(qerr.data(), h->qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int b = 0; b < B; ++b) {
+            const double kth = kth_dev_host[b];
+            if (std::isnan(kth)) {
+                h->floor_host[(size_t)b] = INFINITY;  // query not in the fallback
+                continue;
+            }
+            const double E = max_norm * (qerr[2 * b] * (1.0 + 1e-6) + (acc_gamma(h) + storage_u(h)) * qerr[2 * b + 1]) + 1e-9;
+            float f = (float)(kth - E);
+            if ((double)f > kth - E) f = std::nextafter(f, -INFINITY);
+            h->floor_host[(size_t)b] = f;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(h->floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(h->mkeys.p, 0, (size_t)Bp * 32 * 4, st));
+    HIP_TRY(hipMemsetAsync(h->cnt.p, 0, (size_t)Bp * 4, st));
+
+    const int64_t n_tiles = (h->n + 31) / 32;
+    ScanArgs a{};
+    a.rows = h->rows;
+    a.live = h->live;
+    a.mask = (const uint32_t*)mask_dev;
+    a.qfrag = h->qfrag.as<uint16_t>();
+    a.S = h->S;
+    a.mkeys = h->mkeys.as<uint32_t>();
+    a.floor_q = h->floor_q.as<float>();
+    a.cnt = h->cnt.as<uint32_t>();
+    a.buf = h->buf.as<float2>();
+    a.cap = kCap;
+    a.refresh_every = 4;
+    const bool groups = mode == 0;
+    a.use_groups = groups ? 1 : 0;
+    h->last_sample_ms = 0.f;
+    if (n_tiles > 0) {
+        if (groups) {
+            const int64_t target = std::max<int64_t>(512, n_tiles / 64);
+            a.sample_stride = std::max<int64_t>(1, n_tiles / target);
+            a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
+            HIP_TRY(hipEventRecord(h->ev[0], st));
+            if (int rc = launch_scan(h, pl, a, false, st)) return rc;
+            HIP_TRY(hipEventRecord(h->ev[1], st));
+        }
+        a.sample_stride = 1;
+        a.n_units = n_tiles;
+        HIP_TRY(hipEventRecord(h->ev[2], st));
+        if (int rc = launch_scan(h, pl, a, true, st)) return rc;
+        HIP_TRY(hipEventRecord(h->ev[3], st));
+    }
+    // select
+    const int kc_sel = mode == 0 ? kc : cap_out;
+    const int sort_cap = kCap;  // power of two
+    HIP_TRY(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, sort_cap * 8));
+    hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8, st, h->cnt.as<uint32_t>(), h->buf.as<float2>(),
+                       kCap, h->mkeys.as<uint32_t>(), h->floor_q.as<float>(), a.use_groups, B, kc_sel,
+                       h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), h->bound_approx.as<float>(),
+                       h->overflow.as<int>());
+    HIP_TRY(hipGetLastError());
+    // rescore
+    const int64_t nw = (int64_t)B * kc_sel;
+    int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+        hipLaunchKernelGGL((k_rescore<decltype(dt)::value>), dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st, h->rows,
+                           h->S, h->dpad, h->q32.as<float>(), h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), B,
+                           kc_sel, row_offset, h->bound_approx.as<float>(), h->qerr.as<double>(), max_norm,
+                           acc_gamma(h), storage_u(h), h->overflow.as<int>(), cand_out, bound_out);
+        HIP_TRY(hipGetLastError());
+        return HR_OK;
+    });
+    if (rc) return rc;
+    if (mode == 1) {
+        // collect mode is complete unless the candidate buffer overflowed: bound = -inf, or +inf on overflow
+        std::vector<int> ovf((size_t)B), selc((size_t)B);
+        HIP_TRY(hipMemcpyAsync(ovf.data(), h->overflow.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(selc.data(), h->sel_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<double> bh((size_t)B);
+        for (int b = 0; b < B; ++b) {
+            bool full = ovf[(size_t)b] || selc[(size_t)b] >= cap_out;
+            bh[(size_t)b] = full ? INFINITY : -INFINITY;
+        }
+        HIP_TRY(hipMemcpyAsync(bound_out, bh.data(), (size_t)B * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return HR_OK;
+}
+
+static int shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
+                        Cand* cand_out, double* bound_out, hipStream_t st) {
+    Plan pl;
+    if (int rc = make_plan(h, B, &pl)) return rc;
+    for (int b0 = 0; b0 < B; b0 += pl.Bp) {
+        const int bc = std::min(pl.Bp, B - b0);
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, kc, mask_dev, row_offset, nullptr, 0, 0,
+                                 cand_out + (int64_t)b0 * kc, bound_out + b0, st))
+            return rc;
+    }
+    return HR_OK;
+}
+
+static int validate_search(hr_index* h, int B, int k) {
+    if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
+    if (k <= 0 || k > HR_MAX_K) return set_err(HR_E_INVALID, "k must be in [1, 32]");
+    return HR_OK;
+}
+
+static int launch_merge(int device, const Cand* cand, const double* bounds, int G, int B, int kc, int k, float* s_out,
+                        int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st) {
+    int p2 = 1;
+    while (p2 < G * kc) p2 <<= 1;
+    const int lds = p2 * 16;
+    if (lds > 160 * 1024) return set_err(HR_E_INVALID, "too many candidates to merge");
+    HIP_TRY(hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(k_merge, dim3(B), dim3(256), lds, st, cand, bounds, G, B, kc, k, s_out, r_out, kth_out,
+                       fail_out);
+    HIP_TRY(hipGetLastError());
+    return HR_OK;
+}
+
+static constexpr int kFallbackCap = 512;
+
+// full single-shard search on device-resident queries, with the exact fallback
+static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
+                              int64_t* r_out, hipStream_t st) {
+    if (int rc = validate_search(h, B, k)) return rc;
+    const int kc = HR_MAX_K;
+    HIP_TRY(h->cand.ensure((size_t)B * kc * sizeof(Cand)));
+    HIP_TRY(h->bound.ensure((size_t)B * 8));
+    HIP_TRY(h->kth.ensure((size_t)B * 8));
+    HIP_TRY(h->fail.ensure((size_t)B * 4));
+    if (int rc = shard_search(h, q_dev, B, kc, mask_dev, 0, h->cand.as<Cand>(), h->bound.as<double>(), st)) return rc;
+    if (int rc = launch_merge(h->device, h->cand.as<Cand>(), h->bound.as<double>(), 1, B, kc, k, s_out, r_out,
+                              h->kth.as<double>(), h->fail.as<int32_t>(), st))
+        return rc;
+    std::vector<int32_t> fail((size_t)B);
+    std::vector<double> kth((size_t)B);
+    HIP_TRY(hipMemcpyAsync(fail.data(), h->fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(kth.data(), h->kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[(size_t)b]) failed.push_back(b);
+    if (failed.empty()) return HR_OK;
+    // exact fallback: re-scan the failing queries collecting every row with approx >= kth - E
+    for (int b : failed) {
+        const int kc2 = kFallbackCap;
+        HIP_TRY(h->fb_cand.ensure((size_t)kc2 * sizeof(Cand)));
+        HIP_TRY(h->fb_bound.ensure(64));
+        double kb = kth[(size_t)b];
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, kc2, mask_dev, 0, &kb, 1, kc2,
+                                 h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), st))
+            return rc;
+        double bd = 0;
+        HIP_TRY(hipMemcpyAsync(&bd, h->fb_bound.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (bd > 0) return set_err(HR_E_OVERFLOW, "exact fallback overflowed its candidate buffer (massive ties?)");
+        if (int rc = launch_merge(h->device, h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), 1, 1, kc2, k,
+                                  s_out + (int64_t)b * k, r_out + (int64_t)b * k, h->kth.as<double>() + b,
+                                  h->fail.as<int32_t>() + b, st))
+            return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return HR_OK;
+}
+
+extern "C" int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const uint64_t* row_mask_dev,
+                                      float* scores_out_dev, int64_t* rows_out_dev, void* stream) {
+    if (!h || !q_dev || !scores_out_dev || !rows_out_dev) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
+    return search_device_impl(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
+}
+
+extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
+                               int64_t* rows_out) {
+    if (!h || !q || !scores_out || !rows_out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    if (int rc = validate_search(h, B, k)) return rc;
+    hipStream_t st = h->stream;
+    if (h->n_live == 0) {  // empty index: reference returns [] (faiss_store.py:143-144)
+        for (int64_t i = 0; i < (int64_t)B * k; ++i) {
+            scores_out[i] = -INFINITY;
+            rows_out[i] = -1;
+        }
+        return HR_OK;
+    }
+    HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
+    DevBuf& so = h->stage;
+    const size_t words = (size_t)((h->n + 63) / 64);
+    HIP_TRY(so.ensure((size_t)B * k * 12 + (row_mask ? words * 8 : 0)));
+    float* s_dev = (float*)so.p;
+    int64_t* r_dev = (int64_t*)((uint8_t*)so.p + (size_t)B * k * 4);
+    uint64_t* m_dev = row_mask ? (uint64_t*)((uint8_t*)so.p + (size_t)B * k * 12) : nullptr;
+    if (m_dev && ((uintptr_t)m_dev & 7)) return set_err(HR_E_INVALID, "internal alignment");
+    HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
+    if (row_mask) HIP_TRY(hipMemcpyAsync(m_dev, row_mask, words * 8, hipMemcpyHostToDevice, st));
+    if (int rc = search_device_impl(h, h->q_in.as<float>(), B, k, m_dev, s_dev, r_dev, st)) return rc;
+    HIP_TRY(hipMemcpyAsync(scores_out, s_dev, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(rows_out, r_dev, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return HR_OK;
+}
+
+extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc,
+                                     const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                     double* bound_out_dev, void* stream) {
+    if (!h || !q_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    if (int rc = validate_search(h, B, k)) return rc;
+    if (kc < k || kc > HR_MAX_K) return set_err(HR_E_INVALID, "kc must be in [k, 32]");
+    hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
+    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st);
+}
+
+extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev, int cap,
+                                             const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                             double* bound_out_dev, void* stream) {
+    if (!h || !q_dev || !kth_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
+    if (B <= 0 || cap <= 0 || cap > 2048) return set_err(HR_E_INVALID, "B > 0 and cap in [1, 2048] required");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
+    std::vector<double> kth((size_t)B);
+    HIP_TRY(hipMemcpyAsync(kth.data(), kth_dev, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    Cand* out = (Cand*)cand_out_dev;
+    for (int b = 0; b < B; ++b) {
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, cap, row_mask_dev, row_offset, &kth[(size_t)b], 1,
+                                 cap, out + (int64_t)b * cap, bound_out_dev + b, st))
+            return rc;
+    }
+    return HR_OK;
+}
+
+extern "C" int hr_merge_candidates(int device, const void* cand_dev, const double* bounds_dev, int G, int B, int kc,
+                                   int k, float* scores_out_dev, int64_t* rows_out_dev, double* kth_out_dev,
+                                   int32_t* fail_out_dev, void* stream) {
+    if (!cand_dev || !bounds_dev || !scores_out_dev || !rows_out_dev || !kth_out_dev || !fail_out_dev)
+        return set_err(HR_E_INVALID, "null argument");
+    if (G <= 0 || B <= 0 || kc <= 0 || k <= 0 || k > kc) return set_err(HR_E_INVALID, "bad sizes");
+    HIP_TRY(hipSetDevice(device));
+    return launch_merge(device, (const Cand*)cand_dev, bounds_dev, G, B, kc, k, scores_out_dev, rows_out_dev,
+                        kth_out_dev, fail_out_dev, (hipStream_t)stream);
+}
+
+
+// diagnostics: approximate scores of every row (Bp×n) and the per-query bound E_q
+extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out) {
+    if (!h || !q || !approx_out || !e_out || B <= 0 || B > 64) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    Plan pl;
+    if (int rc = make_plan(h, B, &pl)) return rc;
+    hipStream_t st = h->stream;
+    const int Bp = pl.Bp;
+    const int64_t n_tiles = (h->n + 31) / 32;
+    HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
+    HIP_TRY(h->q32.ensure((size_t)Bp * h->dpad * 4));
+    HIP_TRY(h->qfrag.ensure((size_t)h->S * pl.QB * 1024));
+    HIP_TRY(h->qerr.ensure((size_t)Bp * 2 * 8));
+    HIP_TRY(h->stage.ensure((size_t)Bp * n_tiles * 32 * 4 + 16));
+    HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
+    const int MT = mfma_type(h->dtype);
+    if (MT == BF16)
+        hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
+                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+    else
+        hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
+                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+    HIP_TRY(hipGetLastError());
+    const int lds = scan_lds_bytes(h, pl.QB);
+    int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+        constexpr int DT = decltype(dt)::value;
+        constexpr int MTc = DT == F16 ? F16 : BF16;
+        auto k1 = k_debug_approx<MTc, DT, 1>;
+        auto k2 = k_debug_approx<MTc, DT, 2>;
+        auto kern = pl.QB == 1 ? k1 : k2;
+        HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), lds, st, h->rows,
+                           h->qfrag.as<uint16_t>(), h->S, n_tiles, h->stage.as<float>());
+        HIP_TRY(hipGetLastError());
+        return HR_OK;
+    });
+    if (rc) return rc;
+    std::vector<float> tmp((size_t)Bp * n_tiles * 32);
+    std::vector<double> qerr((size_t)Bp * 2);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), h->stage.p, tmp.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(qerr.data(), h->qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
+    for (int b = 0; b < B; ++b) {
+        std::memcpy(approx_out + (size_t)b * h->n, tmp.data() + (size_t)b * n_tiles * 32, (size_t)h->n * 4);
+        e_out[b] = max_norm * (qerr[2 * b] * (1.0 + 1e-6) + (acc_gamma(h) + storage_u(h)) * qerr[2 * b + 1]) + 1e-9;
+    }
+    return HR_OK;
+}
+
+extern "C" int hr_index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out) {
+    if (!h || n < 0 || (n > 0 && (!rows || !out))) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (n == 0) return HR_OK;
+    for (int64_t i = 0; i < n; ++i)
+        if (rows[i] < 0 || rows[i] >= h->n) return set_err(HR_E_INVALID, "row out of range");
+    if (int rc = set_device(h)) return rc;
+    HIP_TRY(h->stage.ensure((size_t)n * 8 + (size_t)n * h->dim * 4));
+    int64_t* idx = (int64_t*)h->stage.p;
+    float* o = (float*)((uint8_t*)h->stage.p + (size_t)n * 8);
+    HIP_TRY(hipMemcpyAsync(idx, rows, (size_t)n * 8, hipMemcpyHostToDevice, h->stream));
+    int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+        hipLaunchKernelGGL((k_gather<decltype(dt)::value>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream,
+                           h->rows, h->S, h->dim, idx, n, o);
+        HIP_TRY(hipGetLastError());
+        return HR_OK;
+    });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, o, (size_t)n * h->dim * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return HR_OK;
+}
+
+// ---------------------------------------------------------------- persistence
+struct FileHeader {
+    char magic[8];
+    int32_t version, dim, dtype, metric;
+    int64_t n, n_live;
+    double max_norm2;
+};
+
+extern "C" int hr_index_save(hr_index* h, const char* path) {
+    if (!h || !path) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return set_err(HR_E_IO, std::string("cannot open ") + path);
+    FileHeader hd{};
+    std::memcpy(hd.magic, "HIPRAG01", 8);
+    hd.version = 1;
+    hd.dim = h->dim;
+    hd.dtype = h->dtype;
+    hd.metric = h->metric;
+    hd.n = h->n;
+    hd.n_live = h->n_live;
+    hd.max_norm2 = h->max_norm2;
+    bool ok = std::fwrite(&hd, sizeof(hd), 1, f) == 1;
+    const int64_t tiles = (h->n + 31) / 32;
+    const size_t tb = tile_bytes(h);
+    std::vector<uint8_t> tmp;
+    const int64_t step = std::max<int64_t>(1, ((int64_t)256 << 20) / (int64_t)tb);
+    for (int64_t t = 0; ok && t < tiles; t += step) {
+        const int64_t m = std::min(step, tiles - t);
+        tmp.resize((size_t)m * tb);
+        if (hipMemcpy(tmp.data(), h->rows + (size_t)t * tb, (size_t)m * tb, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::fclose(f);
+            return set_err(HR_E_HIP, "save: device copy failed");
+        }
+        ok = std::fwrite(tmp.data(), 1, tmp.size(), f) == tmp.size();
+    }
+    if (ok && tiles > 0) ok = std::fwrite(h->live_host.data(), 4, (size_t)tiles, f) == (size_t)tiles;
+    std::fclose(f);
+    return ok ? HR_OK : set_err(HR_E_IO, std::string("write failed: ") + path);
+}
+
+extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr_index** out) {
+    if (!path || !out) return set_err(HR_E_INVALID, "bad arguments");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return set_err(HR_E_IO, std::string("cannot open ") + path);
+    FileHeader hd{};
+    if (std::fread(&hd, sizeof(hd), 1, f) != 1 || std::memcmp(hd.magic, "HIPRAG01", 8) != 0) {
+        std::fclose(f);
+        return set_err(HR_E_IO, "not a hiprag index file");
+    }
+    hr_index* h = nullptr;
+    if (int rc = hr_index_create(hd.dim, hd.dtype, hd.metric, n_dev, dev_ids, &h)) {
+        std::fclose(f);
+        return rc;
+    }
+    int rc = grow(h, hd.n);  // h is not yet visible to any other thread
+    const int64_t tiles = (hd.n + 31) / 32;
+    const size_t tb = tile_bytes(h);
+    std::vector<uint8_t> tmp;
+    const int64_t step = std::max<int64_t>(1, ((int64_t)256 << 20) / (int64_t)tb);
+    for (int64_t t = 0; rc == HR_OK && t < tiles; t += step) {
+        const int64_t m = std::min(step, tiles - t);
+        tmp.resize((size_t)m * tb);
+        if (std::fread(tmp.data(), 1, tmp.size(), f) != tmp.size()) rc = set_err(HR_E_IO, "truncated index file");
+        else if (hipMemcpy(h->rows + (size_t)t * tb, tmp.data(), tmp.size(), hipMemcpyHostToDevice) != hipSuccess)
+            rc = set_err(HR_E_HIP, "load: device copy failed");
+    }
+    if (rc == HR_OK && tiles > 0) {
+        if (std::fread(h->live_host.data(), 4, (size_t)tiles, f) != (size_t)tiles) rc = set_err(HR_E_IO, "truncated index file");
+        else if (hipMemcpy(h->live, h->live_host.data(), (size_t)tiles * 4, hipMemcpyHostToDevice) != hipSuccess)
+            rc = set_err(HR_E_HIP, "load: device copy failed");
+    }
+    std::fclose(f);
+    if (rc != HR_OK) {
+        hr_index_destroy(h);
+        return rc;
+    }
+    h->n = hd.n;
+    h->n_live = hd.n_live;
+    h->max_norm2 = hd.max_norm2;
+    unsigned long long bits;
+    std::memcpy(&bits, &hd.max_norm2, 8);
+    (void)hipMemcpy(h->norm_bits, &bits, 8, hipMemcpyHostToDevice);
+    *out = h;
+    return HR_OK;
+}
+
+extern "C" void hr_index_destroy(hr_index* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->rows) (void)hipFree(h->rows);
+    if (h->live) (void)hipFree(h->live);
+    if (h->norm_bits) (void)hipFree(h->norm_bits);
+    for (DevBuf* b : {&h->q_in, &h->q32, &h->qfrag, &h->qerr, &h->mkeys, &h->floor_q, &h->cnt, &h->buf, &h->sel_rows,
+                      &h->sel_cnt, &h->bound_approx, &h->overflow, &h->cand, &h->bound, &h->kth, &h->fail,
+                      &h->fb_cand, &h->fb_bound, &h->stage})
+        b->release();
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+extern "C" int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    HIP_TRY(hipEventSynchronize(h->ev[3]));
+    float a = 0.f, b = 0.f;
+    if (hipEventElapsedTime(&a, h->ev[0], h->ev[1]) != hipSuccess) a = 0.f;
+    HIP_TRY(hipEventElapsedTime(&b, h->ev[2], h->ev[3]));
+    if (sample_ms) *sample_ms = a;
+    if (filter_ms) *filter_ms = b;
+    return HR_OK;
+}
+
+extern "C" int hr_device_count(int* n_out) {
+    if (!n_out) return set_err(HR_E_INVALID, "null argument");
+    HIP_TRY(hipGetDeviceCount(n_out));
+    return HR_OK;
+}
+
+extern "C" const char* hr_last_error(void) { return g_err.c_str(); }
+extern "C" int hr_abi_version(void) { return 1; }

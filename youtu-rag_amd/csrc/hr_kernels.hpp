@@ -1,0 +1,619 @@
+// hr_kernels.hpp -- CDNA4 (gfx950) kernels of the hiprag vector index.
+//
+// Corpus layout in HBM ("MFMA-tiled"): rows are grouped in tiles of 32; a tile
+// is S = dpad/16 k-steps; k-step s of tile t is one 1 KiB block (2 KiB for an
+// fp32 corpus) holding, for lane l = r + 32h (r = row in tile, h = 0/1), the 8
+// elements k = 16s + 8h .. 16s + 8h + 7 of row r.  One wave-wide 16-byte load
+// of a k-step is therefore both perfectly coalesced (1 KiB contiguous) and
+// exactly the B operand of v_mfma_f32_32x32x16_{bf16,f16} for those 32 rows.
+// A wave streams its contiguous tile range as one linear byte stream.
+//
+// Kernels (SURVEY.md §2 kernel inventory):
+//   k_store      K1+K2  canonical L2-normalise (cosine) + RNE quantise, tiled write
+//   k_prep_q     K1     query normalise + quantise into A-fragment order, error terms
+//   k_scan       K3+K6  Q·Xᵀ on MFMA, live/mask predicate, group-max threshold,
+//                       ballot-compacted candidate append (SAMPLE / FILTER modes)
+//   k_select     K4     per-query candidate compaction + bitonic top-kc
+//   k_rescore    K5     exact canonical fp64 rescoring + shard error bound
+//   k_merge      K4/C1  (exact desc, row asc) merge over shards + exactness guard
+//   k_gather     get_by_id de-tiling
+#pragma once
+#include "hr_common.hpp"
+
+namespace hr {
+
+// byte offset of k-step chunk (tile, s) for lane l; stride 1 KiB (16-bit) / 2 KiB (fp32)
+template <int DT>
+__device__ __host__ inline size_t chunk_bytes() { return DT == F32 ? 2048 : 1024; }
+
+// element (row r, column d) of the tiled corpus, as float
+template <int DT>
+__device__ inline float load_elem(const uint8_t* base, int S, int64_t r, int d) {
+    int64_t chunk = (r >> 5) * S + (d >> 4);
+    int lane = (int)(r & 31) + 32 * ((d >> 3) & 1);
+    int j = d & 7;
+    if (DT == F32) {
+        const float* p = (const float*)(base + chunk * 2048 + (j >> 2) * 1024 + lane * 16);
+        return p[j & 3];
+    } else {
+        const uint16_t* p = (const uint16_t*)(base + chunk * 1024 + lane * 16);
+        return DT == BF16 ? bf16_to_f32(p[j]) : f16_to_f32(p[j]);
+    }
+}
+
+// ---------------------------------------------------------------- K1+K2: store rows
+// One wave per row.  Phase 1: canonical fp64 norm² (lane-strided + butterfly, exactly the
+// oracle's order).  Phase 2: lane c owns 8-element chunks, scales (cosine), quantises
+// and writes its 16-byte (32-byte for fp32) slot of the tiled layout.
+template <int DT, bool SYNTH>
+__global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uint64_t seed, int64_t grow0, int64_t n,
+                                               int dim, int S, int metric, int64_t lrow0, uint8_t* __restrict__ rows,
+                                               unsigned long long* max_norm2_bits) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    auto src = [&](int d) -> float {
+        if (d >= dim) return 0.0f;
+        return SYNTH ? gen_elem(seed, grow0 + r, dim, d) : in[r * dim + d];
+    };
+    double inv = 1.0;
+    bool scale = false;
+    if (metric == COSINE) {
+        double p = 0.0;
+        for (int d = lane; d < dim; d += 64) {
+            double x = (double)src(d);
+            p = p + x * x;
+        }
+        double n2 = wave_butterfly_sum(p);
+        if (n2 > 0.0) {
+            inv = 1.0 / __builtin_sqrt(n2);
+            scale = true;
+        }
+    }
+    const int64_t R = lrow0 + r;
+    const int nchunk = S * 2;  // 8-element chunks per row
+    double sq = 0.0;
+    for (int c = lane; c < nchunk; c += 64) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = src(8 * c + j);
+            v[j] = scale ? (float)((double)x * inv) : x;
+        }
+        const int s = c >> 1, h = c & 1;
+        const int64_t chunk = (R >> 5) * S + s;
+        const int sl = (int)(R & 31) + 32 * h;
+        if (DT == F32) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sq += (double)v[j] * (double)v[j];
+            float4* p0 = (float4*)(rows + chunk * 2048 + sl * 16);
+            float4* p1 = (float4*)(rows + chunk * 2048 + 1024 + sl * 16);
+            *p0 = make_float4(v[0], v[1], v[2], v[3]);
+            *p1 = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+            uint16_t hq[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                hq[j] = DT == BF16 ? f32_to_bf16_rne(v[j]) : f32_to_f16_rne(v[j]);
+                float dq = DT == BF16 ? bf16_to_f32(hq[j]) : f16_to_f32(hq[j]);
+                sq += (double)dq * (double)dq;
+            }
+            u32x4 w;
+            w[0] = hq[0] | ((uint32_t)hq[1] << 16);
+            w[1] = hq[2] | ((uint32_t)hq[3] << 16);
+            w[2] = hq[4] | ((uint32_t)hq[5] << 16);
+            w[3] = hq[6] | ((uint32_t)hq[7] << 16);
+            *(u32x4*)(rows + chunk * 1024 + sl * 16) = w;
+        }
+    }
+    sq = wave_butterfly_sum(sq);
+    if (lane == 0) atomicMax(max_norm2_bits, (unsigned long long)__builtin_bit_cast(uint64_t, sq));
+}
+
+// ---------------------------------------------------------------- K1: query prep
+// One wave per (padded) query.  q32: normalised fp32 queries [Bp][dpad] (exact rescoring
+// operand); qfrag: MFMA A-fragments [S][QB][64 lanes][8]; qerr[2b] = ||q - q̂||, [2b+1] = ||q̂||.
+template <int MT>
+__global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int B, int Bp, int dim, int dpad, int S,
+                                                int QB, int metric, float* __restrict__ q32,
+                                                uint16_t* __restrict__ qfrag, double* __restrict__ qerr) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= Bp) return;
+    auto src = [&](int d) -> float { return (b < B && d < dim) ? q[(int64_t)b * dim + d] : 0.0f; };
+    double inv = 1.0;
+    bool scale = false;
+    if (metric == COSINE) {
+        double p = 0.0;
+        for (int d = lane; d < dim; d += 64) {
+            double x = (double)src(d);
+            p = p + x * x;
+        }
+        double n2 = wave_butterfly_sum(p);
+        if (n2 > 0.0) {
+            inv = 1.0 / __builtin_sqrt(n2);
+            scale = true;
+        }
+    }
+    double e1 = 0.0, nh = 0.0;
+    const int qb = b >> 5;
+    for (int d = lane; d < dpad; d += 64) {
+        float x = src(d);
+        float v = scale ? (float)((double)x * inv) : x;
+        q32[(int64_t)b * dpad + d] = v;
+        uint16_t h = quant_mt<MT>(v);
+        float dq = dequant_mt<MT>(h);
+        int s = d >> 4, sl = (b & 31) + 32 * ((d >> 3) & 1), j = d & 7;
+        qfrag[(((int64_t)s * QB + qb) * 64 + sl) * 8 + j] = h;
+        double e = (double)v - (double)dq;
+        e1 += e * e;
+        nh += (double)dq * (double)dq;
+    }
+    e1 = wave_butterfly_sum(e1);
+    nh = wave_butterfly_sum(nh);
+    if (lane == 0) {
+        qerr[2 * b] = __builtin_sqrt(e1);
+        qerr[2 * b + 1] = __builtin_sqrt(nh);
+    }
+}
+
+// ---------------------------------------------------------------- K3: the scan
+struct ScanArgs {
+    const uint8_t* rows;     // tiled corpus
+    const uint32_t* live;    // one word per tile
+    const uint32_t* mask;    // one word per tile (u64 row bitmap viewed as u32), nullable
+    const uint16_t* qfrag;   // [S][QB][64][8]
+    int S;
+    int64_t n_units;         // tiles (FILTER) or sample tiles (SAMPLE)
+    int64_t sample_stride;   // SAMPLE: tile = unit * stride
+    uint32_t* mkeys;         // [QB*32][32] group-max keys
+    const float* floor_q;    // [QB*32] per-query floor (collect mode / +inf for padding)
+    int use_groups;          // FILTER: threshold = max(floor, min_g M[q][g]) if set, else floor
+    uint32_t* cnt;           // [QB*32] candidate counts
+    float2* buf;             // [QB*32][cap] (approx score, row bits)
+    int cap;
+    int refresh_every;       // tiles between threshold refreshes (FILTER, use_groups)
+};
+
+template <int MT>
+__device__ inline f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c) {
+    if constexpr (MT == BF16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                        0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                       0, 0);
+}
+
+// X fragment of k-step chunk c (flattened tile*S + s) for this lane, converted to MT
+template <int MT, int DT>
+struct XFrag;
+template <int MT>
+struct XFrag<MT, BF16> {
+    u32x4 v;
+    __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
+        v = *(const u32x4*)(rows + c * 1024 + lane * 16);
+    }
+    __device__ inline u32x4 get() const { return v; }
+};
+template <int MT>
+struct XFrag<MT, F16> {
+    u32x4 v;
+    __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
+        v = *(const u32x4*)(rows + c * 1024 + lane * 16);
+    }
+    __device__ inline u32x4 get() const { return v; }
+};
+template <int MT>
+struct XFrag<MT, F32> {
+    u32x4 a, b;
+    __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
+        a = *(const u32x4*)(rows + c * 2048 + lane * 16);
+        b = *(const u32x4*)(rows + c * 2048 + 1024 + lane * 16);
+    }
+    // fp32 corpus -> MFMA operand: packed hardware RNE conversion (v_cvt_pk_*).  Only the
+    // error-bounded approximate score depends on it (the exact rescoring reads fp32).
+    // Whole-vector bit casts: hipcc (ROCm 7.2) mis-lowers __builtin_bit_cast of single
+    // ext-vector elements here (it re-used one lane value for all eight).
+    __device__ inline u32x4 get() const {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        typedef float f32x8 __attribute__((ext_vector_type(8)));
+        const f32x4 fa = __builtin_bit_cast(f32x4, a);
+        const f32x4 fb = __builtin_bit_cast(f32x4, b);
+        const f32x8 f = __builtin_shufflevector(fa, fb, 0, 1, 2, 3, 4, 5, 6, 7);
+        if constexpr (MT == BF16) {
+            return __builtin_bit_cast(u32x4, __builtin_convertvector(f, bf16x8));
+        } else {
+            return __builtin_bit_cast(u32x4, __builtin_convertvector(f, f16x8));
+        }
+    }
+};
+
+// query index held by accumulator register i of block qb in this lane's half
+__device__ inline int acc_query(int qb, int i, int half) { return qb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half; }
+
+template <int MT, int DT, int QB, int P, bool FILTER>
+__global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int half = lane >> 5;
+    const int g = lane & 31;
+
+    // stage the query fragments (QB*S KiB) into LDS once per launch
+    {
+        const int nvec = a.S * QB * 64;  // 16-byte vectors
+        const u32x4* src = (const u32x4*)a.qfrag;
+        u32x4* dst = (u32x4*)lds;
+        for (int i = tid; i < nvec; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
+    const int64_t base = a.n_units / W, rem = a.n_units % W;
+    const int64_t u0 = w * base + (w < rem ? w : rem);
+    const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
+    if (u0 >= u1) return;
+
+    const int64_t stride = FILTER ? 1 : a.sample_stride;
+    const int S = a.S;
+    const u32x4* qs = (const u32x4*)lds;
+
+    float th[QB][16], gmax[QB][16];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            gmax[qb][i] = -__builtin_inff();
+            th[qb][i] = -__builtin_inff();
+        }
+
+    auto refresh = [&](bool publish) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = acc_query(qb, i, half);
+                uint32_t* mk = a.mkeys + q * 32 + g;
+                if (publish && gmax[qb][i] > th[qb][i]) atomicMax(mk, f2key(gmax[qb][i]));
+                gmax[qb][i] = -__builtin_inff();
+                float f = -__builtin_inff();
+                if (a.use_groups) {
+                    uint32_t k = __hip_atomic_load(mk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    f = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
+#pragma unroll
+                    for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+                }
+                th[qb][i] = fmaxf(th[qb][i], fmaxf(f, a.floor_q[q]));
+            }
+    };
+    if (FILTER) refresh(false);
+
+    XFrag<MT, DT> ring[P];
+    {
+        const int64_t c0 = (u0 * stride) * S;
+#pragma unroll
+        for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
+    }
+
+    for (int64_t u = u0; u < u1; ++u) {
+        const int64_t t = u * stride;
+        const int64_t tn = (u + 1 < u1) ? (u + 1) * stride : t;
+        f32x16 acc[QB];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
+
+        for (int sb = 0; sb < S; sb += P) {
+            const bool same = sb + P < S;
+            const int64_t nc = same ? t * S + sb + P : tn * S;
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                const u32x4 xf = ring[i].get();
+                ring[i].load(a.rows, nc + i, lane);
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) {
+                    const u32x4 qf = qs[((sb + i) * QB + qb) * 64 + lane];
+                    acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
+                }
+            }
+        }
+
+        // epilogue: predicate, group max, threshold filter
+        uint32_t allow = a.live[t];
+        if (a.mask) allow &= a.mask[t];
+        const bool ok = (allow >> g) & 1u;
+        const uint32_t row = (uint32_t)(t * 32 + g);
+        uint64_t any = 0;
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float v = ok ? acc[qb][i] : -__builtin_inff();
+                gmax[qb][i] = fmaxf(gmax[qb][i], v);
+                if (FILTER) any |= __ballot(ok && v >= th[qb][i]);
+            }
+        if (FILTER && any) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float v = acc[qb][i];
+                    const bool pass = ok && v >= th[qb][i];
+                    const uint64_t m = __ballot(pass);
+                    if (m) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const uint32_t mh = (uint32_t)(m >> (32 * h));
+                            if (mh) {
+                                const int q = acc_query(qb, i, h);
+                                const int leader = 32 * h + __builtin_ctz(mh);
+                                uint32_t basepos = 0;
+                                if (lane == leader) basepos = atomicAdd(&a.cnt[q], (uint32_t)__builtin_popcount(mh));
+                                basepos = __shfl(basepos, leader, 64);
+                                if (pass && half == h) {
+                                    const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                                    if (pos < (uint32_t)a.cap)
+                                        a.buf[(int64_t)q * a.cap + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                                }
+                            }
+                        }
+                    }
+                }
+        }
+        if (FILTER && a.use_groups && ((u - u0 + 1) % a.refresh_every) == 0) refresh(true);
+    }
+
+    if (!FILTER) {  // SAMPLE: publish the group maxima
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (gmax[qb][i] > -__builtin_inff())
+                    atomicMax(a.mkeys + acc_query(qb, i, half) * 32 + g, f2key(gmax[qb][i]));
+    }
+}
+
+
+// ---------------------------------------------------------------- diagnostics
+// Approximate (MFMA) scores of every row for the queries in LDS, written densely
+// [Bp][n_tiles*32]; one wave per tile.  Same operand path as k_scan (used by the
+// error-bound test: |approx - exact| <= E_q for every row).
+template <int MT, int DT, int QB>
+__global__ __launch_bounds__(256) void k_debug_approx(const uint8_t* __restrict__ rows, const uint16_t* __restrict__ qfrag,
+                                                      int S, int64_t n_tiles, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int nvec = S * QB * 64;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) ((u32x4*)lds)[i] = ((const u32x4*)qfrag)[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n_tiles) return;
+    const u32x4* qs = (const u32x4*)lds;
+    f32x16 acc[QB];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
+    for (int s = 0; s < S; ++s) {
+        XFrag<MT, DT> x;
+        x.load(rows, t * S + s, lane);
+        const u32x4 xf = x.get();
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma32<MT>(qs[(s * QB + qb) * 64 + lane], xf, acc[qb]);
+    }
+    const int64_t ncol = n_tiles * 32;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) out[(int64_t)acc_query(qb, i, lane >> 5) * ncol + t * 32 + (lane & 31)] = acc[qb][i];
+}
+
+// ---------------------------------------------------------------- K4: select top-kc
+// One 1024-thread block per query.  Keys (u64) = f2key(score) << 32 | ~row: descending
+// key order == (score desc, row asc).
+__device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of two
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    uint64_t x = s[i], y = s[ixj];
+                    bool desc = (i & k) == 0;
+                    if (desc ? (x < y) : (x > y)) {
+                        s[i] = y;
+                        s[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
+                                                 int cap, const uint32_t* __restrict__ mkeys,
+                                                 const float* __restrict__ floor_q, int use_groups, int B, int kc,
+                                                 uint32_t* __restrict__ sel_rows, int* __restrict__ sel_cnt,
+                                                 float* __restrict__ bound_approx, int* __restrict__ overflow) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t* keys = (uint64_t*)smem;
+    __shared__ int m_sh;
+    __shared__ float thr_sh;
+    const int q = blockIdx.x;
+    if (q >= B) return;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        float f = -__builtin_inff();
+        if (use_groups && tid < 32) {
+            uint32_t k = mkeys[q * 32 + tid];
+            f = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
+        } else if (use_groups) {
+            f = __builtin_inff();
+        }
+        for (int off = 32; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+        if (tid == 0) {
+            thr_sh = fmaxf(f, floor_q[q]);
+            m_sh = 0;
+        }
+    }
+    __syncthreads();
+    const uint32_t c = cnt[q];
+    const int n = c < (uint32_t)cap ? (int)c : cap;
+    const float thr = thr_sh;
+    for (int i = tid; i < n; i += blockDim.x) {
+        float2 e = buf[(int64_t)q * cap + i];
+        if (e.x >= thr) {
+            int p = atomicAdd(&m_sh, 1);
+            keys[p] = ((uint64_t)f2key(e.x) << 32) | (uint64_t)(0xFFFFFFFFu - __builtin_bit_cast(uint32_t, e.y));
+        }
+    }
+    __syncthreads();
+    const int m = m_sh;
+    int p2 = 1;
+    while (p2 < m) p2 <<= 1;
+    for (int i = m + tid; i < p2; i += blockDim.x) keys[i] = 0;
+    __syncthreads();
+    if (p2 > 1) block_bitonic_desc(keys, p2);
+    const int keep = m < kc ? m : kc;
+    for (int i = tid; i < kc; i += blockDim.x)
+        sel_rows[q * kc + i] = i < keep ? 0xFFFFFFFFu - (uint32_t)(keys[i] & 0xFFFFFFFFu) : 0xFFFFFFFFu;
+    if (tid == 0) {
+        sel_cnt[q] = keep;
+        bound_approx[q] = (m >= kc && kc > 0) ? key2f((uint32_t)(keys[kc - 1] >> 32)) : thr;
+        overflow[q] = c > (uint32_t)cap ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------- K5: exact rescoring
+// One wave per (query, candidate slot): canonical fp64 dot of the stored row and the
+// normalised fp32 query.  Slot 0 also writes the shard bound = bound_approx + E_q.
+template <int DT>
+__global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ rows, int S, int dpad,
+                                                 const float* __restrict__ q32, const uint32_t* __restrict__ sel_rows,
+                                                 const int* __restrict__ sel_cnt, int B, int kc, int64_t row_offset,
+                                                 const float* __restrict__ bound_approx,
+                                                 const double* __restrict__ qerr, double max_norm, double gamma,
+                                                 double u_x, const int* __restrict__ overflow, Cand* __restrict__ out,
+                                                 double* __restrict__ bound_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wid >= (int64_t)B * kc) return;
+    const int q = (int)(wid / kc), c = (int)(wid % kc);
+    if (c == 0 && lane == 0) {
+        float ba = bound_approx[q];
+        double e1 = qerr[2 * q], nh = qerr[2 * q + 1];
+        double E = max_norm * (e1 * (1.0 + 1e-6) + (gamma + u_x) * nh) + 1e-9;
+        double bd = (ba == -__builtin_inff()) ? -__builtin_inf() : (double)ba + E;
+        if (overflow && overflow[q]) bd = __builtin_inf();
+        bound_out[q] = bd;
+    }
+    if (c >= sel_cnt[q]) {
+        if (lane == 0) out[wid] = Cand{-__builtin_inf(), -1};
+        return;
+    }
+    const int64_t r = (int64_t)sel_rows[q * kc + c];
+    const float* qv = q32 + (int64_t)q * dpad;
+    double p = 0.0;
+    for (int d = lane; d < dpad; d += 64) p = p + (double)load_elem<DT>(rows, S, r, d) * (double)qv[d];
+    p = wave_butterfly_sum(p);
+    if (lane == 0) out[wid] = Cand{p, r + row_offset};
+}
+
+// ---------------------------------------------------------------- K4/C1: merge shards
+// One block per query over G*kc exact candidates.  Sort key: (d2key(score) desc, row asc).
+__global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, const double* __restrict__ bounds, int G,
+                                               int B, int kc, int k, float* __restrict__ scores_out,
+                                               int64_t* __restrict__ rows_out, double* __restrict__ kth_out,
+                                               int32_t* __restrict__ fail_out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int q = blockIdx.x;
+    if (q >= B) return;
+    const int n = G * kc;
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    uint64_t* ks = (uint64_t*)smem;  // score keys
+    int64_t* rs = (int64_t*)(ks + p2);
+    for (int i = threadIdx.x; i < p2; i += blockDim.x) {
+        if (i < n) {
+            const int gi = i / kc, ci = i % kc;
+            Cand e = cand[((int64_t)gi * B + q) * kc + ci];
+            if (e.row < 0) {
+                ks[i] = 0;
+                rs[i] = INT64_MAX;
+            } else {
+                ks[i] = d2key(e.score);
+                rs[i] = e.row;
+            }
+        } else {
+            ks[i] = 0;
+            rs[i] = INT64_MAX;
+        }
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= p2; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < p2; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    uint64_t a = ks[i], b = ks[ixj];
+                    int64_t ra = rs[i], rb = rs[ixj];
+                    bool a_first = a > b || (a == b && ra < rb);
+                    bool desc = (i & kk) == 0;
+                    if (desc ? !a_first : a_first) {
+                        ks[i] = b;
+                        ks[ixj] = a;
+                        rs[i] = rb;
+                        rs[ixj] = ra;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        int valid = 0;
+        for (int i = 0; i < p2 && rs[i] != INT64_MAX; ++i) ++valid;
+        double maxb = -__builtin_inf();
+        for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, bounds[(int64_t)gi * B + q]);
+        double sk = -__builtin_inf();
+        for (int i = 0; i < k; ++i) {
+            if (i < valid) {
+                uint64_t key = ks[i];
+                uint64_t u = (key & 0x8000000000000000ull) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
+                double s = __builtin_bit_cast(double, u);
+                scores_out[(int64_t)q * k + i] = (float)s;
+                rows_out[(int64_t)q * k + i] = rs[i];
+                if (i == k - 1) sk = s;
+            } else {
+                scores_out[(int64_t)q * k + i] = -__builtin_inff();
+                rows_out[(int64_t)q * k + i] = -1;
+            }
+        }
+        if (valid >= k && k > 0) {
+            uint64_t key = ks[k - 1];
+            uint64_t u = (key & 0x8000000000000000ull) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
+            sk = __builtin_bit_cast(double, u);
+        } else if (valid > 0) {
+            sk = -__builtin_inf();  // fewer than k: every remaining row is a candidate
+        }
+        kth_out[q] = sk;
+        bool fail = maxb > -__builtin_inf() && (valid < k || !(sk > maxb));
+        fail_out[q] = fail ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------- get_by_id: de-tile rows
+template <int DT>
+__global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ rows, int S, int dim,
+                                                const int64_t* __restrict__ idx, int64_t n, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n) return;
+    const int64_t r = idx[w];
+    for (int d = lane; d < dim; d += 64) out[w * dim + d] = load_elem<DT>(rows, S, r, d);
+}
+
+}  // namespace hr

@@ -1,0 +1,253 @@
+"""ctypes bindings to libhiprag.so (the HIP/gfx950 vector index).
+
+Declarations: include/hiprag.h.  ctypes releases the GIL for the duration of
+every foreign call, so a blocking search does not stall other Python threads.
+There is no CPU fallback: if the shared library or a GPU is missing, the
+constructors raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhiprag.so")
+
+DTYPES = {"f32": 0, "float32": 0, "fp32": 0, "bf16": 1, "bfloat16": 1, "f16": 2, "float16": 2, "fp16": 2}
+METRICS = {"cosine": 0, "ip": 1, "dot": 1, "euclidean": 2, "l2": 2}
+HR_MAX_K = 32
+CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand
+
+E_INVALID, E_HIP, E_UNSUPPORTED, E_OVERFLOW, E_IO = -1, -2, -3, -4, -5
+
+# every symbol include/hiprag.h declares (checked by tests/test_native_abi.py)
+EXPORTS = [
+    "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_remove",
+    "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows", "hr_index_save",
+    "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_index_last_scan_ms", "hr_device_count", "hr_last_error",
+    "hr_abi_version",
+]
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hiprag error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path: str | None = None):
+    """Load libhiprag.so (raises OSError if it was not built: run __graft_entry__.build())."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
+        # /opt/rocm's).  Loading torch first makes libhiprag.so bind to that same runtime, so
+        # torch tensors, streams and RCCL interoperate with our kernels.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise OSError(f"{p} not found; build it with `make -C youtu-rag_amd/csrc` or __graft_entry__.build()")
+        L = ctypes.CDLL(p)
+        vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
+        pp = ctypes.POINTER(ctypes.c_void_p)
+        sig = {
+            "hr_index_create": [i32, i32, i32, i32, vp, pp],
+            "hr_index_reserve": [vp, i64],
+            "hr_index_add": [vp, vp, i64, vp],
+            "hr_index_add_synthetic": [vp, u64, i64, i64, vp],
+            "hr_index_remove": [vp, vp, i64],
+            "hr_index_search": [vp, vp, i32, i32, vp, vp, vp],
+            "hr_index_search_device": [vp, vp, i32, i32, vp, vp, vp, vp],
+            "hr_index_size": [vp, vp, vp],
+            "hr_index_get_rows": [vp, vp, i64, vp],
+            "hr_index_save": [vp, ctypes.c_char_p],
+            "hr_index_load": [ctypes.c_char_p, i32, vp, pp],
+            "hr_index_search_shard": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp],
+            "hr_index_search_shard_collect": [vp, vp, i32, vp, i32, vp, i64, vp, vp, vp],
+            "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
+            "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
+            "hr_index_last_scan_ms": [vp, vp, vp],
+            "hr_device_count": [vp],
+            "hr_index_debug_approx": [vp, vp, i32, vp, vp],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = i32
+        L.hr_index_destroy.argtypes = [vp]
+        L.hr_index_destroy.restype = None
+        L.hr_last_error.argtypes = []
+        L.hr_last_error.restype = ctypes.c_char_p
+        L.hr_abi_version.restype = i32
+        _lib = L
+        return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = (load_library().hr_last_error() or b"").decode(errors="replace")
+        if rc == E_INVALID:
+            raise ValueError(msg)
+        if rc == E_UNSUPPORTED:
+            raise NotImplementedError(msg)
+        raise NativeError(rc, msg)
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(load_library().hr_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class NativeIndex:
+    """One device shard of the vector index (an hr_index handle)."""
+
+    def __init__(self, dim: int, dtype: str = "bf16", metric: str = "cosine", device: int = 0, _handle=None):
+        self.lib = load_library()
+        self.dim, self.dtype, self.metric, self.device = int(dim), dtype, metric, int(device)
+        if _handle is not None:
+            self._h = _handle
+            return
+        if dtype not in DTYPES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        if metric not in METRICS:
+            raise ValueError(f"unknown metric {metric!r}")
+        h = ctypes.c_void_p()
+        dev = (ctypes.c_int * 1)(self.device)
+        _check(self.lib.hr_index_create(self.dim, DTYPES[dtype], METRICS[metric], 1, dev, ctypes.byref(h)))
+        self._h = h
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.hr_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- data
+    def reserve(self, rows: int):
+        _check(self.lib.hr_index_reserve(self._h, int(rows)))
+
+    def add(self, rows: np.ndarray) -> int:
+        rows = np.ascontiguousarray(rows, np.float32)
+        if rows.ndim != 2 or rows.shape[1] != self.dim:
+            raise ValueError(f"rows must be (n, {self.dim}) float32")
+        first = ctypes.c_int64(0)
+        _check(self.lib.hr_index_add(self._h, _ptr(rows), rows.shape[0], ctypes.byref(first)))
+        return first.value
+
+    def add_synthetic(self, seed: int, global_row0: int, n: int) -> int:
+        first = ctypes.c_int64(0)
+        _check(self.lib.hr_index_add_synthetic(self._h, int(seed), int(global_row0), int(n), ctypes.byref(first)))
+        return first.value
+
+    def remove(self, rows) -> None:
+        r = np.ascontiguousarray(np.asarray(rows, np.int64).reshape(-1))
+        _check(self.lib.hr_index_remove(self._h, _ptr(r), len(r)))
+
+    def size(self) -> tuple[int, int]:
+        n, live = ctypes.c_int64(0), ctypes.c_int64(0)
+        _check(self.lib.hr_index_size(self._h, ctypes.byref(n), ctypes.byref(live)))
+        return n.value, live.value
+
+    def get_rows(self, rows) -> np.ndarray:
+        r = np.ascontiguousarray(np.asarray(rows, np.int64).reshape(-1))
+        out = np.empty((len(r), self.dim), np.float32)
+        _check(self.lib.hr_index_get_rows(self._h, _ptr(r), len(r), _ptr(out)))
+        return out
+
+    # -- search
+    def search(self, q: np.ndarray, k: int, mask: np.ndarray | None = None) -> tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(q, np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.shape[1] != self.dim:
+            raise ValueError(f"query dim {q.shape[1]} != index dim {self.dim}")
+        B = q.shape[0]
+        s = np.empty((B, k), np.float32)
+        r = np.empty((B, k), np.int64)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint64)
+        _check(self.lib.hr_index_search(self._h, _ptr(q), B, int(k), _ptr(m), _ptr(s), _ptr(r)))
+        return s, r
+
+    def search_device(self, q_ptr: int, B: int, k: int, scores_ptr: int, rows_ptr: int, mask_ptr: int = 0,
+                      stream: int = 0) -> None:
+        _check(self.lib.hr_index_search_device(self._h, ctypes.c_void_p(q_ptr), int(B), int(k),
+                                               ctypes.c_void_p(mask_ptr or None), ctypes.c_void_p(scores_ptr),
+                                               ctypes.c_void_p(rows_ptr), ctypes.c_void_p(stream or None)))
+
+    def search_shard(self, q_ptr: int, B: int, k: int, kc: int, row_offset: int, cand_ptr: int, bound_ptr: int,
+                     mask_ptr: int = 0, stream: int = 0) -> None:
+        _check(self.lib.hr_index_search_shard(self._h, ctypes.c_void_p(q_ptr), int(B), int(k), int(kc),
+                                              ctypes.c_void_p(mask_ptr or None), int(row_offset),
+                                              ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bound_ptr),
+                                              ctypes.c_void_p(stream or None)))
+
+    def search_shard_collect(self, q_ptr: int, B: int, kth_ptr: int, cap: int, row_offset: int, cand_ptr: int,
+                             bound_ptr: int, mask_ptr: int = 0, stream: int = 0) -> None:
+        _check(self.lib.hr_index_search_shard_collect(self._h, ctypes.c_void_p(q_ptr), int(B), ctypes.c_void_p(kth_ptr),
+                                                      int(cap), ctypes.c_void_p(mask_ptr or None), int(row_offset),
+                                                      ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bound_ptr),
+                                                      ctypes.c_void_p(stream or None)))
+
+    def debug_approx(self, q: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """(approximate MFMA scores B×n, error bound E per query) -- diagnostics."""
+        q = np.ascontiguousarray(q, np.float32)
+        n, _ = self.size()
+        out = np.empty((q.shape[0], n), np.float32)
+        e = np.empty(q.shape[0], np.float64)
+        _check(self.lib.hr_index_debug_approx(self._h, _ptr(q), q.shape[0], _ptr(out), _ptr(e)))
+        return out, e
+
+    def last_scan_ms(self) -> tuple[float, float]:
+        a, b = ctypes.c_float(0), ctypes.c_float(0)
+        _check(self.lib.hr_index_last_scan_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    # -- persistence
+    def save(self, path: str) -> None:
+        _check(self.lib.hr_index_save(self._h, os.fsencode(path)))
+
+    @classmethod
+    def load(cls, path: str, device: int = 0, dim: int | None = None, dtype: str | None = None,
+             metric: str | None = None) -> "NativeIndex":
+        L = load_library()
+        h = ctypes.c_void_p()
+        dev = (ctypes.c_int * 1)(int(device))
+        _check(L.hr_index_load(os.fsencode(path), 1, dev, ctypes.byref(h)))
+        return cls(dim or 0, dtype or "bf16", metric or "cosine", device, _handle=h)
+
+
+def merge_candidates(device: int, cand_ptr: int, bounds_ptr: int, G: int, B: int, kc: int, k: int, scores_ptr: int,
+                     rows_ptr: int, kth_ptr: int, fail_ptr: int, stream: int = 0) -> None:
+    _check(load_library().hr_merge_candidates(int(device), ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bounds_ptr),
+                                              int(G), int(B), int(kc), int(k), ctypes.c_void_p(scores_ptr),
+                                              ctypes.c_void_p(rows_ptr), ctypes.c_void_p(kth_ptr),
+                                              ctypes.c_void_p(fail_ptr), ctypes.c_void_p(stream or None)))
+
+
+def pool_normalize(hidden_ptr: int, dtype: str, mask_ptr: int, B: int, T: int, H: int, n_instr: int, out_ptr: int,
+                   stream: int = 0) -> None:
+    _check(load_library().hr_pool_normalize(ctypes.c_void_p(hidden_ptr), DTYPES[dtype], ctypes.c_void_p(mask_ptr),
+                                            int(B), int(T), int(H), int(n_instr), ctypes.c_void_p(out_ptr),
+                                            ctypes.c_void_p(stream or None)))

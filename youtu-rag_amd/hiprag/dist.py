@@ -1,0 +1,117 @@
+"""Row-sharded multi-GPU search: one process per GPU, RCCL over xGMI for the merge.
+
+The corpus is split into contiguous row ranges, one per rank (global row =
+shard offset + local row).  Every rank scans its shard for the same replicated
+query batch and produces, per query, its exact top-kc candidates (fp64 canonical
+scores + global rows) and a bound on the score of every row it did NOT return.
+One ``all_gather`` moves B·kc·16 bytes per rank (12 KB at B=64, kc=32 -- latency-
+bound, so one collective per batch and nothing else crosses xGMI); each rank then
+merges the G·kc candidates on its own GPU with the same (score desc, row asc)
+order and the same guard, so all ranks hold identical results.  Queries whose
+guard fails (top-k not provably complete) are re-scanned in collect mode: every
+shard returns all rows whose approximate score could still reach the k-th exact
+score, and a second merge is exact by construction.
+
+The reference is single-process (SURVEY.md §2 "Parallelism strategies: none");
+this module is the C1 collective of the SURVEY kernel inventory.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native
+
+FALLBACK_CAP = 512
+
+
+class ShardedSearch:
+    """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
+
+    def __init__(self, index, row_offset: int, max_batch: int, kc: int = _native.HR_MAX_K, group=None,
+                 device=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.index = index
+        self.row_offset = int(row_offset)
+        self.group = group
+        self.G = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.kc = int(kc)
+        self.max_batch = int(max_batch)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        B, G, kc = self.max_batch, self.G, self.kc
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.cand = torch.empty((B, kc, 2), **f64)          # {score, row bits} records (hr::Cand)
+        self.bound = torch.empty((B,), **f64)
+        self.cand_all = torch.empty((G, B, kc, 2), **f64)
+        self.bound_all = torch.empty((G, B), **f64)
+        self.kth = torch.empty((B,), **f64)
+        self.fail = torch.empty((B,), dtype=torch.int32, device=self.device)
+
+    # hooks (overridden in CPU tests of the orchestration logic)
+    def _stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def _merge(self, cand_all, bound_all, G, B, kc, k, s_out, r_out, kth, fail):
+        _native.merge_candidates(self.device.index or 0, cand_all.data_ptr(), bound_all.data_ptr(), G, B, kc, k,
+                                 s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream())
+
+    def _all_gather(self, out, inp):
+        if self.G == 1:
+            out[0].copy_(inp)
+        else:
+            self.dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    # the search
+    def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
+        """q: (B, dim) float32 device tensor (same on every rank).  Returns (scores, rows) device tensors."""
+        torch = self.torch
+        B = int(q.shape[0])
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > max_batch {self.max_batch}")
+        if not 1 <= k <= self.kc:
+            raise ValueError(f"k must be in [1, {self.kc}]")
+        q = q.contiguous()
+        s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
+        r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
+        cand, bound = self.cand[:B], self.bound[:B]
+        self.index.search_shard(q.data_ptr(), B, k, self.kc, self.row_offset, cand.data_ptr(), bound.data_ptr(),
+                                mask_ptr=mask_ptr, stream=self._stream())
+        cand_all = self.cand_all[:, :B] if B == self.max_batch else torch.empty((self.G, B, self.kc, 2),
+                                                                                  dtype=torch.float64,
+                                                                                  device=self.device)
+        bound_all = self.bound_all[:, :B] if B == self.max_batch else torch.empty((self.G, B), dtype=torch.float64,
+                                                                                    device=self.device)
+        self._all_gather(cand_all, cand)
+        self._all_gather(bound_all, bound)
+        kth, fail = self.kth[:B], self.fail[:B]
+        self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
+        failed = np.nonzero(fail.cpu().numpy())[0]  # host sync: the only one per batch
+        if len(failed):
+            self._fallback(q, k, failed, kth, s_out, r_out, mask_ptr)
+        return s_out, r_out
+
+    def _fallback(self, q, k, failed, kth, s_out, r_out, mask_ptr):
+        torch = self.torch
+        idx = torch.as_tensor(failed, device=self.device)
+        qf = q[idx].contiguous()
+        kf = kth[idx].contiguous()
+        Bf, cap = len(failed), FALLBACK_CAP
+        cand = torch.empty((Bf, cap, 2), dtype=torch.float64, device=self.device)
+        bound = torch.empty((Bf,), dtype=torch.float64, device=self.device)
+        self.index.search_shard_collect(qf.data_ptr(), Bf, kf.data_ptr(), cap, self.row_offset, cand.data_ptr(),
+                                        bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+        cand_all = torch.empty((self.G, Bf, cap, 2), dtype=torch.float64, device=self.device)
+        bound_all = torch.empty((self.G, Bf), dtype=torch.float64, device=self.device)
+        self._all_gather(cand_all, cand)
+        self._all_gather(bound_all, bound)
+        s2 = torch.empty((Bf, k), dtype=torch.float32, device=self.device)
+        r2 = torch.empty((Bf, k), dtype=torch.int64, device=self.device)
+        kth2 = torch.empty((Bf,), dtype=torch.float64, device=self.device)
+        fail2 = torch.empty((Bf,), dtype=torch.int32, device=self.device)
+        self._merge(cand_all, bound_all, self.G, Bf, cap, k, s2, r2, kth2, fail2)
+        if int(fail2.sum().item()):
+            raise RuntimeError("exact fallback overflowed its candidate buffer (massive ties?)")
+        s_out[idx] = s2
+        r_out[idx] = r2

@@ -1,0 +1,52 @@
+"""Oracle-backed stand-in for hiprag._native.NativeIndex -- CPU tests of the HOST logic only.
+
+It lets the store/retriever/distributed orchestration be tested without a GPU; it is
+injected explicitly (``index_factory=``) and never reachable from the product path.
+"""
+import numpy as np
+
+import oracle
+from oracle import ref_numpy as R
+
+
+class OracleIndex:
+    def __init__(self, dim, dtype="bf16", metric="cosine", device=0):
+        self.dim, self.dtype, self.metric = dim, dtype, metric
+        self.rows = np.zeros((0, dim), np.float32 if dtype == "f32" else np.uint16)
+        self.live = np.zeros(0, bool)
+        self.searches = 0
+
+    def reserve(self, n):
+        pass
+
+    def add(self, x):
+        x = np.asarray(x, np.float32)
+        first = len(self.rows)
+        self.rows = np.concatenate([self.rows, R.process_rows(x, self.metric, self.dtype)])
+        self.live = np.concatenate([self.live, np.ones(len(x), bool)])
+        return first
+
+    def remove(self, rows):
+        self.live[np.asarray(rows)] = False
+
+    def size(self):
+        return len(self.rows), int(self.live.sum())
+
+    def get_rows(self, rows):
+        return R.dequantize(self.rows[np.asarray(rows)], self.dtype)
+
+    def search(self, q, k, mask=None):
+        self.searches += 1
+        q = np.asarray(q, np.float32)
+        if q.ndim == 1:
+            q = q[None]
+        allowed = self.live.copy()
+        if mask is not None:
+            bits = np.unpackbits(np.asarray(mask, np.uint64).view(np.uint8), bitorder="little")[: len(allowed)]
+            allowed &= bits.astype(bool)
+        s, r = oracle.c_search(self.rows, self.dtype, R.process_queries(q, self.metric), k,
+                               oracle.mask_from_bool(allowed), nthreads=2)
+        return s.astype(np.float32), r
+
+    def close(self):
+        pass

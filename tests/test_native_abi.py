@@ -1,0 +1,46 @@
+"""CPU: libhiprag.so loads and exports every entry point include/hiprag.h declares
+(no compute call is made without a GPU)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "hiprag.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(hr_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    assert "hr_index_search" in syms and "hr_merge_candidates" in syms and len(syms) >= 20
+
+
+def test_library_exports_every_declared_symbol():
+    from hiprag import _native
+
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libhiprag.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = {line.split()[-1] for line in out.stdout.splitlines() if line.strip()}
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    assert sorted(_native.EXPORTS) == declared_symbols()
+
+
+def test_library_loads_and_reports_errors():
+    from hiprag import _native
+
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libhiprag.so not built")
+    L = _native.load_library()
+    assert L.hr_abi_version() == 1
+    with pytest.raises(ValueError):  # argument validation happens before any device call
+        _native.NativeIndex(0, "bf16", "cosine")
+    with pytest.raises(ValueError):
+        _native.NativeIndex(64, "int8", "cosine")

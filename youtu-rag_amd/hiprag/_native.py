@@ -28,7 +28,8 @@ EXPORTS = [
     "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_remove",
     "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows", "hr_index_save",
     "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_index_last_scan_ms", "hr_device_count", "hr_last_error",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_index_last_scan_ms", "hr_device_count", "hr_index_debug_approx",
+    "hr_last_error",
     "hr_abi_version",
 ]
 

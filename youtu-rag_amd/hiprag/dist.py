@@ -57,11 +57,21 @@ class ShardedSearch:
         _native.merge_candidates(self.device.index or 0, cand_all.data_ptr(), bound_all.data_ptr(), G, B, kc, k,
                                  s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream())
 
+    def _shard_search(self, q, k, cand, bound, mask_ptr):
+        self.index.search_shard(q.data_ptr(), q.shape[0], k, self.kc, self.row_offset, cand.data_ptr(),
+                                bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+
+    def _shard_collect(self, q, kth, cap, cand, bound, mask_ptr):
+        self.index.search_shard_collect(q.data_ptr(), q.shape[0], kth.data_ptr(), cap, self.row_offset,
+                                        cand.data_ptr(), bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+
     def _all_gather(self, out, inp):
         if self.G == 1:
             out[0].copy_(inp)
         else:
-            self.dist.all_gather_into_tensor(out, inp, group=self.group)
+            # output as the rank-concatenation along dim 0 (accepted by RCCL and gloo alike)
+            flat = out.view(self.G * inp.shape[0], *inp.shape[1:])
+            self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
     # the search
     def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
@@ -76,8 +86,7 @@ class ShardedSearch:
         s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
         r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
         cand, bound = self.cand[:B], self.bound[:B]
-        self.index.search_shard(q.data_ptr(), B, k, self.kc, self.row_offset, cand.data_ptr(), bound.data_ptr(),
-                                mask_ptr=mask_ptr, stream=self._stream())
+        self._shard_search(q, k, cand, bound, mask_ptr)
         cand_all = self.cand_all[:, :B] if B == self.max_batch else torch.empty((self.G, B, self.kc, 2),
                                                                                   dtype=torch.float64,
                                                                                   device=self.device)
@@ -100,8 +109,7 @@ class ShardedSearch:
         Bf, cap = len(failed), FALLBACK_CAP
         cand = torch.empty((Bf, cap, 2), dtype=torch.float64, device=self.device)
         bound = torch.empty((Bf,), dtype=torch.float64, device=self.device)
-        self.index.search_shard_collect(qf.data_ptr(), Bf, kf.data_ptr(), cap, self.row_offset, cand.data_ptr(),
-                                        bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+        self._shard_collect(qf, kf, cap, cand, bound, mask_ptr)
         cand_all = torch.empty((self.G, Bf, cap, 2), dtype=torch.float64, device=self.device)
         bound_all = torch.empty((self.G, Bf), dtype=torch.float64, device=self.device)
         self._all_gather(cand_all, cand)

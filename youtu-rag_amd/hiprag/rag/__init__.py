@@ -1,0 +1,19 @@
+"""Drop-in mirror of the reference's KB-search plugin API (utu/rag) backed by the MI355X index."""
+from .base import (BaseEmbedder, BaseKnowledgeBuilder, BaseReranker, BaseRetriever, BaseStorageMonitor,
+                   BaseTextSplitter, BaseVectorStore, BuildStatus, Chunk, Document, HealthStatus, QueryRequest,
+                   QueryResponse, RetrievalResult)
+from .chunker import RecursiveTextSplitter
+from .config import (ChunkingConfig, EmbeddingConfig, KnowledgeBuilderConfig, MonitorConfig, RAGConfig,
+                     RetrieverConfig, VectorStoreConfig)
+from .embeddings import EmbedderFactory, ServiceEmbedder, create_embedder
+from .retriever import BatchedVectorRetriever, HybridRetriever, VectorRetriever
+from .storage import HipVectorStore, VectorStoreFactory
+
+__all__ = [
+    "BaseEmbedder", "BaseKnowledgeBuilder", "BaseReranker", "BaseRetriever", "BaseStorageMonitor", "BaseTextSplitter",
+    "BaseVectorStore", "BuildStatus", "Chunk", "Document", "HealthStatus", "QueryRequest", "QueryResponse",
+    "RetrievalResult", "RecursiveTextSplitter", "ChunkingConfig", "EmbeddingConfig", "KnowledgeBuilderConfig",
+    "MonitorConfig", "RAGConfig", "RetrieverConfig", "VectorStoreConfig", "EmbedderFactory", "ServiceEmbedder",
+    "create_embedder", "BatchedVectorRetriever", "HybridRetriever", "VectorRetriever", "HipVectorStore",
+    "VectorStoreFactory",
+]

@@ -159,6 +159,21 @@ def main():
                      "sample_pass_ms": round(sample_avg, 4)},
     }
 
+    # PMC traffic of the same workload from the committed rocprofv3 summary (tools/profile.sh +
+    # tools/summarize_profile.py): FETCH_SIZE x 2 (gfx950 correction) x 1024, per FILTER launch
+    import glob
+
+    suffix = f"_{N // 1_000_000}Mx{D}_b{B}_summary.json" if G == 1 else f"_{N // 1_000_000}Mx{D}_b{B}_g{G}_summary.json"
+    summaries = sorted(glob.glob(os.path.join(REPO, "profiles", "r*" + suffix)))
+    if summaries and args.dtype == "bf16" and K == 10:
+        with open(summaries[-1]) as f:
+            prof = json.load(f)
+        if prof.get("k_scan_filter_hbm_read_bytes"):
+            result["roofline"]["traffic"] = round(prof["k_scan_filter_hbm_read_bytes"] / 1e9, 3)
+            result["roofline"]["traffic_unit"] = "GB per launch (HBM read, PMC)"
+            result["roofline"]["traffic_source"] = os.path.relpath(summaries[-1], REPO)
+            result["roofline"]["profiled_avg_launch_ms"] = round(prof["k_scan_filter_ms_avg"], 4)
+
     # recall@10 against the oracle's exact answer over the full corpus (rank 0)
     if rank == 0 and not args.no_cpu:
         try:

@@ -1,0 +1,62 @@
+"""GPU: the full drop-in stack -- HipVectorStore on libhiprag.so behind the reference's
+VectorRetriever semantics -- reproduces the golden retriever outputs; persistence round-trips."""
+import asyncio
+import json
+import os
+
+import numpy as np
+import pytest
+
+from hiprag.rag import (BatchedVectorRetriever, Chunk, HipVectorStore, RetrieverConfig, VectorRetriever,
+                        VectorStoreConfig, VectorStoreFactory)
+
+pytestmark = pytest.mark.gpu
+
+
+class TableEmbedder:
+    def __init__(self, table):
+        self.table = table
+
+    async def embed_query(self, q):
+        return self.table[q].tolist()
+
+    async def embed_texts(self, texts):
+        return [self.table[t].tolist() for t in texts]
+
+
+def _chunks(d, meta):
+    return [Chunk(id=f"chunk_{r}", document_id=m["document_id"], content=f"text {r}", chunk_index=m["chunk_index"],
+                  metadata={"group": m["group"]}, embedding=d["corpus"][r].tolist()) for r, m in enumerate(meta["metas"])]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_store_retriever_golden(tmp_path, golden_dir, dtype):
+    d = dict(np.load(os.path.join(golden_dir, "c1_retrieval.npz")))
+    meta = json.load(open(os.path.join(golden_dir, "c1_retrieval.json")))
+    cfg = VectorStoreConfig(backend="hip", collection_name="c1", persist_directory=str(tmp_path),
+                            index_params={"dtype": dtype})
+    store = VectorStoreFactory.create(cfg)
+    assert isinstance(store, HipVectorStore)
+    asyncio.run(store.add_chunks(_chunks(d, meta)))
+    emb = TableEmbedder(dict(zip(meta["query_names"], d["queries"])))
+    for tag, rc, kw in [("thr0", RetrieverConfig(top_k=5, similarity_threshold=0.0), {}),
+                        ("thr_default", RetrieverConfig(top_k=5), {}),
+                        ("filtered_g1", RetrieverConfig(top_k=5, similarity_threshold=0.0), {"filters": {"group": "g1"}})]:
+        for cls in (VectorRetriever, BatchedVectorRetriever):
+            got = asyncio.run(cls(store, emb, rc).batch_retrieve(meta["query_names"], top_k=5, **kw))
+            exp = meta["results"][tag]
+            if dtype == "f32":  # the golden store is fp32; bf16 storage may legitimately reorder near-ties
+                assert [[(r.chunk.id, r.rank) for r in res] for res in got] == \
+                    [[(e["chunk_id"], e["rank"]) for e in res] for res in exp]
+                for res, ex in zip(got, exp):
+                    np.testing.assert_allclose([r.score for r in res], [e["score"] for e in ex], atol=1e-5, rtol=0)
+            else:
+                assert [res[0].chunk.id for res in got if res] == [res[0]["chunk_id"] for res in exp if res]
+    # persistence: a new store object on the same directory serves the same answers
+    before = store.search_batch(d["queries"], 5)
+    store2 = HipVectorStore(cfg)
+    assert asyncio.run(store2.count()) == 1000
+    after = store2.search_batch(d["queries"], 5)
+    assert [[c.id for c, _ in res] for res in before] == [[c.id for c, _ in res] for res in after]
+    asyncio.run(store2.delete_by_document_id("doc_0"))
+    assert asyncio.run(HipVectorStore(cfg).count()) == 990

@@ -1,0 +1,15 @@
+# rocprofv3 passes over the headline bench (kernel trace + stats, then HBM PMC counters).
+# Usage on the GPU box: bash tools/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}; shift || true
+ARGS=${@:-"--steps 10 --warmup 2 --no-cpu"}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o run --output-format csv -- python3 bench.py $ARGS > $OUT/bench_kt.log 2>&1
+rc=$?; echo "kernel-trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_scan -T -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py $ARGS > $OUT/bench_pmc1.log 2>&1
+rc=$?; echo "pmc FETCH_SIZE rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_scan -T -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py $ARGS > $OUT/bench_pmc2.log 2>&1
+echo "pmc WRITE_SIZE rc=$?"
+find $OUT -name "*.csv" | head -20

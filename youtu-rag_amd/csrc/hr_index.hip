@@ -574,11 +574,12 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
     DevBuf& so = h->stage;
     const size_t words = (size_t)((h->n + 63) / 64);
-    HIP_TRY(so.ensure((size_t)B * k * 12 + (row_mask ? words * 8 : 0)));
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t off_r = up((size_t)B * k * 4), off_m = off_r + up((size_t)B * k * 8);
+    HIP_TRY(so.ensure(off_m + (row_mask ? words * 8 : 0)));
     float* s_dev = (float*)so.p;
-    int64_t* r_dev = (int64_t*)((uint8_t*)so.p + (size_t)B * k * 4);
-    uint64_t* m_dev = row_mask ? (uint64_t*)((uint8_t*)so.p + (size_t)B * k * 12) : nullptr;
-    if (m_dev && ((uintptr_t)m_dev & 7)) return set_err(HR_E_INVALID, "internal alignment");
+    int64_t* r_dev = (int64_t*)((uint8_t*)so.p + off_r);
+    uint64_t* m_dev = row_mask ? (uint64_t*)((uint8_t*)so.p + off_m) : nullptr;
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     if (row_mask) HIP_TRY(hipMemcpyAsync(m_dev, row_mask, words * 8, hipMemcpyHostToDevice, st));
     if (int rc = search_device_impl(h, h->q_in.as<float>(), B, k, m_dev, s_dev, r_dev, st)) return rc;

@@ -94,12 +94,18 @@ int hr_merge_candidates(int device, const void* cand_dev /* G*B*kc records */, c
 int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,
                       float* out_dev, void* stream);
 
-/* Timing of the most recent scan launch on this handle (ms, HIP events). */
+/* Timing of the main-pass scans (ms, HIP events recorded on the search stream).
+ * take_scan_times harvests, in launch order, every (SAMPLE, FILTER) pair launched since the
+ * previous harvest (blocking on the pending events; up to cap entries; count in n_out);
+ * last_scan_ms harvests everything and reports the most recent pair. */
+int hr_index_take_scan_times(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n_out);
 int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms);
 int hr_device_count(int* n_out);
 /* Diagnostics: approximate MFMA scores of every row (B <= 64; approx_out B×n) and the
  * per-query error bound E_q that the exactness guard uses (e_out, B). */
 int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out);
+/* Diagnostics: candidates appended by the most recent FILTER scan (sum, max per query). */
+int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

@@ -5,7 +5,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -52,7 +54,8 @@ struct DevBuf {
     }
 };
 
-static constexpr int kCap = 8192;       // candidate buffer per query (scan FILTER mode)
+static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
+static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
 static constexpr int kScanThreads = 512;
 
 struct hr_index {
@@ -64,13 +67,21 @@ struct hr_index {
     std::vector<uint32_t> live_host;
     unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {};
+    // per-launch timing of the main (SAMPLE, FILTER) scan pair: events are recorded on the
+    // search stream and harvested later, so batches can be pipelined (see hr_index_take_scan_times)
+    struct ScanEvents {
+        hipEvent_t e[4];
+        bool sampled;
+    };
+    std::vector<ScanEvents> ev_free;
+    std::deque<ScanEvents> ev_pending;
     float last_sample_ms = 0.f, last_filter_ms = 0.f;
     int n_cu = 256;
     std::mutex mu;
     // search workspace
     DevBuf q_in, q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, cand, bound,
-        kth, fail, fb_cand, fb_bound, stage;
+        kth, fail, fb_cand, fb_bound, stage, pbuf, pcnt;
+    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
     std::vector<float> floor_host;
 };
 
@@ -117,7 +128,6 @@ extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const 
     h->device = dev;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&h->ev[i]);
     if (e == hipSuccess) e = hipMalloc(&h->norm_bits, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(h->norm_bits, 0, sizeof(unsigned long long));
     hipDeviceProp_t prop;
@@ -285,14 +295,16 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     p->QB = QB;
     p->Bp = QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
-    const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : (QB == 2 ? 8 : 16);
+    const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
     p->P = (h->S % 16 == 0 && pmax >= 16) ? 16 : (h->S % 8 == 0 && pmax >= 8 ? 8 : 4);
+    static const int ring_env = getenv("HIPRAG_RING") ? atoi(getenv("HIPRAG_RING")) : 0;  // tuning experiments
+    if ((ring_env == 4 || ring_env == 8 || ring_env == 16) && ring_env <= pmax && h->S % ring_env == 0) p->P = ring_env;
     return HR_OK;
 }
 
-template <int MT, int DT, int QB, int P, bool FILTER>
+template <int MT, int DT, int QB, int P, int MODE>
 static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds) {
-    auto kern = k_scan<MT, DT, QB, P, FILTER>;
+    auto kern = k_scan<MT, DT, QB, P, MODE>;
     static std::mutex attr_mu;
     static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
     static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown)
@@ -312,33 +324,48 @@ static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds
         }
         per_cu = occ[dev][bucket];
     }
-    int64_t waves_needed = a.n_units;
-    int64_t blocks = std::min<int64_t>((int64_t)h->n_cu * per_cu, (waves_needed + 7) / 8);
-    blocks = std::max<int64_t>(blocks, 1);
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kScanThreads), lds, st, a);
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu, (a.n_units + 7) / 8));
+    ScanArgs args = a;
+    if (MODE == SCAN_FILTER) {
+        const int64_t W = blocks * (kScanThreads / 64);
+        const int Bq = QB * 32;
+        HIP_TRY(h->pbuf.ensure((size_t)Bq * W * kCapW * sizeof(float2)));
+        HIP_TRY(h->pcnt.ensure((size_t)Bq * W * 4));
+        args.pbuf = h->pbuf.as<float2>();
+        args.pcnt = h->pcnt.as<uint32_t>();
+        args.capw = kCapW;
+        h->last_W = W;
+        h->last_Bp = Bq;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kScanThreads), lds, st, args);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }
 
-template <int MT, int DT, bool FILTER>
+template <int MT, int DT, int MODE>
 static int launch_scan_p(hr_index* h, const Plan& pl, const ScanArgs& a, hipStream_t st) {
     const int lds = scan_lds_bytes(h, pl.QB);
 #define HR_SCAN_CASE(QBv, Pv) \
-    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, FILTER>(h, a, st, lds);
-    if constexpr (DT == F32) {
+    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, a, st, lds);
+    if constexpr (MODE == SCAN_COLLECT) {  // the fallback runs one query at a time
+        HR_SCAN_CASE(1, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4)
+    } else if constexpr (DT == F32) {
         HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
     } else {
-        HR_SCAN_CASE(1, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(2, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
+        HR_SCAN_CASE(1, 16) HR_SCAN_CASE(2, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(2, 8) HR_SCAN_CASE(1, 4)
+        HR_SCAN_CASE(2, 4)
     }
 #undef HR_SCAN_CASE
     return set_err(HR_E_INVALID, "no scan variant for this plan");
 }
 
-static int launch_scan(hr_index* h, const Plan& pl, const ScanArgs& a, bool filter, hipStream_t st) {
+static int launch_scan(hr_index* h, const Plan& pl, const ScanArgs& a, int mode, hipStream_t st) {
     return dispatch_dt(h->dtype, [&](auto dt) -> int {
         constexpr int DT = decltype(dt)::value;
         constexpr int MT = DT == F16 ? F16 : BF16;
-        return filter ? launch_scan_p<MT, DT, true>(h, pl, a, st) : launch_scan_p<MT, DT, false>(h, pl, a, st);
+        if (mode == SCAN_SAMPLE) return launch_scan_p<MT, DT, SCAN_SAMPLE>(h, pl, a, st);
+        if (mode == SCAN_FILTER) return launch_scan_p<MT, DT, SCAN_FILTER>(h, pl, a, st);
+        return launch_scan_p<MT, DT, SCAN_COLLECT>(h, pl, a, st);
     });
 }
 
@@ -369,13 +396,17 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(h->bound_approx.ensure((size_t)Bp * 4));
     HIP_TRY(h->overflow.ensure((size_t)Bp * 4));
 
+    static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int MT = mfma_type(h->dtype);
+    float* fl = (mode == 0 && !(dbg & 1)) ? h->floor_q.as<float>() : nullptr;  // else uploaded below
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad,
-                           h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+                           h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
+                           h->mkeys.as<uint32_t>(), h->cnt.as<uint32_t>(), fl);
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
-                           pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+                           pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
+                           h->mkeys.as<uint32_t>(), h->cnt.as<uint32_t>(), fl);
     HIP_TRY(hipGetLastError());
 
     // floors: padded queries never collect; mode 1 uses kth - E (computed on the host from qerr)
@@ -398,9 +429,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             h->floor_host[(size_t)b] = f;
         }
     }
-    HIP_TRY(hipMemcpyAsync(h->floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(h->mkeys.p, 0, (size_t)Bp * 32 * 4, st));
-    HIP_TRY(hipMemsetAsync(h->cnt.p, 0, (size_t)Bp * 4, st));
+    // HIPRAG_SCAN_DEBUG (timing experiments only; results are wrong with bits 1/4 set):
+    // 1 = no candidate appends, 2 = no threshold refresh, 4 = no sample pass, 8 = refresh never publishes,
+    // 16 = publish with relaxed stores instead of atomicMax
+    if (!fl) {
+        if (dbg & 1)
+            for (auto& f : h->floor_host) f = INFINITY;
+        HIP_TRY(hipMemcpyAsync(h->floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
+    }
 
     const int64_t n_tiles = (h->n + 31) / 32;
     ScanArgs a{};
@@ -414,31 +450,57 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.cnt = h->cnt.as<uint32_t>();
     a.buf = h->buf.as<float2>();
     a.cap = kCap;
-    a.refresh_every = 4;
+    static const int refresh_env = getenv("HIPRAG_REFRESH") ? atoi(getenv("HIPRAG_REFRESH")) : 0;
+    a.publish = (dbg & 8) ? 0 : (dbg & 16) ? 2 : 1;
+    a.private_bufs = mode == 0 ? 1 : 0;
+    a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
-    h->last_sample_ms = 0.f;
     if (n_tiles > 0) {
-        if (groups) {
+        hr_index::ScanEvents ev{};
+        if (groups) {  // time the main pass only, not fallbacks
+            if (h->ev_free.empty()) {
+                for (auto& x : ev.e) HIP_TRY(hipEventCreate(&x));
+            } else {
+                ev = h->ev_free.back();
+                h->ev_free.pop_back();
+            }
+            ev.sampled = false;
+        }
+        if (groups && !(dbg & 4)) {
             const int64_t target = std::max<int64_t>(512, n_tiles / 64);
             a.sample_stride = std::max<int64_t>(1, n_tiles / target);
             a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
-            HIP_TRY(hipEventRecord(h->ev[0], st));
-            if (int rc = launch_scan(h, pl, a, false, st)) return rc;
-            HIP_TRY(hipEventRecord(h->ev[1], st));
+            HIP_TRY(hipEventRecord(ev.e[0], st));
+            if (int rc = launch_scan(h, pl, a, SCAN_SAMPLE, st)) return rc;
+            HIP_TRY(hipEventRecord(ev.e[1], st));
+            ev.sampled = true;
         }
         a.sample_stride = 1;
         a.n_units = n_tiles;
-        HIP_TRY(hipEventRecord(h->ev[2], st));
-        if (int rc = launch_scan(h, pl, a, true, st)) return rc;
-        HIP_TRY(hipEventRecord(h->ev[3], st));
+        if (groups) HIP_TRY(hipEventRecord(ev.e[2], st));
+        if (int rc = launch_scan(h, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
+        if (groups) {
+            HIP_TRY(hipEventRecord(ev.e[3], st));
+            h->ev_pending.push_back(ev);
+            while (h->ev_pending.size() > 4096) {  // nobody is harvesting: recycle the oldest
+                h->ev_free.push_back(h->ev_pending.front());
+                h->ev_pending.pop_front();
+            }
+        }
     }
     // select
     const int kc_sel = mode == 0 ? kc : cap_out;
     const int sort_cap = kCap;  // power of two
-    HIP_TRY(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, sort_cap * 8));
-    hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8, st, h->cnt.as<uint32_t>(), h->buf.as<float2>(),
-                       kCap, h->mkeys.as<uint32_t>(), h->floor_q.as<float>(), a.use_groups, B, kc_sel,
+    static bool sel_attr[64] = {};  // per device, set once
+    if (!sel_attr[h->device & 63]) {
+        HIP_TRY(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, sort_cap * 8 + 16));
+        sel_attr[h->device & 63] = true;
+    }
+    const bool priv = a.private_bufs && n_tiles > 0;
+    hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st, h->cnt.as<uint32_t>(), h->buf.as<float2>(),
+                       kCap, priv ? h->pcnt.as<uint32_t>() : nullptr, priv ? h->pbuf.as<float2>() : nullptr,
+                       (int)h->last_W, kCapW, Bp, h->mkeys.as<uint32_t>(), h->floor_q.as<float>(), a.use_groups, B, kc_sel,
                        h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), h->bound_approx.as<float>(),
                        h->overflow.as<int>());
     HIP_TRY(hipGetLastError());
@@ -495,7 +557,11 @@ static int launch_merge(int device, const Cand* cand, const double* bounds, int 
     while (p2 < G * kc) p2 <<= 1;
     const int lds = p2 * 16;
     if (lds > 160 * 1024) return set_err(HR_E_INVALID, "too many candidates to merge");
-    HIP_TRY(hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    static bool merge_attr[64] = {};
+    if (!merge_attr[device & 63]) {
+        HIP_TRY(hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        merge_attr[device & 63] = true;
+    }
     hipLaunchKernelGGL(k_merge, dim3(B), dim3(256), lds, st, cand, bounds, G, B, kc, k, s_out, r_out, kth_out,
                        fail_out);
     HIP_TRY(hipGetLastError());
@@ -652,10 +718,12 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     const int MT = mfma_type(h->dtype);
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
-                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
+                           nullptr, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
-                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>());
+                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
+                           nullptr, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
     const int lds = scan_lds_bytes(h, pl.QB);
     int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
@@ -804,24 +872,74 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     for (DevBuf* b : {&h->q_in, &h->q32, &h->qfrag, &h->qerr, &h->mkeys, &h->floor_q, &h->cnt, &h->buf, &h->sel_rows,
                       &h->sel_cnt, &h->bound_approx, &h->overflow, &h->cand, &h->bound, &h->kth, &h->fail,
-                      &h->fb_cand, &h->fb_bound, &h->stage})
+                      &h->fb_cand, &h->fb_bound, &h->stage, &h->pbuf, &h->pcnt})
         b->release();
-    for (auto& e : h->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto* list : {&h->ev_free})
+        for (auto& ev : *list)
+            for (auto& x : ev.e) (void)hipEventDestroy(x);
+    for (auto& ev : h->ev_pending)
+        for (auto& x : ev.e) (void)hipEventDestroy(x);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
+}
+
+// harvest (blocking) the timings of every main-pass scan launched since the last harvest
+static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n) {
+    int k = 0;
+    while (!h->ev_pending.empty() && k < cap) {
+        hr_index::ScanEvents ev = h->ev_pending.front();
+        h->ev_pending.pop_front();
+        HIP_TRY(hipEventSynchronize(ev.e[3]));
+        float a = 0.f, b = 0.f;
+        if (ev.sampled) HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ev.e[2], ev.e[3]));
+        if (sample_ms) sample_ms[k] = a;
+        if (filter_ms) filter_ms[k] = b;
+        h->last_sample_ms = a;
+        h->last_filter_ms = b;
+        h->ev_free.push_back(ev);
+        ++k;
+    }
+    if (n) *n = k;
+    return HR_OK;
+}
+
+extern "C" int hr_index_take_scan_times(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n_out) {
+    if (!h || cap < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    return harvest(h, sample_ms, filter_ms, cap, n_out);
 }
 
 extern "C" int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
-    HIP_TRY(hipEventSynchronize(h->ev[3]));
-    float a = 0.f, b = 0.f;
-    if (hipEventElapsedTime(&a, h->ev[0], h->ev[1]) != hipSuccess) a = 0.f;
-    HIP_TRY(hipEventElapsedTime(&b, h->ev[2], h->ev[3]));
-    if (sample_ms) *sample_ms = a;
-    if (filter_ms) *filter_ms = b;
+    if (int rc = harvest(h, nullptr, nullptr, 1 << 30, nullptr)) return rc;
+    if (sample_ms) *sample_ms = h->last_sample_ms;
+    if (filter_ms) *filter_ms = h->last_filter_ms;
+    return HR_OK;
+}
+
+
+// diagnostics: candidates appended by the last FILTER scan (sum and max over queries)
+extern "C" int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    // private per-wave counts of the last FILTER scan: pcnt[W][Bp]
+    const int64_t n = h->last_W * h->last_Bp;
+    std::vector<uint32_t> c((size_t)n);
+    if (n) HIP_TRY(hipMemcpy(c.data(), h->pcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    std::vector<int64_t> per_q((size_t)h->last_Bp, 0);
+    for (int64_t i = 0; i < n; ++i) per_q[(size_t)(i % h->last_Bp)] += c[(size_t)i];
+    int64_t t = 0, m = 0;
+    for (int64_t v : per_q) {
+        t += v;
+        m = std::max<int64_t>(m, v);
+    }
+    if (total) *total = t;
+    if (max_per_query) *max_per_query = m;
     return HR_OK;
 }
 

@@ -116,10 +116,20 @@ __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uin
 template <int MT>
 __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int B, int Bp, int dim, int dpad, int S,
                                                 int QB, int metric, float* __restrict__ q32,
-                                                uint16_t* __restrict__ qfrag, double* __restrict__ qerr) {
+                                                uint16_t* __restrict__ qfrag, double* __restrict__ qerr,
+                                                uint32_t* __restrict__ mkeys, uint32_t* __restrict__ cnt,
+                                                float* __restrict__ floor_q) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
+    // per-batch scratch of this query (replaces two memsets and an H2D copy per batch):
+    // group maxima -> -inf, candidate count -> 0, floor -> -inf (+inf for padding rows);
+    // floor_q == nullptr: the caller uploaded explicit floors (collect mode)
+    if (mkeys && lane < 32) mkeys[b * 32 + lane] = HR_KEY_NEG_INF;
+    if (lane == 0) {
+        if (cnt) cnt[b] = 0;
+        if (floor_q) floor_q[b] = b < B ? -__builtin_inff() : __builtin_inff();
+    }
     auto src = [&](int d) -> float { return (b < B && d < dim) ? q[(int64_t)b * dim + d] : 0.0f; };
     double inv = 1.0;
     bool scale = false;
@@ -166,13 +176,22 @@ struct ScanArgs {
     int S;
     int64_t n_units;         // tiles (FILTER) or sample tiles (SAMPLE)
     int64_t sample_stride;   // SAMPLE: tile = unit * stride
-    uint32_t* mkeys;         // [QB*32][32] group-max keys
+    uint32_t* mkeys;         // [QB*32 queries][32 groups] group-max keys (a wave-wide access spans 2 lines)
     const float* floor_q;    // [QB*32] per-query floor (collect mode / +inf for padding)
     int use_groups;          // FILTER: threshold = max(floor, min_g M[q][g]) if set, else floor
-    uint32_t* cnt;           // [QB*32] candidate counts
+    uint32_t* cnt;           // [QB*32] candidate counts (shared-buffer mode)
     float2* buf;             // [QB*32][cap] (approx score, row bits)
     int cap;
     int refresh_every;       // tiles between threshold refreshes (FILTER, use_groups)
+    int publish;             // FILTER: publish this wave's group maxima at refresh
+    // private mode (FILTER): each wave appends into its own region pbuf[w][q][capw] and
+    // reports pcnt[w][q]; no atomics on the append path.  The [wave][query] order makes the
+    // query index a compile-time offset from a wave-uniform base (no hoisted per-query
+    // pointers: those cost ~150 VGPRs of spills in the fully unrolled epilogue).
+    int private_bufs;
+    float2* pbuf;
+    uint32_t* pcnt;
+    int capw;
 };
 
 template <int MT>
@@ -232,8 +251,15 @@ struct XFrag<MT, F32> {
 // query index held by accumulator register i of block qb in this lane's half
 __device__ inline int acc_query(int qb, int i, int half) { return qb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half; }
 
-template <int MT, int DT, int QB, int P, bool FILTER>
+// MODE: SCAN_SAMPLE (group maxima only), SCAN_FILTER (threshold + private per-wave
+// candidate regions, no atomics on the append path), SCAN_COLLECT (floor-only threshold,
+// shared per-query buffer with atomic slot reservation; the exact fallback)
+enum { SCAN_SAMPLE = 0, SCAN_FILTER = 1, SCAN_COLLECT = 2 };
+
+template <int MT, int DT, int QB, int P, int MODE>
 __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
+    constexpr bool FILTER = MODE != SCAN_SAMPLE;
+    constexpr bool priv = MODE == SCAN_FILTER;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -254,13 +280,23 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const int64_t base = a.n_units / W, rem = a.n_units % W;
     const int64_t u0 = w * base + (w < rem ? w : rem);
     const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
-    if (u0 >= u1) return;
+    if (u0 >= u1) {
+        if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = 0;
+        return;
+    }
+    uint32_t mycnt = 0;  // private mode: lane q counts the candidates of query q in this wave
+    float2* const wave_buf = priv ? a.pbuf + w * (QB * 32) * a.capw : nullptr;
 
     const int64_t stride = FILTER ? 1 : a.sample_stride;
     const int S = a.S;
     const u32x4* qs = (const u32x4*)lds;
 
     float th[QB][16], gmax[QB][16];
+    // this lane's group column of the group-max table, one base per query block; the per-register
+    // query offset 32*((i&3) + 8(i>>2)) words stays under the 4 KiB immediate-offset range
+    uint32_t* gkq[QB];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) gkq[qb] = a.mkeys + (qb * 32 + 4 * half) * 32 + g;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
@@ -269,22 +305,46 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
             th[qb][i] = -__builtin_inff();
         }
 
+    // Threshold refresh.  All 16*QB group-max loads are issued back to back (one memory round
+    // trip per refresh; a load->compare->branch chain costs one round trip PER register and
+    // measured 0.6 ms of a 1.0 ms scan at 1.25M rows), then this wave's group max is published
+    // only where it beats the global value (a blind atomicMax from every wave piles ~#waves
+    // atomics onto each of the 32*B addresses).
     auto refresh = [&](bool publish) {
+        if (!a.use_groups) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    gmax[qb][i] = -__builtin_inff();
+                    th[qb][i] = fmaxf(th[qb][i], a.floor_q[acc_query(qb, i, half)]);
+                }
+            return;
+        }
+        uint32_t key[QB][16];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                key[qb][i] = __hip_atomic_load(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int q = acc_query(qb, i, half);
-                uint32_t* mk = a.mkeys + q * 32 + g;
-                if (publish && gmax[qb][i] > th[qb][i]) atomicMax(mk, f2key(gmax[qb][i]));
-                gmax[qb][i] = -__builtin_inff();
-                float f = -__builtin_inff();
-                if (a.use_groups) {
-                    uint32_t k = __hip_atomic_load(mk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    f = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
-#pragma unroll
-                    for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+                float f = key2f(key[qb][i] > HR_KEY_NEG_INF ? key[qb][i] : HR_KEY_NEG_INF);
+                if (publish && a.publish && gmax[qb][i] > f) {
+                    if (a.publish == 2)
+                        __hip_atomic_store(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
+                    f = gmax[qb][i];
                 }
+#pragma unroll
+                for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+                gmax[qb][i] = -__builtin_inff();
                 th[qb][i] = fmaxf(th[qb][i], fmaxf(f, a.floor_q[q]));
             }
     };
@@ -347,7 +407,16 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
                             const uint32_t mh = (uint32_t)(m >> (32 * h));
-                            if (mh) {
+                            if (priv && mh) {
+                                const int q = acc_query(qb, i, h);  // compile-time: readlane is cheap
+                                const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)mycnt, q);
+                                if (pass && half == h) {
+                                    const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                                    if (pos < (uint32_t)a.capw)
+                                        wave_buf[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                                }
+                                mycnt += (lane == q) ? (uint32_t)__builtin_popcount(mh) : 0u;
+                            } else if (!priv && mh) {
                                 const int q = acc_query(qb, i, h);
                                 const int leader = 32 * h + __builtin_ctz(mh);
                                 uint32_t basepos = 0;
@@ -363,16 +432,17 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
                     }
                 }
         }
-        if (FILTER && a.use_groups && ((u - u0 + 1) % a.refresh_every) == 0) refresh(true);
+        if (MODE == SCAN_FILTER && ((u - u0 + 1) % a.refresh_every) == 0) refresh(true);
     }
 
+    if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;
     if (!FILTER) {  // SAMPLE: publish the group maxima
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 if (gmax[qb][i] > -__builtin_inff())
-                    atomicMax(a.mkeys + acc_query(qb, i, half) * 32 + g, f2key(gmax[qb][i]));
+                    atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
     }
 }
 
@@ -434,14 +504,18 @@ __device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of t
 }
 
 __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
-                                                 int cap, const uint32_t* __restrict__ mkeys,
+                                                 int cap, const uint32_t* __restrict__ pcnt,
+                                                 const float2* __restrict__ pbuf, int W, int capw, int Bp,
+                                                 const uint32_t* __restrict__ mkeys,
                                                  const float* __restrict__ floor_q, int use_groups, int B, int kc,
                                                  uint32_t* __restrict__ sel_rows, int* __restrict__ sel_cnt,
                                                  float* __restrict__ bound_approx, int* __restrict__ overflow) {
+    // all LDS in the dynamic region (G17): 16 B of scalars, then the sort keys
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t* keys = (uint64_t*)smem;
-    __shared__ int m_sh;
-    __shared__ float thr_sh;
+    int& m_sh = *(int*)smem;
+    int& ovf_sh = *(int*)(smem + 4);
+    float& thr_sh = *(float*)(smem + 8);
+    uint64_t* keys = (uint64_t*)(smem + 16);
     const int q = blockIdx.x;
     if (q >= B) return;
     const int tid = threadIdx.x;
@@ -457,21 +531,37 @@ __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cn
         if (tid == 0) {
             thr_sh = fmaxf(f, floor_q[q]);
             m_sh = 0;
+            ovf_sh = 0;
         }
     }
     __syncthreads();
-    const uint32_t c = cnt[q];
-    const int n = c < (uint32_t)cap ? (int)c : cap;
     const float thr = thr_sh;
-    for (int i = tid; i < n; i += blockDim.x) {
-        float2 e = buf[(int64_t)q * cap + i];
+    bool ovf = false;
+    auto push = [&](float2 e) {
         if (e.x >= thr) {
             int p = atomicAdd(&m_sh, 1);
-            keys[p] = ((uint64_t)f2key(e.x) << 32) | (uint64_t)(0xFFFFFFFFu - __builtin_bit_cast(uint32_t, e.y));
+            if (p < cap)
+                keys[p] = ((uint64_t)f2key(e.x) << 32) | (uint64_t)(0xFFFFFFFFu - __builtin_bit_cast(uint32_t, e.y));
+            else
+                ovf = true;
         }
+    };
+    if (pcnt) {  // private per-wave regions of the FILTER scan
+        for (int w = tid; w < W; w += blockDim.x) {
+            const uint32_t c = pcnt[(int64_t)w * Bp + q];
+            if (c > (uint32_t)capw) ovf = true;
+            const int n = c < (uint32_t)capw ? (int)c : capw;
+            for (int j = 0; j < n; ++j) push(pbuf[((int64_t)w * Bp + q) * capw + j]);
+        }
+    } else {
+        const uint32_t c = cnt[q];
+        if (c > (uint32_t)cap) ovf = true;
+        const int n = c < (uint32_t)cap ? (int)c : cap;
+        for (int i = tid; i < n; i += blockDim.x) push(buf[(int64_t)q * cap + i]);
     }
+    if (ovf) atomicOr(&ovf_sh, 1);
     __syncthreads();
-    const int m = m_sh;
+    const int m = m_sh < cap ? m_sh : cap;
     int p2 = 1;
     while (p2 < m) p2 <<= 1;
     for (int i = m + tid; i < p2; i += blockDim.x) keys[i] = 0;
@@ -483,7 +573,7 @@ __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cn
     if (tid == 0) {
         sel_cnt[q] = keep;
         bound_approx[q] = (m >= kc && kc > 0) ? key2f((uint32_t)(keys[kc - 1] >> 32)) : thr;
-        overflow[q] = c > (uint32_t)cap ? 1 : 0;
+        overflow[q] = ovf_sh;
     }
 }
 

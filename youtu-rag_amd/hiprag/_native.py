@@ -28,8 +28,8 @@ EXPORTS = [
     "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_remove",
     "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows", "hr_index_save",
     "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_index_last_scan_ms", "hr_device_count", "hr_index_debug_approx",
-    "hr_last_error",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_index_take_scan_times", "hr_index_last_scan_ms", "hr_device_count", "hr_index_debug_approx",
+    "hr_index_last_candidates", "hr_last_error",
     "hr_abi_version",
 ]
 
@@ -79,8 +79,10 @@ def load_library(path: str | None = None):
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
             "hr_index_last_scan_ms": [vp, vp, vp],
+            "hr_index_take_scan_times": [vp, vp, vp, i32, vp],
             "hr_device_count": [vp],
             "hr_index_debug_approx": [vp, vp, i32, vp, vp],
+            "hr_index_last_candidates": [vp, vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -219,6 +221,19 @@ class NativeIndex:
         e = np.empty(q.shape[0], np.float64)
         _check(self.lib.hr_index_debug_approx(self._h, _ptr(q), q.shape[0], _ptr(out), _ptr(e)))
         return out, e
+
+    def last_candidates(self) -> tuple[int, int]:
+        t, m = ctypes.c_int64(0), ctypes.c_int64(0)
+        _check(self.lib.hr_index_last_candidates(self._h, ctypes.byref(t), ctypes.byref(m)))
+        return t.value, m.value
+
+    def take_scan_times(self, cap: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
+        """(sample_ms, filter_ms) of every main-pass scan since the previous harvest."""
+        a = np.empty(cap, np.float32)
+        b = np.empty(cap, np.float32)
+        n = ctypes.c_int(0)
+        _check(self.lib.hr_index_take_scan_times(self._h, _ptr(a), _ptr(b), int(cap), ctypes.byref(n)))
+        return a[: n.value].copy(), b[: n.value].copy()
 
     def last_scan_ms(self) -> tuple[float, float]:
         a, b = ctypes.c_float(0), ctypes.c_float(0)

@@ -4,13 +4,18 @@ The corpus is split into contiguous row ranges, one per rank (global row =
 shard offset + local row).  Every rank scans its shard for the same replicated
 query batch and produces, per query, its exact top-kc candidates (fp64 canonical
 scores + global rows) and a bound on the score of every row it did NOT return.
-One ``all_gather`` moves B·kc·16 bytes per rank (12 KB at B=64, kc=32 -- latency-
+One ``all_gather`` moves B·kc·16 bytes per rank (32 KB at B=64, kc=32 -- latency-
 bound, so one collective per batch and nothing else crosses xGMI); each rank then
 merges the G·kc candidates on its own GPU with the same (score desc, row asc)
 order and the same guard, so all ranks hold identical results.  Queries whose
 guard fails (top-k not provably complete) are re-scanned in collect mode: every
 shard returns all rows whose approximate score could still reach the k-th exact
 score, and a second merge is exact by construction.
+
+Batches can be pipelined: ``submit`` enqueues a whole batch (scan, gather, merge,
+a non-blocking copy of the guard flags) and returns a ticket; ``finalize`` waits for
+that batch's flags only and runs the (rare) fallback.  With ``depth`` tickets in
+flight the host's per-batch work overlaps the GPU's.
 
 The reference is single-process (SURVEY.md §2 "Parallelism strategies: none");
 this module is the C1 collective of the SURVEY kernel inventory.
@@ -24,11 +29,25 @@ from . import _native
 FALLBACK_CAP = 512
 
 
+class _Slot:
+    def __init__(self, torch, device, G, B, kc, pinned):
+        f64 = dict(dtype=torch.float64, device=device)
+        self.cand = torch.empty((B, kc, 2), **f64)  # {score, row bits} records (hr::Cand)
+        self.bound = torch.empty((B,), **f64)
+        self.cand_all = torch.empty((G, B, kc, 2), **f64) if G > 1 else None
+        self.bound_all = torch.empty((G, B), **f64) if G > 1 else None
+        self.kth = torch.empty((B,), **f64)
+        self.fail = torch.empty((B,), dtype=torch.int32, device=device)
+        self.fail_h = torch.empty((B,), dtype=torch.int32, pin_memory=pinned)
+        self.event = torch.cuda.Event() if pinned else None
+        self.ticket = None  # (q, k, s_out, r_out, mask_ptr, B) while in flight
+
+
 class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
     def __init__(self, index, row_offset: int, max_batch: int, kc: int = _native.HR_MAX_K, group=None,
-                 device=None):
+                 device=None, depth: int = 2):
         import torch
         import torch.distributed as dist
 
@@ -40,14 +59,9 @@ class ShardedSearch:
         self.kc = int(kc)
         self.max_batch = int(max_batch)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        B, G, kc = self.max_batch, self.G, self.kc
-        f64 = dict(dtype=torch.float64, device=self.device)
-        self.cand = torch.empty((B, kc, 2), **f64)          # {score, row bits} records (hr::Cand)
-        self.bound = torch.empty((B,), **f64)
-        self.cand_all = torch.empty((G, B, kc, 2), **f64)
-        self.bound_all = torch.empty((G, B), **f64)
-        self.kth = torch.empty((B,), **f64)
-        self.fail = torch.empty((B,), dtype=torch.int32, device=self.device)
+        pinned = self.device.type == "cuda"
+        self.slots = [_Slot(torch, self.device, self.G, self.max_batch, self.kc, pinned) for _ in range(max(1, depth))]
+        self._next = 0
 
     # hooks (overridden in CPU tests of the orchestration logic)
     def _stream(self) -> int:
@@ -74,32 +88,66 @@ class ShardedSearch:
             self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
     # the search
-    def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
-        """q: (B, dim) float32 device tensor (same on every rank).  Returns (scores, rows) device tensors."""
+    def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
+        """Enqueue one batch; returns a ticket for finalize().  q: (B, dim) float32 device tensor,
+        identical on every rank."""
         torch = self.torch
         B = int(q.shape[0])
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
         if not 1 <= k <= self.kc:
             raise ValueError(f"k must be in [1, {self.kc}]")
+        slot = self.slots[self._next]
+        self._next = (self._next + 1) % len(self.slots)
+        if slot.ticket is not None:
+            self.finalize(slot)
         q = q.contiguous()
         s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
         r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
-        cand, bound = self.cand[:B], self.bound[:B]
+        cand, bound = slot.cand[:B], slot.bound[:B]
         self._shard_search(q, k, cand, bound, mask_ptr)
-        cand_all = self.cand_all[:, :B] if B == self.max_batch else torch.empty((self.G, B, self.kc, 2),
-                                                                                  dtype=torch.float64,
-                                                                                  device=self.device)
-        bound_all = self.bound_all[:, :B] if B == self.max_batch else torch.empty((self.G, B), dtype=torch.float64,
-                                                                                    device=self.device)
-        self._all_gather(cand_all, cand)
-        self._all_gather(bound_all, bound)
-        kth, fail = self.kth[:B], self.fail[:B]
+        if self.G == 1:  # nothing to exchange: merge straight from this shard's candidates
+            cand_all, bound_all = cand.view(1, B, self.kc, 2), bound.view(1, B)
+        else:
+            full = B == self.max_batch
+            cand_all = slot.cand_all if full else torch.empty((self.G, B, self.kc, 2), dtype=torch.float64,
+                                                              device=self.device)
+            bound_all = slot.bound_all if full else torch.empty((self.G, B), dtype=torch.float64, device=self.device)
+            self._all_gather(cand_all, cand)
+            self._all_gather(bound_all, bound)
+        kth, fail = slot.kth[:B], slot.fail[:B]
         self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
-        failed = np.nonzero(fail.cpu().numpy())[0]  # host sync: the only one per batch
+        if slot.event is not None:
+            slot.fail_h[:B].copy_(fail, non_blocking=True)
+            slot.event.record(torch.cuda.current_stream(self.device))
+        else:
+            slot.fail_h[:B].copy_(fail)
+        slot.ticket = (q, k, s_out, r_out, mask_ptr, B)
+        return slot
+
+    def finalize(self, slot) -> tuple:
+        """Wait for a submitted batch's guard flags (only those) and run its fallback if needed."""
+        if slot.ticket is None:
+            raise ValueError("ticket already finalized")
+        q, k, s_out, r_out, mask_ptr, B = slot.ticket
+        slot.ticket = None
+        if slot.event is not None:
+            slot.event.synchronize()
+        failed = np.nonzero(slot.fail_h[:B].numpy())[0]
         if len(failed):
-            self._fallback(q, k, failed, kth, s_out, r_out, mask_ptr)
+            self._fallback(q, k, failed, slot.kth[:B], s_out, r_out, mask_ptr)
         return s_out, r_out
+
+    def finalize_all(self):
+        for i in range(len(self.slots)):
+            slot = self.slots[(self._next + i) % len(self.slots)]
+            if slot.ticket is not None:
+                self.finalize(slot)
+
+    def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
+        """Synchronous search of one batch.  Returns (scores, rows) device tensors."""
+        self.finalize_all()
+        return self.finalize(self.submit(q, k, s_out, r_out, mask_ptr))
 
     def _fallback(self, q, k, failed, kth, s_out, r_out, mask_ptr):
         torch = self.torch

@@ -85,7 +85,13 @@ class ShardedSearch:
         else:
             # output as the rank-concatenation along dim 0 (accepted by RCCL and gloo alike)
             flat = out.view(self.G * inp.shape[0], *inp.shape[1:])
-            self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
+            if out.is_cuda and self.dist.get_backend(self.group) != "nccl":
+                # gloo (tests: several ranks sharing one GPU) gathers host tensors
+                tmp = flat.cpu()
+                self.dist.all_gather_into_tensor(tmp, inp.cpu().contiguous(), group=self.group)
+                flat.copy_(tmp)
+            else:
+                self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
     # the search
     def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):

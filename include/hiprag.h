@@ -59,12 +59,18 @@ enum {
     HR_E_IO = -5
 };
 
-#define HR_MAX_K 32            /* top-k served by the fast path */
+#define HR_MAX_K 128           /* largest top-k (kb_file_search recall 15 x 3, rerank top-100) */
+#define HR_MAX_KC 160          /* largest per-shard candidate count kc */
 
 int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);
 int hr_index_reserve(hr_index* h, int64_t capacity_rows);
 int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* first_row_out);
 int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global_row0, int64_t n, int64_t* first_row_out);
+/* Same as hr_index_add for n fp32 rows already in device memory (e.g. the in-process embedder's
+ * hr_pool_normalize output): ordered after the work queued on `stream`, no host round trip of the
+ * vectors; returns once the rows are stored (rows_dev may then be reused).
+ * Replaces embed_texts -> add_chunks in BaseProcessor._chunk_and_store (processors.py:413-418). */
+int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n, int64_t* first_row_out, void* stream);
 int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n);
 int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
                     int64_t* rows_out);
@@ -78,7 +84,10 @@ void hr_index_destroy(hr_index* h);
 
 /* Row-sharded search pieces (one process per GPU; RCCL moves the candidates).
  * Candidate record = {double exact_score; int64 global_row} (16 bytes).
- * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_K).             */
+ * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_KC); the scan keeps
+ * ceil(kc/32) row parts of group maxima.  hr_kc_for_k gives the kc the single-GPU search
+ * uses: 32 for k <= 32, else k + 16 rounded up to a multiple of 32 (margin for the guard). */
+int hr_kc_for_k(int k);
 int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                           int64_t row_offset, void* cand_out_dev /* B*kc records */,
                           double* bound_out_dev /* B */, void* stream);

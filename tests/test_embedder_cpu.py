@@ -1,0 +1,113 @@
+"""CPU: host logic of the in-process embedder and the GPU ingest slice.
+
+* HashWordTokenizer: HF-style padding / truncation / special tokens.
+* TorchRocmEmbedder: prefixes, instruction-token count, batching -- with the K7 kernel
+  replaced by the torch restatement (tests/embed_ref.py) so the rest runs on CPU; the
+  K7 kernel itself is checked against the same restatement in test_gpu_embedder.py.
+* GpuIngestor: chunk ids / metadata as processors.py:387-407, delete-before-add,
+  batches spanning documents (oracle-backed index, host-list embedder).
+"""
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+
+from embed_ref import ref_mean_pooling, ref_passages, ref_queries
+from fake_index import OracleIndex
+from hiprag.rag import ChunkingConfig, Document, HipVectorStore, VectorStoreConfig
+from hiprag.rag.ingest import GpuIngestor, make_chunks
+from hiprag.rag.rocm_embedder import HashWordTokenizer, TorchRocmEmbedder
+
+
+def run(c):
+    return asyncio.run(c)
+
+
+def test_hash_tokenizer_hf_semantics():
+    tok = HashWordTokenizer()
+    one = tok("Hello, world!", add_special_tokens=True)["input_ids"]
+    assert one[0] == 101 and one[-1] == 102 and len(one) == 6
+    assert tok("", add_special_tokens=True)["input_ids"] == [101, 102]
+    assert tok("", add_special_tokens=False)["input_ids"] == []
+    assert tok("hello")["input_ids"][1] == tok("HELLO")["input_ids"][1]
+    b = tok(["a b c d e f", "x"], padding=True, truncation=True, max_length=5, return_tensors="pt")
+    assert b["input_ids"].shape == (2, 5) and b["attention_mask"].tolist() == [[1] * 5, [1, 1, 1, 0, 0]]
+    assert b["input_ids"][0, -1] == 102 and b["input_ids"][1, -1] == 0
+
+
+class CpuEmbedder(TorchRocmEmbedder):
+    def _pool(self, hidden, mask, n_instr):
+        m = mask.clone()
+        m[:, :n_instr] = 0
+        return torch.nn.functional.normalize(ref_mean_pooling(hidden, m), dim=-1)
+
+
+@pytest.fixture(scope="module")
+def cpu_emb():
+    return CpuEmbedder(preset="tiny", device="cpu", batch_size=3, max_length=64)
+
+
+def test_embedder_matches_reference_encode_on_cpu(cpu_emb):
+    texts = ["the quick brown fox", "jumps over", "the lazy dog " * 10, "a", "retrieval augmented generation"]
+    got = cpu_emb.encode_passages(texts)
+    ref = torch.cat([ref_passages(cpu_emb, texts[i:i + 3]) for i in range(0, 5, 3)])
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-6)
+    q = cpu_emb.encode_queries(["what is a fox?", "dog"])
+    torch.testing.assert_close(q, ref_queries(cpu_emb, ["what is a fox?", "dog"]), rtol=0, atol=1e-6)
+    assert cpu_emb.query_instruction.startswith("Instruction: Given a search query") and \
+        cpu_emb.query_instruction.endswith(" \nQuery:")
+    # the empty passage instruction still masks the tokenizer's special tokens (mdx:98-107 quirk)
+    assert cpu_emb._n_instruction_tokens("") == 2
+    v = run(cpu_emb.embed_query("dog"))
+    assert isinstance(v, list) and len(v) == 256 and abs(np.linalg.norm(v) - 1) < 1e-5
+    assert len(run(cpu_emb.embed_texts(texts))) == 5
+    assert cpu_emb.max_length == 64
+
+
+def test_embedder_rejects_missing_local_model():
+    with pytest.raises(FileNotFoundError):
+        TorchRocmEmbedder("/nonexistent/model", device="cpu")
+
+
+def test_make_chunks_matches_processor_convention():
+    doc = Document(id="report.pdf", content="", metadata={"source": "s3", "_private": 1})
+    ch = make_chunks(doc, ["a", "b"], {"kb": 7})
+    assert [c.id for c in ch] == ["report.pdf_chunk_0", "report.pdf_chunk_1"]
+    assert ch[1].metadata == {"source": "s3", "index_type": "index_content", "kb": 7} and ch[1].chunk_index == 1
+    doc2 = Document(id="d", content="", metadata={"index_type": "index_summary"})
+    assert make_chunks(doc2, ["x"])[0].metadata["index_type"] == "index_summary"
+
+
+class HashEmbedder:
+    """Host-list embedder: deterministic vectors per text."""
+    batch_size = 4
+
+    def __init__(self):
+        self.batches = []
+
+    async def embed_texts(self, texts):
+        self.batches.append(len(texts))
+        return [np.random.default_rng(abs(hash(t)) % 2**32).standard_normal(16).tolist() for t in texts]
+
+
+def test_ingestor_batches_across_documents_and_replaces_old_chunks(tmp_path):
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
+                            index_params={"dtype": "f32", "persist": False})
+    store = HipVectorStore(cfg, index_factory=lambda d: OracleIndex(d, "f32"))
+    emb = HashEmbedder()
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=100, chunk_overlap=0))
+    docs = [Document(id=f"doc{i}", content=" ".join(f"word{j}" for j in range(30 * i + 2)), metadata={"n": i})
+            for i in range(6)]
+    n = run(ing.ingest(docs))
+    assert n == run(store.count()) and sum(emb.batches) == n and max(emb.batches) == 4
+    assert all(b == 4 for b in emb.batches[:-1])
+    c = run(store.get_by_id("doc3_chunk_0"))
+    assert c.metadata["n"] == 3 and c.metadata["index_type"] == "index_content"
+    # re-ingesting a document replaces its chunks
+    before = run(store.count())
+    old = len(store._doc_rows["doc5"])
+    m = run(ing.chunk_and_store(Document(id="doc5", content="short text", metadata={})))
+    assert run(store.count()) == before - old + m and len(store._doc_rows["doc5"]) == m
+    with pytest.raises(NotImplementedError):
+        ing.split(Document(id="h", content="# x", metadata={"_use_hierarchical_splitter": True}))

@@ -1,0 +1,102 @@
+"""GPU: the in-process embedder (PyTorch-ROCm forward + K7 HIP pooling) and the GPU ingest slice.
+
+* K7 (hr_pool_normalize) vs the torch restatement of mean_pooling + F.normalize
+  (tests/embed_ref.py <- deploying-locally.mdx:75-79, :114-115) on ragged masks, every
+  hidden dtype and instruction lengths 0 / inside / past the sequence.  Tolerance: 1e-5
+  absolute on unit vectors (fp32 sums in a different order; the NorthStar score tolerance).
+* TorchRocmEmbedder.encode == the reference encode on the same model/tokenizer, fp32 and bf16.
+* split -> embed -> hr_index_add_device -> BatchedVectorRetriever: stored rows bit-equal to the
+  oracle's quantisation of the embedder output, ids identical to the oracle search.
+"""
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from embed_ref import ref_mean_pooling, ref_passages, ref_queries
+from hiprag import _native
+from hiprag.rag import BatchedVectorRetriever, ChunkingConfig, Document, HipVectorStore, RetrieverConfig, VectorStoreConfig
+from hiprag.rag.ingest import GpuIngestor
+from hiprag.rag.rocm_embedder import TorchRocmEmbedder
+from oracle import ref_numpy as R
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-5
+DEV = torch.device("cuda", 0)
+TD = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n_instr", [0, 3, 19])
+def test_k7_pool_normalize_matches_torch(dt, n_instr):
+    g = torch.Generator(device="cpu").manual_seed(7)
+    B, T, H = 6, 37, 1000
+    hidden = torch.randn((B, T, H), generator=g).to(DEV, TD[dt])
+    lens = torch.tensor([37, 20, 1, 25, 19, 36])
+    mask = (torch.arange(T)[None, :] < lens[:, None]).to(torch.int32).to(DEV)
+    out = torch.empty((B, H), dtype=torch.float32, device=DEV)
+    _native.pool_normalize(hidden.data_ptr(), dt, mask.data_ptr(), B, T, H, n_instr, out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    m = mask.clone()
+    m[:, :n_instr] = 0
+    ref = torch.nn.functional.normalize(ref_mean_pooling(hidden, m), dim=-1)
+    torch.cuda.synchronize()
+    # rows whose every token is masked are 0/0 = NaN in the reference too
+    torch.testing.assert_close(out, ref, rtol=0, atol=ATOL, equal_nan=True)
+    assert torch.isnan(out).any(1).tolist() == (m.sum(1) == 0).tolist()
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_embedder_matches_reference_encode(dtype):
+    emb = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=3)
+    texts = [f"passage {i}: " + " ".join(f"w{(i * 7 + j) % 97}" for j in range(5 + 11 * i)) for i in range(8)]
+    got = emb.encode_passages(texts)
+    ref = ref_passages(emb, texts)
+    assert got.shape == (8, 768) and got.dtype == torch.float32
+    torch.testing.assert_close(got, ref.float(), rtol=0, atol=ATOL)
+    qs = ["what is w3?", "tell me about passage five and w12 w40"]
+    torch.testing.assert_close(emb.encode_queries(qs), ref_queries(emb, qs).float(), rtol=0, atol=ATOL)
+    v = asyncio.run(emb.embed_query(qs[0]))
+    np.testing.assert_allclose(v, ref_queries(emb, qs[:1])[0].float().cpu().numpy(), atol=ATOL, rtol=0)
+
+
+def test_ingest_split_embed_add_query(tmp_path):
+    emb = TorchRocmEmbedder(preset="tiny", batch_size=32, max_length=128, seed=1)
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
+                            index_params={"dtype": "bf16", "persist": True})
+    store = HipVectorStore(cfg)
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20))
+    seen = []  # the exact device vectors handed to the index
+    inner = emb.embed_texts_device
+    emb.embed_texts_device = lambda texts: seen.append(inner(texts)) or seen[-1]
+    rng = np.random.default_rng(0)
+    words = [f"term{i}" for i in range(400)]
+    docs = [Document(id=f"doc{d}", content=". ".join(" ".join(rng.choice(words, 12)) for _ in range(20 + d)),
+                     metadata={"source": f"s{d % 3}"}) for d in range(25)]
+    n = asyncio.run(ing.ingest(docs))
+    assert n == asyncio.run(store.count()) > 300
+    # the stored rows are exactly the oracle's bf16 quantisation of the embedder's vectors
+    records = [r for r in store._records if r is not None]
+    vecs = torch.cat(seen).cpu().numpy()
+    assert len(vecs) == len(records)
+    rows = np.array([store._id_to_row[r["id"]] for r in records])
+    assert (rows == np.arange(len(rows))).all()
+    stored = store._index.get_rows(rows)
+    expect = R.process_rows(vecs, "cosine", "bf16")
+    np.testing.assert_array_equal(stored, R.dequantize(expect, "bf16"))
+    # retrieval through the reference retriever API == oracle search over the same vectors
+    queries = [" ".join(rng.choice(words, 6)) for _ in range(12)]
+    got = asyncio.run(BatchedVectorRetriever(store, emb, RetrieverConfig(top_k=10, similarity_threshold=0.0))
+                      .batch_retrieve(queries, top_k=10))
+    qv = emb.encode_queries(queries).cpu().numpy()
+    order = np.argsort(rows)
+    s_ref, r_ref = oracle.c_search(expect[order], "bf16", R.process_queries(qv, "cosine"), 10)
+    ids_sorted = [records[i]["id"] for i in order]
+    assert [[r.chunk.id for r in res] for res in got] == [[ids_sorted[j] for j in rr] for rr in r_ref]
+    for res, sr in zip(got, s_ref):
+        np.testing.assert_allclose([r.score for r in res], sr, atol=ATOL, rtol=0)
+    # persisted once at the end of the bulk ingest; a fresh store serves the same rows
+    store2 = HipVectorStore(cfg)
+    assert asyncio.run(store2.count()) == n

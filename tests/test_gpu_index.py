@@ -128,6 +128,67 @@ def test_random_vs_oracle(native, dim, dtype, n, B, k):
     _check(s, r, s_ref, r_ref)
 
 
+# top-k beyond 32 (kb_file_search recall 15 x 3, rerank top-100): ceil(kc/32) row parts of group maxima
+LARGE_K = [(768, "bf16", 40000, 64, 45), (1024, "bf16", 30000, 64, 100), (256, "f16", 9000, 33, 128),
+           (384, "f32", 20000, 20, 64), (128, "bf16", 3000, 5, 128), (64, "bf16", 150, 3, 100)]
+
+
+@pytest.mark.parametrize("dim,dtype,n,B,k", LARGE_K)
+def test_large_k_vs_oracle(native, dim, dtype, n, B, k):
+    rng = np.random.default_rng(dim + k)
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    idx.add_synthetic(6, 0, n)
+    raw = R.gen_rows(6, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+    allowed = rng.random(n) < 0.7
+    stored = oracle.c_build_synthetic(6, 0, n, dim, dtype, "cosine")
+    for mask in (None, allowed):
+        s, r = idx.search(q, k, None if mask is None else oracle.mask_from_bool(mask))
+        s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, "cosine"), k,
+                                       None if mask is None else oracle.mask_from_bool(mask))
+        _check(s, r, s_ref, r_ref)
+
+
+def test_large_k_massive_ties(native):
+    """300 identical rows, k = 100: the 100 lowest duplicate rows, via the exact fallback."""
+    dim, n = 128, 8000
+    raw = R.gen_rows(12, 0, n, dim)
+    dups = np.sort(np.random.default_rng(4).choice(n, 300, replace=False))
+    raw[dups] = raw[dups[0]]
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    s, r = idx.search(raw[dups[:1]].copy(), 100)
+    np.testing.assert_array_equal(r[0], dups[:100])
+
+
+@pytest.mark.parametrize("dtype,k", [("bf16", 10), ("f32", 128), ("f16", 45)])
+def test_exhaustive_exact_when_window_overflows(native, dtype, k):
+    """Concentrated embeddings (every row within the error bound of the k-th score, as a
+    random-init transformer produces) and 2000 exact duplicates: the collect window overflows
+    its buffer and the exhaustive exact pass answers -- still identical to the oracle."""
+    dim, n = 256, 12000
+    rng = np.random.default_rng(21)
+    base = rng.standard_normal(dim).astype(np.float32)
+    raw = (base + 1e-4 * rng.standard_normal((n, dim))).astype(np.float32)
+    dups = np.sort(rng.choice(n, 2000, replace=False))
+    raw[dups] = raw[dups[0]]
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    idx.add(raw)
+    gone = rng.choice(n, 500, replace=False)
+    idx.remove(gone)
+    allowed = rng.random(n) < 0.8
+    eff = allowed.copy()
+    eff[gone] = False
+    q = np.stack([raw[dups[0]], base + 1e-4 * rng.standard_normal(dim).astype(np.float32), rng.standard_normal(dim)])
+    q = q.astype(np.float32)
+    stored = R.process_rows(raw, "cosine", dtype)
+    for m in (None, allowed):
+        s, r = idx.search(q, k, None if m is None else oracle.mask_from_bool(m))
+        s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, "cosine"), k,
+                                       oracle.mask_from_bool(eff if m is not None else ~np.isin(np.arange(n), gone)))
+        _check(s, r, s_ref, r_ref)
+
+
 def test_ip_metric(native):
     rng = np.random.default_rng(5)
     x = rng.standard_normal((3000, 128)).astype(np.float32) * rng.uniform(0.1, 3.0, (3000, 1)).astype(np.float32)
@@ -175,7 +236,7 @@ def test_empty_small_and_ragged(native):
     s, r = idx.search(q, 5)
     assert (r == -1).all()
     with pytest.raises(ValueError):
-        idx.search(q, 33)
+        idx.search(q, native.HR_MAX_K + 1)
     with pytest.raises(ValueError):
         idx.search(np.ones((1, 63), np.float32), 5)
 
@@ -245,6 +306,38 @@ def test_device_and_sharded_merge(native):
     assert fail.sum().item() == 0
     np.testing.assert_array_equal(rd.cpu().numpy(), r_host)
     np.testing.assert_array_equal(sd.cpu().numpy(), s_host)
+
+
+def test_sharded_merge_large_k(native):
+    torch = pytest.importorskip("torch")
+    dim, n, B, k = 256, 20000, 40, 100
+    kc = native.kc_for_k(k)
+    raw = R.gen_rows(13, 0, n, dim)
+    q = _planted_queries(raw, B, np.random.default_rng(8))
+    s_ref, r_ref = oracle.c_search(R.process_rows(raw, "cosine", "bf16"), "bf16", R.process_queries(q, "cosine"), k)
+    cuts = [0, 6001, 13007, n]
+    qd = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    G = len(cuts) - 1
+    cand = torch.empty((G, B, kc, 2), dtype=torch.float64, device="cuda")
+    bounds = torch.empty((G, B), dtype=torch.float64, device="cuda")
+    shards = []
+    for g in range(G):
+        sh = native.NativeIndex(dim, "bf16", "cosine")
+        sh.add(raw[cuts[g]:cuts[g + 1]])
+        sh.search_shard(qd.data_ptr(), B, k, kc, cuts[g], cand[g].data_ptr(), bounds[g].data_ptr(), stream=st)
+        shards.append(sh)
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    rd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kth = torch.empty(B, dtype=torch.float64, device="cuda")
+    fail = torch.empty(B, dtype=torch.int32, device="cuda")
+    native.merge_candidates(0, cand.data_ptr(), bounds.data_ptr(), G, B, kc, k, sd.data_ptr(), rd.data_ptr(),
+                            kth.data_ptr(), fail.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    ok = fail.cpu().numpy() == 0
+    assert ok.mean() > 0.9  # planted queries: the guard should almost always hold
+    np.testing.assert_array_equal(rd.cpu().numpy()[ok], r_ref[ok])
+    np.testing.assert_array_equal(sd.cpu().numpy()[ok], s_ref[ok].astype(np.float32))
 
 
 def test_pool_normalize_matches_torch(native):

@@ -76,6 +76,31 @@ __device__ __host__ inline uint64_t d2key(double d) {
     return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
+// inverse of d2key
+__device__ __host__ inline double key2d(uint64_t k) {
+    uint64_t u = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __builtin_bit_cast(double, u);
+}
+
+// byte offset of k-step chunk (tile, s) for lane l; stride 1 KiB (16-bit) / 2 KiB (fp32)
+template <int DT>
+__device__ __host__ inline size_t chunk_bytes() { return DT == F32 ? 2048 : 1024; }
+
+// element (row r, column d) of the tiled corpus, as float
+template <int DT>
+__device__ inline float load_elem(const uint8_t* base, int S, int64_t r, int d) {
+    int64_t chunk = (r >> 5) * S + (d >> 4);
+    int lane = (int)(r & 31) + 32 * ((d >> 3) & 1);
+    int j = d & 7;
+    if (DT == F32) {
+        const float* p = (const float*)(base + chunk * 2048 + (j >> 2) * 1024 + lane * 16);
+        return p[j & 3];
+    } else {
+        const uint16_t* p = (const uint16_t*)(base + chunk * 1024 + lane * 16);
+        return DT == BF16 ? bf16_to_f32(p[j]) : f16_to_f32(p[j]);
+    }
+}
+
 __device__ inline uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -1,0 +1,101 @@
+// hr_exhaustive.hip -- last-resort exact top-m of one query over a whole shard.
+//
+// The collect fallback (DESIGN.md "Exactness guard") gathers every row whose approximate
+// score is within the error bound of the k-th exact score; when that window holds more rows
+// than its buffer (massive exact ties, or an embedding model that maps every chunk to
+// nearly the same direction -- a random-init transformer does), this path takes over:
+// canonical fp64 score of every live, allowed row (same arithmetic as k_rescore, so the
+// same bits as the oracle), then a stable descending radix sort of (score key, row) --
+// stability keeps equal scores in row order, i.e. the (score desc, row asc) order of
+// the reference (faiss_store.py:139-149 / the oracle).  Cost ~ one exact pass over the
+// shard plus the sort; it only runs for queries whose collect window overflowed.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "../../include/hiprag.h"
+#include "hr_common.hpp"
+
+namespace {
+
+// one wave per row; key 0 (below d2key(-inf)) marks rows that are deleted or masked out
+template <int DT>
+__global__ __launch_bounds__(256) void k_exact_all(const uint8_t* __restrict__ rows, int S, int dpad,
+                                                   const float* __restrict__ qv, const uint32_t* __restrict__ live,
+                                                   const uint32_t* __restrict__ mask, int64_t n,
+                                                   uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    uint32_t allow = live[r >> 5];
+    if (mask) allow &= mask[r >> 5];
+    if (!((allow >> (r & 31)) & 1u)) {
+        if (lane == 0) {
+            keys[r] = 0;
+            vals[r] = (uint32_t)r;
+        }
+        return;
+    }
+    double p = 0.0;
+    for (int d = lane; d < dpad; d += 64) p = p + (double)hr::load_elem<DT>(rows, S, r, d) * (double)qv[d];
+    p = hr::wave_butterfly_sum(p);
+    if (lane == 0) {
+        keys[r] = hr::d2key(p);
+        vals[r] = (uint32_t)r;
+    }
+}
+
+__global__ void k_take(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n, int m,
+                       int64_t row_offset, hr::Cand* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    if (i < n && keys[i] != 0)
+        out[i] = hr::Cand{hr::key2d(keys[i]), (int64_t)vals[i] + row_offset};
+    else
+        out[i] = hr::Cand{-__builtin_inf(), -1};
+}
+
+}  // namespace
+
+namespace hr {
+
+// scratch layout: keys_in, keys_out (8n each), vals_in, vals_out (4n each), radix-sort temp
+size_t exhaustive_scratch_bytes(int64_t n) {
+    size_t tmp = 0;
+    if (rocprim::radix_sort_pairs_desc(nullptr, tmp, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                       (uint32_t*)nullptr, (size_t)n, 0, 64) != hipSuccess)
+        tmp = 0;  // the sort call below then reports the error
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return up(8 * (size_t)n) * 2 + up(4 * (size_t)n) * 2 + up(tmp);
+}
+
+// exact top-m (score desc, row asc) of query qv over rows [0, n) into out[0..m); empty slots -inf / -1
+int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, const uint32_t* live,
+                    const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
+                    size_t scratch_bytes, hipStream_t st) {
+    if (n <= 0 || m <= 0) return HR_E_INVALID;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    uint8_t* p = (uint8_t*)scratch;
+    uint64_t* k_in = (uint64_t*)p;
+    uint64_t* k_out = (uint64_t*)(p + up(8 * (size_t)n));
+    uint32_t* v_in = (uint32_t*)(p + 2 * up(8 * (size_t)n));
+    uint32_t* v_out = (uint32_t*)(p + 2 * up(8 * (size_t)n) + up(4 * (size_t)n));
+    uint8_t* tmp = p + 2 * up(8 * (size_t)n) + 2 * up(4 * (size_t)n);
+    if (scratch_bytes < exhaustive_scratch_bytes(n)) return HR_E_INVALID;
+    size_t tmp_bytes = scratch_bytes - (size_t)(tmp - p);
+    const dim3 grid((unsigned)((n + 3) / 4));
+    switch (dtype) {
+        case HR_F32: hipLaunchKernelGGL(k_exact_all<F32>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
+        case HR_BF16: hipLaunchKernelGGL(k_exact_all<BF16>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
+        case HR_F16: hipLaunchKernelGGL(k_exact_all<F16>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
+        default: return HR_E_INVALID;
+    }
+    if (hipGetLastError() != hipSuccess) return HR_E_HIP;
+    if (rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)n, 0, 64, st) != hipSuccess)
+        return HR_E_HIP;
+    hipLaunchKernelGGL(k_take, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, k_out, v_out, n, m, row_offset,
+                       out);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
+}  // namespace hr

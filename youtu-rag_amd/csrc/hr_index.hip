@@ -54,6 +54,13 @@ struct DevBuf {
     }
 };
 
+namespace hr {  // hr_exhaustive.hip
+size_t exhaustive_scratch_bytes(int64_t n);
+int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, const uint32_t* live,
+                    const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
+                    size_t scratch_bytes, hipStream_t st);
+}  // namespace hr
+
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
 static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
 static constexpr int kScanThreads = 512;
@@ -80,7 +87,8 @@ struct hr_index {
     std::mutex mu;
     // search workspace
     DevBuf q_in, q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, cand, bound,
-        kth, fail, fb_cand, fb_bound, stage, pbuf, pcnt;
+        kth, fail, fb_cand, fb_bound, stage, pbuf, pcnt, exh;
+    int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
     int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
     std::vector<float> floor_host;
 };
@@ -194,8 +202,12 @@ static int finish_add(hr_index* h) {
     return HR_OK;
 }
 
-template <bool SYNTH>
-static int add_impl(hr_index* h, const float* rows_host, uint64_t seed, int64_t grow0, int64_t n, int64_t* first) {
+// SRC: where the fp32 rows come from (host memory staged through h->stage, the generator, or device memory).
+enum { ADD_HOST = 0, ADD_SYNTH = 1, ADD_DEVICE = 2 };
+
+template <int SRC>
+static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t grow0, int64_t n, int64_t* first) {
+    constexpr bool SYNTH = SRC == ADD_SYNTH;
     if (int rc = set_device(h)) return rc;
     if (int rc = grow(h, h->n + n)) return rc;
     const int64_t r0 = h->n;
@@ -203,11 +215,13 @@ static int add_impl(hr_index* h, const float* rows_host, uint64_t seed, int64_t 
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t m = std::min(chunk, n - off);
         const float* src = nullptr;
-        if (!SYNTH) {
+        if (SRC == ADD_HOST) {
             HIP_TRY(h->stage.ensure((size_t)m * h->dim * 4));
-            HIP_TRY(hipMemcpyAsync(h->stage.p, rows_host + off * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice,
+            HIP_TRY(hipMemcpyAsync(h->stage.p, rows + off * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice,
                                    h->stream));
             src = h->stage.as<float>();
+        } else if (SRC == ADD_DEVICE) {
+            src = rows + off * h->dim;
         }
         const dim3 grid((unsigned)((m + 3) / 4));
         int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
@@ -233,7 +247,7 @@ extern "C" int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* 
         if (first_row_out) *first_row_out = h->n;
         return HR_OK;
     }
-    return add_impl<false>(h, rows, 0, 0, n, first_row_out);
+    return add_impl<ADD_HOST>(h, rows, 0, 0, n, first_row_out);
 }
 
 extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global_row0, int64_t n,
@@ -245,7 +259,28 @@ extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global
         if (first_row_out) *first_row_out = h->n;
         return HR_OK;
     }
-    return add_impl<true>(h, nullptr, seed, global_row0, n, first_row_out);
+    return add_impl<ADD_SYNTH>(h, nullptr, seed, global_row0, n, first_row_out);
+}
+
+extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n, int64_t* first_row_out,
+                                   void* stream) {
+    if (!h || n < 0 || (n > 0 && !rows_dev)) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (n == 0) {
+        if (first_row_out) *first_row_out = h->n;
+        return HR_OK;
+    }
+    if (int rc = set_device(h)) return rc;
+    // the rows are produced on the caller's stream (e.g. the embedder's pooling kernel): order the store after it.
+    // add_impl synchronises h->stream before returning, so the caller may reuse rows_dev afterwards.
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    HIP_TRY(e);
+    return add_impl<ADD_DEVICE>(h, rows_dev, 0, 0, n, first_row_out);
 }
 
 extern "C" int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n) {
@@ -387,7 +422,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(h->q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(h->qfrag.ensure((size_t)h->S * pl.QB * 1024));
     HIP_TRY(h->qerr.ensure((size_t)Bp * 2 * 8));
-    HIP_TRY(h->mkeys.ensure((size_t)Bp * 32 * 4));
+    // row parts for the group-max bound: 32 groups bound the 32nd best, so kc > 32 needs ceil(kc/32) parts
+    const int np = mode == 0 ? (kc + 31) / 32 : 1;
+    HIP_TRY(h->mkeys.ensure((size_t)np * Bp * 32 * 4));
     HIP_TRY(h->floor_q.ensure((size_t)Bp * 4));
     HIP_TRY(h->cnt.ensure((size_t)Bp * 4));
     HIP_TRY(h->buf.ensure((size_t)Bp * kCap * 8));
@@ -402,11 +439,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad,
                            h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           h->mkeys.as<uint32_t>(), h->cnt.as<uint32_t>(), fl);
+                           h->mkeys.as<uint32_t>(), np, h->cnt.as<uint32_t>(), fl);
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
                            pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           h->mkeys.as<uint32_t>(), h->cnt.as<uint32_t>(), fl);
+                           h->mkeys.as<uint32_t>(), np, h->cnt.as<uint32_t>(), fl);
     HIP_TRY(hipGetLastError());
 
     // floors: padded queries never collect; mode 1 uses kth - E (computed on the host from qerr)
@@ -446,6 +483,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.qfrag = h->qfrag.as<uint16_t>();
     a.S = h->S;
     a.mkeys = h->mkeys.as<uint32_t>();
+    a.np = np;
+    a.part_tiles = np > 1 ? std::max<int64_t>(1, (n_tiles + np - 1) / np) : ((int64_t)1 << 62);
+    a.pstride = (int64_t)Bp * 32;
     a.floor_q = h->floor_q.as<float>();
     a.cnt = h->cnt.as<uint32_t>();
     a.buf = h->buf.as<float2>();
@@ -500,7 +540,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const bool priv = a.private_bufs && n_tiles > 0;
     hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st, h->cnt.as<uint32_t>(), h->buf.as<float2>(),
                        kCap, priv ? h->pcnt.as<uint32_t>() : nullptr, priv ? h->pbuf.as<float2>() : nullptr,
-                       (int)h->last_W, kCapW, Bp, h->mkeys.as<uint32_t>(), h->floor_q.as<float>(), a.use_groups, B, kc_sel,
+                       (int)h->last_W, kCapW, Bp, h->mkeys.as<uint32_t>(), np, h->floor_q.as<float>(), a.use_groups, B, kc_sel,
                        h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), h->bound_approx.as<float>(),
                        h->overflow.as<int>());
     HIP_TRY(hipGetLastError());
@@ -521,10 +561,17 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         HIP_TRY(hipMemcpyAsync(ovf.data(), h->overflow.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(selc.data(), h->sel_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        std::vector<double> bh((size_t)B);
+        std::vector<double> bh((size_t)B, -INFINITY);
         for (int b = 0; b < B; ++b) {
-            bool full = ovf[(size_t)b] || selc[(size_t)b] >= cap_out;
-            bh[(size_t)b] = full ? INFINITY : -INFINITY;
+            if (!(ovf[(size_t)b] || selc[(size_t)b] >= cap_out)) continue;
+            // the window held more rows than the buffer: exact top-cap_out of the whole shard instead
+            // (complete by construction, so the bound stays -inf)
+            HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
+            if (int rc2 = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, h->q32.as<float>() + (int64_t)b * h->dpad,
+                                          h->live, (const uint32_t*)mask_dev, h->n, row_offset, cap_out,
+                                          cand_out + (int64_t)b * cap_out, h->exh.p, h->exh.bytes, st))
+                return set_err(rc2, "exhaustive exact pass failed");
+            h->n_exhaustive++;
         }
         HIP_TRY(hipMemcpyAsync(bound_out, bh.data(), (size_t)B * 8, hipMemcpyHostToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
@@ -547,7 +594,7 @@ static int shard_search(hr_index* h, const float* q_dev, int B, int kc, const ui
 
 static int validate_search(hr_index* h, int B, int k) {
     if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
-    if (k <= 0 || k > HR_MAX_K) return set_err(HR_E_INVALID, "k must be in [1, 32]");
+    if (k <= 0 || k > HR_MAX_K) return set_err(HR_E_INVALID, "k must be in [1, HR_MAX_K]");
     return HR_OK;
 }
 
@@ -574,7 +621,7 @@ static constexpr int kFallbackCap = 512;
 static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
                               int64_t* r_out, hipStream_t st) {
     if (int rc = validate_search(h, B, k)) return rc;
-    const int kc = HR_MAX_K;
+    const int kc = hr_kc_for_k(k);
     HIP_TRY(h->cand.ensure((size_t)B * kc * sizeof(Cand)));
     HIP_TRY(h->bound.ensure((size_t)B * 8));
     HIP_TRY(h->kth.ensure((size_t)B * 8));
@@ -662,7 +709,7 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
     if (int rc = validate_search(h, B, k)) return rc;
-    if (kc < k || kc > HR_MAX_K) return set_err(HR_E_INVALID, "kc must be in [k, 32]");
+    if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
     return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st);
 }
@@ -719,11 +766,11 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
                            h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           nullptr, nullptr, nullptr);
+                           nullptr, 1, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
                            h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           nullptr, nullptr, nullptr);
+                           nullptr, 1, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
     const int lds = scan_lds_bytes(h, pl.QB);
     int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
@@ -872,7 +919,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     for (DevBuf* b : {&h->q_in, &h->q32, &h->qfrag, &h->qerr, &h->mkeys, &h->floor_q, &h->cnt, &h->buf, &h->sel_rows,
                       &h->sel_cnt, &h->bound_approx, &h->overflow, &h->cand, &h->bound, &h->kth, &h->fail,
-                      &h->fb_cand, &h->fb_bound, &h->stage, &h->pbuf, &h->pcnt})
+                      &h->fb_cand, &h->fb_bound, &h->stage, &h->pbuf, &h->pcnt, &h->exh})
         b->release();
     for (auto* list : {&h->ev_free})
         for (auto& ev : *list)
@@ -950,4 +997,6 @@ extern "C" int hr_device_count(int* n_out) {
 }
 
 extern "C" const char* hr_last_error(void) { return g_err.c_str(); }
-extern "C" int hr_abi_version(void) { return 1; }
+extern "C" int hr_abi_version(void) { return 2; }
+
+extern "C" int hr_kc_for_k(int k) { return k <= 32 ? 32 : std::min(HR_MAX_KC, (k + 16 + 31) / 32 * 32); }

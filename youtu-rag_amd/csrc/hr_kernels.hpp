@@ -22,25 +22,6 @@
 
 namespace hr {
 
-// byte offset of k-step chunk (tile, s) for lane l; stride 1 KiB (16-bit) / 2 KiB (fp32)
-template <int DT>
-__device__ __host__ inline size_t chunk_bytes() { return DT == F32 ? 2048 : 1024; }
-
-// element (row r, column d) of the tiled corpus, as float
-template <int DT>
-__device__ inline float load_elem(const uint8_t* base, int S, int64_t r, int d) {
-    int64_t chunk = (r >> 5) * S + (d >> 4);
-    int lane = (int)(r & 31) + 32 * ((d >> 3) & 1);
-    int j = d & 7;
-    if (DT == F32) {
-        const float* p = (const float*)(base + chunk * 2048 + (j >> 2) * 1024 + lane * 16);
-        return p[j & 3];
-    } else {
-        const uint16_t* p = (const uint16_t*)(base + chunk * 1024 + lane * 16);
-        return DT == BF16 ? bf16_to_f32(p[j]) : f16_to_f32(p[j]);
-    }
-}
-
 // ---------------------------------------------------------------- K1+K2: store rows
 // One wave per row.  Phase 1: canonical fp64 norm² (lane-strided + butterfly, exactly the
 // oracle's order).  Phase 2: lane c owns 8-element chunks, scales (cosine), quantises
@@ -117,7 +98,7 @@ template <int MT>
 __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int B, int Bp, int dim, int dpad, int S,
                                                 int QB, int metric, float* __restrict__ q32,
                                                 uint16_t* __restrict__ qfrag, double* __restrict__ qerr,
-                                                uint32_t* __restrict__ mkeys, uint32_t* __restrict__ cnt,
+                                                uint32_t* __restrict__ mkeys, int np, uint32_t* __restrict__ cnt,
                                                 float* __restrict__ floor_q) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -125,7 +106,8 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     // per-batch scratch of this query (replaces two memsets and an H2D copy per batch):
     // group maxima -> -inf, candidate count -> 0, floor -> -inf (+inf for padding rows);
     // floor_q == nullptr: the caller uploaded explicit floors (collect mode)
-    if (mkeys && lane < 32) mkeys[b * 32 + lane] = HR_KEY_NEG_INF;
+    if (mkeys && lane < 32)
+        for (int p = 0; p < np; ++p) mkeys[((int64_t)p * Bp + b) * 32 + lane] = HR_KEY_NEG_INF;
     if (lane == 0) {
         if (cnt) cnt[b] = 0;
         if (floor_q) floor_q[b] = b < B ? -__builtin_inff() : __builtin_inff();
@@ -176,7 +158,10 @@ struct ScanArgs {
     int S;
     int64_t n_units;         // tiles (FILTER) or sample tiles (SAMPLE)
     int64_t sample_stride;   // SAMPLE: tile = unit * stride
-    uint32_t* mkeys;         // [QB*32 queries][32 groups] group-max keys (a wave-wide access spans 2 lines)
+    uint32_t* mkeys;         // [np parts][QB*32 queries][32 groups] group-max keys (a wave access spans 2 lines)
+    int np;                  // row parts: group (p, g) = rows of tile part p with row % 32 == g (k > 32)
+    int64_t part_tiles;      // tiles per part (part of tile t = t / part_tiles)
+    int64_t pstride;         // words between parts of mkeys (QB*32*32)
     const float* floor_q;    // [QB*32] per-query floor (collect mode / +inf for padding)
     int use_groups;          // FILTER: threshold = max(floor, min_g M[q][g]) if set, else floor
     uint32_t* cnt;           // [QB*32] candidate counts (shared-buffer mode)
@@ -294,9 +279,14 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     float th[QB][16], gmax[QB][16];
     // this lane's group column of the group-max table, one base per query block; the per-register
     // query offset 32*((i&3) + 8(i>>2)) words stays under the 4 KiB immediate-offset range
+    // With np > 1 parts (top-k beyond 32) the groups are (part, row % 32): 32*np disjoint row sets,
+    // so min over all of them bounds the (32*np)-th best score; gkq points at this wave's current
+    // part and the other parts sit at scalar offsets (p - part) * pstride.
+    int64_t part = (u0 * stride) / a.part_tiles;
+    int64_t part_end = (part + 1) * a.part_tiles;
     uint32_t* gkq[QB];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) gkq[qb] = a.mkeys + (qb * 32 + 4 * half) * 32 + g;
+    for (int qb = 0; qb < QB; ++qb) gkq[qb] = a.mkeys + part * a.pstride + (qb * 32 + 4 * half) * 32 + g;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
@@ -332,20 +322,51 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int q = acc_query(qb, i, half);
-                float f = key2f(key[qb][i] > HR_KEY_NEG_INF ? key[qb][i] : HR_KEY_NEG_INF);
-                if (publish && a.publish && gmax[qb][i] > f) {
+                key[qb][i] = key[qb][i] > HR_KEY_NEG_INF ? key[qb][i] : HR_KEY_NEG_INF;
+                if (publish && a.publish && gmax[qb][i] > key2f(key[qb][i])) {
                     if (a.publish == 2)
                         __hip_atomic_store(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     else
                         atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
-                    f = gmax[qb][i];
+                    key[qb][i] = f2key(gmax[qb][i]);
                 }
+            }
+        // the other parts' groups of this lane (keys order like floats: min of keys = min of scores)
+        for (int p = 0; p < a.np; ++p) {
+            if (p == part) continue;
+            const int64_t off = (p - part) * a.pstride;
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    uint32_t k2 = __hip_atomic_load(gkq[qb] + off + 32 * ((i & 3) + 8 * (i >> 2)), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                    k2 = k2 > HR_KEY_NEG_INF ? k2 : HR_KEY_NEG_INF;
+                    key[qb][i] = key[qb][i] < k2 ? key[qb][i] : k2;
+                }
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = acc_query(qb, i, half);
+                float f = key2f(key[qb][i]);
 #pragma unroll
                 for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
                 gmax[qb][i] = -__builtin_inff();
                 th[qb][i] = fmaxf(th[qb][i], fmaxf(f, a.floor_q[q]));
+            }
+    };
+    // publish the group maxima of the part being left (or at the end of a SAMPLE range)
+    auto flush = [&]() {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (gmax[qb][i] > -__builtin_inff())
+                    atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
+                gmax[qb][i] = -__builtin_inff();
             }
     };
     if (FILTER) refresh(false);
@@ -360,6 +381,14 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     for (int64_t u = u0; u < u1; ++u) {
         const int64_t t = u * stride;
         const int64_t tn = (u + 1 < u1) ? (u + 1) * stride : t;
+        if (t >= part_end) {  // wave-uniform; never taken with one part
+            if (MODE != SCAN_COLLECT && a.use_groups) flush();
+            const int64_t np_ = t / a.part_tiles;
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) gkq[qb] += (np_ - part) * a.pstride;
+            part = np_;
+            part_end = (part + 1) * a.part_tiles;
+        }
         f32x16 acc[QB];
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
@@ -436,14 +465,7 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     }
 
     if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;
-    if (!FILTER) {  // SAMPLE: publish the group maxima
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (gmax[qb][i] > -__builtin_inff())
-                    atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
-    }
+    if (!FILTER) flush();  // SAMPLE: publish the group maxima
 }
 
 
@@ -506,7 +528,7 @@ __device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of t
 __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
                                                  int cap, const uint32_t* __restrict__ pcnt,
                                                  const float2* __restrict__ pbuf, int W, int capw, int Bp,
-                                                 const uint32_t* __restrict__ mkeys,
+                                                 const uint32_t* __restrict__ mkeys, int np,
                                                  const float* __restrict__ floor_q, int use_groups, int B, int kc,
                                                  uint32_t* __restrict__ sel_rows, int* __restrict__ sel_cnt,
                                                  float* __restrict__ bound_approx, int* __restrict__ overflow) {
@@ -520,13 +542,13 @@ __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cn
     if (q >= B) return;
     const int tid = threadIdx.x;
     if (tid < 64) {
-        float f = -__builtin_inff();
-        if (use_groups && tid < 32) {
-            uint32_t k = mkeys[q * 32 + tid];
-            f = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
-        } else if (use_groups) {
-            f = __builtin_inff();
-        }
+        // min over the 32*np group maxima of this query (mkeys [np][Bp][32])
+        float f = use_groups ? __builtin_inff() : -__builtin_inff();
+        if (use_groups)
+            for (int j = tid; j < np * 32; j += 64) {
+                uint32_t k = mkeys[((int64_t)(j >> 5) * Bp + q) * 32 + (j & 31)];
+                f = fminf(f, key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF));
+            }
         for (int off = 32; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
         if (tid == 0) {
             thr_sh = fmaxf(f, floor_q[q]);

@@ -18,19 +18,27 @@ LIB_PATH = os.path.join(_HERE, "libhiprag.so")
 
 DTYPES = {"f32": 0, "float32": 0, "fp32": 0, "bf16": 1, "bfloat16": 1, "f16": 2, "float16": 2, "fp16": 2}
 METRICS = {"cosine": 0, "ip": 1, "dot": 1, "euclidean": 2, "l2": 2}
-HR_MAX_K = 32
+HR_MAX_K = 128   # include/hiprag.h
+HR_MAX_KC = 160
+
+
+def kc_for_k(k: int) -> int:
+    """Per-shard candidate count for top-k (hr_kc_for_k): 32 for k <= 32, else k + 16 rounded up to 32."""
+    return 32 if k <= 32 else min(HR_MAX_KC, (k + 16 + 31) // 32 * 32)
+
+
 CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand
 
 E_INVALID, E_HIP, E_UNSUPPORTED, E_OVERFLOW, E_IO = -1, -2, -3, -4, -5
 
 # every symbol include/hiprag.h declares (checked by tests/test_native_abi.py)
 EXPORTS = [
-    "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_remove",
-    "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows", "hr_index_save",
-    "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_index_take_scan_times", "hr_index_last_scan_ms", "hr_device_count", "hr_index_debug_approx",
-    "hr_index_last_candidates", "hr_last_error",
-    "hr_abi_version",
+    "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_add_device",
+    "hr_index_remove", "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows",
+    "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_index_take_scan_times", "hr_index_last_scan_ms",
+    "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
+    "hr_kc_for_k",
 ]
 
 _lib = None
@@ -67,6 +75,7 @@ def load_library(path: str | None = None):
             "hr_index_reserve": [vp, i64],
             "hr_index_add": [vp, vp, i64, vp],
             "hr_index_add_synthetic": [vp, u64, i64, i64, vp],
+            "hr_index_add_device": [vp, vp, i64, vp, vp],
             "hr_index_remove": [vp, vp, i64],
             "hr_index_search": [vp, vp, i32, i32, vp, vp, vp],
             "hr_index_search_device": [vp, vp, i32, i32, vp, vp, vp, vp],
@@ -93,6 +102,8 @@ def load_library(path: str | None = None):
         L.hr_last_error.argtypes = []
         L.hr_last_error.restype = ctypes.c_char_p
         L.hr_abi_version.restype = i32
+        L.hr_kc_for_k.argtypes = [i32]
+        L.hr_kc_for_k.restype = i32
         _lib = L
         return L
 
@@ -157,6 +168,13 @@ class NativeIndex:
             raise ValueError(f"rows must be (n, {self.dim}) float32")
         first = ctypes.c_int64(0)
         _check(self.lib.hr_index_add(self._h, _ptr(rows), rows.shape[0], ctypes.byref(first)))
+        return first.value
+
+    def add_device(self, rows_ptr: int, n: int, stream: int = 0) -> int:
+        """Add n fp32 rows (row-major, dim wide) already in device memory; ordered after `stream`."""
+        first = ctypes.c_int64(0)
+        _check(self.lib.hr_index_add_device(self._h, ctypes.c_void_p(int(rows_ptr)), int(n), ctypes.byref(first),
+                                            ctypes.c_void_p(int(stream))))
         return first.value
 
     def add_synthetic(self, seed: int, global_row0: int, n: int) -> int:

@@ -46,8 +46,8 @@ class _Slot:
 class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
-    def __init__(self, index, row_offset: int, max_batch: int, kc: int = _native.HR_MAX_K, group=None,
-                 device=None, depth: int = 2):
+    def __init__(self, index, row_offset: int, max_batch: int, kc: int | None = None, group=None,
+                 device=None, depth: int = 2, max_k: int = 32):
         import torch
         import torch.distributed as dist
 
@@ -56,7 +56,7 @@ class ShardedSearch:
         self.row_offset = int(row_offset)
         self.group = group
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.kc = int(kc)
+        self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k)  # candidates per shard per query
         self.max_batch = int(max_batch)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         pinned = self.device.type == "cuda"

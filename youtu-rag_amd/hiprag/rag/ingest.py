@@ -1,0 +1,101 @@
+"""KB ingest slice on one GPU: split -> embed (in-process) -> add to the HIP index (config 4).
+
+Restates BaseProcessor._chunk_and_store (utu/rag/knowledge_builder/processors.py:340-421):
+for each document, old chunks with the same document_id are deleted first (:363-369),
+the text is split with the configured RecursiveTextSplitter (:385), chunk i gets
+id f"{document.id}_chunk_{i}", document metadata without "_"-prefixed keys plus
+index_type="index_content" unless present, updated with the call's extra metadata
+(:387-407), and the chunk texts are embedded and added to the store (:412-418).
+
+What changes is where the vectors go: with the in-process TorchRocmEmbedder, texts of
+many documents are packed into full embedder batches and each batch's (B, H) float32
+device tensor is appended to the index by hr_index_add_device -- the embeddings never
+visit the host.  Any other BaseEmbedder (host lists) falls back to add_chunks.
+HierarchicalMarkdownSplitter documents ("_use_hierarchical_splitter") are outside
+this slice and are rejected loudly.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Any
+
+from .base import BaseEmbedder, Chunk, Document
+from .chunker import RecursiveTextSplitter
+from .config import ChunkingConfig
+
+logger = logging.getLogger(__name__)
+
+
+def make_chunks(document: Document, texts: list[str], metadata: dict[str, Any] | None = None) -> list[Chunk]:
+    """Chunk records of one document exactly as processors.py:387-407 builds them."""
+    chunks = []
+    for i, text in enumerate(texts):
+        meta = {k: v for k, v in (document.metadata or {}).items() if not k.startswith("_")}
+        meta.setdefault("index_type", "index_content")
+        chunks.append(Chunk(id=f"{document.id}_chunk_{i}", document_id=document.id, content=text, chunk_index=i,
+                            metadata=meta))
+    if metadata:
+        for c in chunks:
+            c.metadata.update(metadata)
+    return chunks
+
+
+class GpuIngestor:
+    """split -> embed -> add for a HipVectorStore, batching embedder work across documents."""
+
+    def __init__(self, vector_store, embedder: BaseEmbedder, chunker=None, chunking: ChunkingConfig | None = None,
+                 embed_batch: int | None = None):
+        self.vector_store = vector_store
+        self.embedder = embedder
+        self.chunker = chunker or RecursiveTextSplitter(chunking or ChunkingConfig())
+        self.embed_batch = int(embed_batch or getattr(embedder, "batch_size", 64))
+        self._device = hasattr(embedder, "embed_texts_device") and hasattr(vector_store, "add_chunks_device")
+
+    def split(self, document: Document, metadata: dict[str, Any] | None = None) -> list[Chunk]:
+        if (document.metadata or {}).get("_use_hierarchical_splitter", False):
+            raise NotImplementedError("HierarchicalMarkdownSplitter documents are outside the GPU ingest slice")
+        return make_chunks(document, self.chunker.split_text(document.content, document.metadata), metadata)
+
+    async def _store(self, chunks: list[Chunk]) -> int:
+        if not chunks:
+            return 0
+        texts = [c.content for c in chunks]
+        if self._device:
+            emb = self.embedder.embed_texts_device(texts)
+            return self.vector_store.add_chunks_device(chunks, emb)
+        for c, e in zip(chunks, await self.embedder.embed_texts(texts)):
+            c.embedding = e
+        await self.vector_store.add_chunks(chunks)
+        return len(chunks)
+
+    async def chunk_and_store(self, document: Document, metadata: dict[str, Any] | None = None) -> int:
+        """One document (BaseProcessor._chunk_and_store).  Returns the number of chunks created."""
+        return await self.ingest([document], metadata)
+
+    async def ingest(self, documents: list[Document], metadata: dict[str, Any] | None = None) -> int:
+        """Many documents; embedder batches span document boundaries.  Returns chunks created."""
+        created, pending = 0, []
+        with self.vector_store.deferred_save():
+            for doc in documents:
+                if any(c.document_id == doc.id for c in pending):  # same id twice: store the first copy first
+                    await self._store(pending)
+                    pending = []
+                created += await self._one(doc, metadata, pending)
+                while len(pending) >= self.embed_batch:
+                    await self._store(pending[:self.embed_batch])
+                    pending = pending[self.embed_batch:]
+            await self._store(pending)
+        return created
+
+    async def _one(self, doc: Document, metadata, pending: list[Chunk]) -> int:
+        try:
+            n_old = await self.vector_store.delete_by_document_id(doc.id)
+            if n_old:
+                logger.info("deleted %d old chunks for document %s", n_old, doc.id)
+        except Exception as e:  # the reference carries on (processors.py:367-369)
+            logger.warning("failed to delete old chunks for %s: %s", doc.id, e)
+        chunks = self.split(doc, metadata)
+        if not chunks:
+            logger.warning("no chunks created for document %s", doc.id)
+        pending.extend(chunks)
+        return len(chunks)

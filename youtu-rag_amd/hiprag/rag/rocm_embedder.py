@@ -1,0 +1,211 @@
+"""In-process PyTorch-ROCm embedder behind BaseEmbedder.
+
+Replaces the reference's HTTP hop to its embedding server (ServiceEmbedder,
+utu/rag/embeddings/service_embedder.py:73-177) with the server's own computation
+run in this process (LLMEmbeddingModel, docs/content/docs/en/youtu-embedding/
+deploying-locally.mdx:41-126):
+
+* tokenise with padding=True, truncation=True, max_length, add_special_tokens=True
+  (mdx:83-90); queries are prefixed with
+  "Instruction: {query_instruction} \\nQuery:" and passages with "" (mdx:64-71, :118-126);
+* transformer forward on the GPU (PyTorch-ROCm -- the only torch compute here);
+* the first len(tokenizer(instruction)["input_ids"]) mask positions are zeroed --
+  with add_special_tokens=True, so even the empty passage instruction masks the
+  tokeniser's special tokens, as the reference does (mdx:98-107);
+* masked mean-pool + F.normalize run as the K7 HIP kernel (hr_pool_normalize,
+  mdx:75-79, :114-115) straight from the model's hidden-state tensor.
+
+``embed_texts_device`` keeps the vectors on the GPU so the ingest path
+(hiprag.rag.ingest) can hand them to the index without a host round trip.
+
+No checkpoint can be downloaded here: ``model_name_or_path`` must be a local
+directory (AutoModel/AutoTokenizer with local_files_only); without one a
+random-init BERT of the named preset shape is built from a config object with a
+seeded init, with the offline HashWordTokenizer below.
+"""
+from __future__ import annotations
+
+import os
+import re
+import zlib
+
+from .. import _native
+from .base import BaseEmbedder
+
+DEFAULT_QUERY_INSTRUCTION = "Given a search query, retrieve passages that answer the question"
+
+# BertConfig shapes of the models the reference configs name (bge-base 768-d,
+# bge-large 1024-d).
+PRESETS = {
+    "bge-base": dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072),
+    "bge-large": dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096),
+    "tiny": dict(hidden_size=256, num_hidden_layers=2, num_attention_heads=4, intermediate_size=512),
+}
+
+_TORCH_DTYPES = {"float32": "float32", "fp32": "float32", "bfloat16": "bfloat16", "bf16": "bfloat16",
+                 "float16": "float16", "fp16": "float16"}
+_K7_DTYPE = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
+
+
+class HashWordTokenizer:
+    """Deterministic offline tokenizer for random-init models (no vocab files exist offline).
+
+    Lower-cased words and punctuation marks (``\\w+|[^\\w\\s]``) hash (crc32) into
+    [first_id, vocab_size); BERT's special ids ([PAD]=0, [CLS]=101, [SEP]=102).  The
+    call signature and padding/truncation behaviour are the subset of Hugging Face's
+    tokenizer __call__ the embedder uses: right padding to the longest sequence,
+    truncation to max_length counting the special tokens, lists or "pt" tensors.
+    """
+
+    pad_token_id, cls_token_id, sep_token_id, first_id = 0, 101, 102, 1000
+    _word = re.compile(r"\w+|[^\w\s]", re.UNICODE)
+
+    def __init__(self, vocab_size: int = 30522):
+        self.vocab_size = int(vocab_size)
+
+    def _ids(self, text: str) -> list[int]:
+        span = self.vocab_size - self.first_id
+        return [self.first_id + zlib.crc32(w.encode("utf-8")) % span for w in self._word.findall(text.lower())]
+
+    def __call__(self, text, padding=False, truncation=False, max_length=None, return_tensors=None,
+                 add_special_tokens=True, **_):
+        single = isinstance(text, str)
+        texts = [text] if single else list(text)
+        seqs = []
+        for t in texts:
+            ids = self._ids(t)
+            if truncation and max_length is not None:
+                ids = ids[:max(0, int(max_length) - (2 if add_special_tokens else 0))]
+            seqs.append([self.cls_token_id, *ids, self.sep_token_id] if add_special_tokens else ids)
+        width = max((len(s) for s in seqs), default=0) if padding else None
+        input_ids, mask = [], []
+        for s in seqs:
+            pad = (width - len(s)) if width is not None else 0
+            input_ids.append(s + [self.pad_token_id] * pad)
+            mask.append([1] * len(s) + [0] * pad)
+        if return_tensors == "pt":
+            import torch
+
+            return {"input_ids": torch.tensor(input_ids, dtype=torch.long),
+                    "attention_mask": torch.tensor(mask, dtype=torch.long)}
+        if single:
+            return {"input_ids": input_ids[0], "attention_mask": mask[0]}
+        return {"input_ids": input_ids, "attention_mask": mask}
+
+
+def build_random_bert(preset: str = "bge-large", seed: int = 0, **overrides):
+    """Seeded random-init BertModel of a named shape (no weights exist offline)."""
+    import torch
+    from transformers import BertConfig, BertModel
+
+    cfg = dict(PRESETS[preset])
+    cfg.update(overrides)
+    config = BertConfig(vocab_size=30522, max_position_embeddings=512, **cfg)
+    fork = torch.random.fork_rng(devices=[])
+    with fork:
+        torch.manual_seed(seed)
+        model = BertModel(config, add_pooling_layer=False)
+    return model
+
+
+class TorchRocmEmbedder(BaseEmbedder):
+    """BaseEmbedder running the embedding model in-process on an MI355X (provider "rocm")."""
+
+    def __init__(self, model_name_or_path: str | None = None, *, model=None, tokenizer=None, preset: str = "bge-large",
+                 batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
+                 query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
+                 trust_remote_code: bool = False, **_ignored):
+        import torch
+
+        self.torch = torch
+        self.device = torch.device(device) if device is not None else torch.device("cuda", gpu_id)
+        if dtype not in _TORCH_DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(_TORCH_DTYPES)}")
+        self.dtype_name = _TORCH_DTYPES[dtype]
+        tdt = getattr(torch, self.dtype_name)
+        if model is None:
+            if model_name_or_path and os.path.isdir(model_name_or_path):
+                from transformers import AutoModel, AutoTokenizer
+
+                model = AutoModel.from_pretrained(model_name_or_path, local_files_only=True,
+                                                  trust_remote_code=trust_remote_code)
+                tokenizer = tokenizer or AutoTokenizer.from_pretrained(
+                    model_name_or_path, padding_side="right", local_files_only=True,
+                    trust_remote_code=trust_remote_code)
+            elif model_name_or_path:
+                raise FileNotFoundError(f"{model_name_or_path!r} is not a local model directory (no downloads)")
+            else:
+                model = build_random_bert(preset, seed)
+        self.tokenizer = tokenizer if tokenizer is not None else HashWordTokenizer(
+            getattr(getattr(model, "config", None), "vocab_size", 30522))
+        self.model = model.to(self.device, tdt).eval()
+        max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
+        self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
+        self.batch_size = int(batch_size)
+        if self.batch_size < 1:
+            raise ValueError("batch_size must be at least one")
+        self.query_instruction = (f"Instruction: {query_instruction} \nQuery:" if query_instruction else "Query:")
+        self.doc_instruction = ""
+        self.dim = int(getattr(getattr(model, "config", None), "hidden_size", 0)) or None
+
+    # ------------------------------------------------------------------ core
+    def _n_instruction_tokens(self, instruction: str) -> int:
+        ids = self.tokenizer(instruction, padding=False, truncation=True, max_length=self.max_length,
+                             add_special_tokens=True)["input_ids"]
+        return len(ids)
+
+    def _pool(self, hidden, mask, n_instr: int):
+        """K7: masked mean-pool + L2 normalise on the GPU -> (B, H) float32."""
+        torch = self.torch
+        B, T, H = hidden.shape
+        out = torch.empty((B, H), dtype=torch.float32, device=hidden.device)
+        _native.pool_normalize(hidden.data_ptr(), _K7_DTYPE[self.dtype_name], mask.data_ptr(), B, T, H, n_instr,
+                               out.data_ptr(), torch.cuda.current_stream(hidden.device).cuda_stream)
+        return out
+
+    def encode(self, sentences: list[str], instruction: str):
+        """One batch -> (B, H) float32 device tensor (LLMEmbeddingModel.encode, mdx:81-116)."""
+        torch = self.torch
+        inputs = self.tokenizer(list(sentences), padding=True, truncation=True, return_tensors="pt",
+                                max_length=self.max_length, add_special_tokens=True)
+        inputs = {k: v.to(self.device, non_blocking=True) for k, v in inputs.items()}
+        with torch.inference_mode():
+            hidden = self.model(**inputs)[0]
+            if hidden.dtype != getattr(torch, self.dtype_name):
+                hidden = hidden.to(getattr(torch, self.dtype_name))
+            hidden = hidden.contiguous()
+            mask = inputs["attention_mask"].to(torch.int32).contiguous()
+            return self._pool(hidden, mask, self._n_instruction_tokens(instruction))
+
+    def _encode_all(self, texts: list[str], prefix: str, instruction: str):
+        torch = self.torch
+        texts = [f"{prefix}{t}" for t in texts]
+        parts = [self.encode(texts[i:i + self.batch_size], instruction) for i in range(0, len(texts), self.batch_size)]
+        if not parts:
+            return torch.empty((0, self.dim or 0), dtype=torch.float32, device=self.device)
+        return parts[0] if len(parts) == 1 else torch.cat(parts)
+
+    def encode_queries(self, queries):
+        queries = queries if isinstance(queries, list) else [queries]
+        return self._encode_all(queries, self.query_instruction, self.query_instruction)
+
+    def encode_passages(self, passages):
+        passages = passages if isinstance(passages, list) else [passages]
+        return self._encode_all(passages, self.doc_instruction, self.doc_instruction)
+
+    # ------------------------------------------------------------- BaseEmbedder
+    def embed_texts_device(self, texts: list[str]):
+        """Passages -> (n, H) float32 device tensor (no host copy; used by the GPU ingest path)."""
+        return self.encode_passages(list(texts))
+
+    def embed_queries_device(self, queries: list[str]):
+        return self.encode_queries(list(queries))
+
+    async def embed_texts(self, texts: list[str]) -> list[list[float]]:
+        return self.encode_passages(list(texts)).cpu().tolist()
+
+    async def embed_query(self, query: str) -> list[float]:
+        return self.encode_queries([query])[0].cpu().tolist()
+
+    async def embed_queries(self, queries: list[str]) -> list[list[float]]:
+        return self.encode_queries(list(queries)).cpu().tolist()

@@ -20,6 +20,7 @@ id_to_idx / idx_to_chunk (faiss_store.py:52-54, :112-121).  Persistence:
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import logging
 import os
@@ -56,7 +57,9 @@ class HipVectorStore(BaseVectorStore):
         self.dim: int | None = None
         self._records: list[dict | None] = []
         self._id_to_row: dict[str, int] = {}
+        self._doc_rows: dict[str, list[int]] = {}
         self._cols = F.MetadataColumns()
+        self._defer, self._dirty = 0, False
         if self.persist:
             self._load_if_present()
 
@@ -79,12 +82,28 @@ class HipVectorStore(BaseVectorStore):
         for row, rec in enumerate(records):
             if rec is not None:
                 self._id_to_row[rec["id"]] = row
+                self._doc_rows.setdefault(rec["document_id"], []).append(row)
         self._cols.append([(rec or {}).get("metadata", {}) for rec in records])
         logger.info("loaded %d chunks from %s", len(self._id_to_row), idx_path)
+
+    @contextlib.contextmanager
+    def deferred_save(self):
+        """Write the persist files once at the end of a block of adds/deletes (bulk ingest)."""
+        self._defer += 1
+        try:
+            yield self
+        finally:
+            self._defer -= 1
+            if self._defer == 0 and self._dirty:
+                self._save()
 
     def _save(self):
         if not self.persist or self._index is None:
             return
+        if self._defer:
+            self._dirty = True
+            return
+        self._dirty = False
         os.makedirs(self.config.persist_directory, exist_ok=True)
         idx_path, rows_path = self._paths()
         self._index.save(idx_path)
@@ -96,30 +115,26 @@ class HipVectorStore(BaseVectorStore):
         os.replace(tmp, rows_path)
 
     # ---------------------------------------------------------------- writes
-    async def add_chunks(self, chunks: list[Chunk]) -> None:
-        if not chunks:
-            return
+    def _fresh(self, chunks: list[Chunk]) -> list[int]:
+        """Indices of chunks whose id is not stored yet (chroma skips existing ids, chroma_store.py:64-88)."""
         ids = [c.id for c in chunks]
         if len(set(ids)) != len(ids):
             raise ValueError("duplicate chunk ids inside one add_chunks call")
-        fresh = [c for c in chunks if c.id not in self._id_to_row]
-        if len(fresh) < len(chunks):
-            logger.warning("skipping %d chunk(s) whose id already exists", len(chunks) - len(fresh))
-        if not fresh:
-            return
-        if any(c.embedding is None for c in fresh):
-            raise ValueError("every chunk needs an embedding")
-        emb = np.asarray([c.embedding for c in fresh], dtype=np.float32)
-        if emb.ndim != 2:
-            raise ValueError("embeddings must all have the same dimension")
+        keep = [i for i, c in enumerate(chunks) if c.id not in self._id_to_row]
+        if len(keep) < len(chunks):
+            logger.warning("skipping %d chunk(s) whose id already exists", len(chunks) - len(keep))
+        return keep
+
+    def _ensure_index(self, dim: int):
         if self._index is None:
-            self.dim = emb.shape[1]
+            self.dim = int(dim)
             self._index = self._factory(self.dim)
             if self.capacity:
                 self._index.reserve(self.capacity)
-        elif emb.shape[1] != self.dim:
-            raise ValueError(f"embedding dim {emb.shape[1]} != collection dim {self.dim}")
-        first = self._index.add(emb)
+        elif dim != self.dim:
+            raise ValueError(f"embedding dim {dim} != collection dim {self.dim}")
+
+    def _register(self, fresh: list[Chunk], first: int):
         metas = []
         for i, c in enumerate(fresh):
             meta = {"document_id": c.document_id, "chunk_index": c.chunk_index,
@@ -129,10 +144,47 @@ class HipVectorStore(BaseVectorStore):
             assert first + i == len(self._records)
             self._records.append(rec)
             self._id_to_row[c.id] = first + i
+            self._doc_rows.setdefault(c.document_id, []).append(first + i)
             metas.append(meta)
         self._cols.append(metas)
         self._save()
         logger.info("added %d chunks to %s", len(fresh), self.config.collection_name)
+
+    async def add_chunks(self, chunks: list[Chunk]) -> None:
+        if not chunks:
+            return
+        fresh = [chunks[i] for i in self._fresh(chunks)]
+        if not fresh:
+            return
+        if any(c.embedding is None for c in fresh):
+            raise ValueError("every chunk needs an embedding")
+        emb = np.asarray([c.embedding for c in fresh], dtype=np.float32)
+        if emb.ndim != 2:
+            raise ValueError("embeddings must all have the same dimension")
+        self._ensure_index(emb.shape[1])
+        self._register(fresh, self._index.add(emb))
+
+    def add_chunks_device(self, chunks: list[Chunk], embeddings, stream: int | None = None) -> int:
+        """add_chunks for embeddings that are already on the GPU (the in-process embedder's output):
+        `embeddings` is a (len(chunks), dim) float32 device tensor; the vectors never visit the host
+        (replaces embed_texts -> add_chunks, processors.py:413-418).  Returns the number added."""
+        import torch
+
+        if not chunks:
+            return 0
+        if embeddings.dim() != 2 or embeddings.shape[0] != len(chunks) or not embeddings.is_cuda:
+            raise ValueError("embeddings must be a (len(chunks), dim) device tensor")
+        keep = self._fresh(chunks)
+        if not keep:
+            return 0
+        emb = embeddings if len(keep) == len(chunks) else embeddings[torch.as_tensor(keep, device=embeddings.device)]
+        emb = emb.to(torch.float32).contiguous()
+        self._ensure_index(emb.shape[1])
+        if stream is None:
+            stream = torch.cuda.current_stream(emb.device).cuda_stream
+        first = self._index.add_device(emb.data_ptr(), emb.shape[0], stream)
+        self._register([chunks[i] for i in keep], first)
+        return len(keep)
 
     def _remove_rows(self, rows: list[int]) -> int:
         rows = [r for r in rows if self._records[r] is not None]
@@ -140,7 +192,13 @@ class HipVectorStore(BaseVectorStore):
             return 0
         self._index.remove(np.asarray(rows, np.int64))
         for r in rows:
-            self._id_to_row.pop(self._records[r]["id"], None)
+            rec = self._records[r]
+            self._id_to_row.pop(rec["id"], None)
+            doc = self._doc_rows.get(rec["document_id"])
+            if doc is not None:
+                doc.remove(r)
+                if not doc:
+                    del self._doc_rows[rec["document_id"]]
             self._records[r] = None
         self._save()
         return len(rows)
@@ -153,8 +211,7 @@ class HipVectorStore(BaseVectorStore):
     async def delete_by_document_id(self, document_id: str) -> int:
         if self._index is None:
             return 0
-        rows = [r for r, rec in enumerate(self._records) if rec is not None and rec["document_id"] == document_id]
-        n = self._remove_rows(rows)
+        n = self._remove_rows(list(self._doc_rows.get(document_id, ())))
         logger.info("deleted %d chunks for document_id %s", n, document_id)
         return n
 
@@ -168,7 +225,7 @@ class HipVectorStore(BaseVectorStore):
         if self._index is not None:
             self._index.close()
         self._index, self.dim = None, None
-        self._records, self._id_to_row = [], {}
+        self._records, self._id_to_row, self._doc_rows = [], {}, {}
         self._cols.clear()
         for p in self._paths():
             if os.path.exists(p):

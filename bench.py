@@ -58,6 +58,9 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+TIME_EVERY = 4
+
+
 def main():
     args = parse()
     import torch
@@ -109,6 +112,10 @@ def main():
     searcher.finalize_all()
     torch.cuda.synchronize()
     index.take_scan_times()  # drop warmup launches
+    # HIP events around every 4th FILTER launch of the timed region (starting with the first):
+    # each event record leaves a ~6 us bubble on the stream, so timing every launch would
+    # slow the very steps being measured
+    index.set_scan_timing(TIME_EVERY)
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -103,6 +103,9 @@ int hr_merge_candidates(int device, const void* cand_dev /* G*B*kc records */, c
 int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,
                       float* out_dev, void* stream);
 
+/* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
+ * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
+int hr_index_set_scan_timing(hr_index* h, int every);
 /* Timing of the main-pass scans (ms, HIP events recorded on the search stream).
  * take_scan_times harvests, in launch order, every (SAMPLE, FILTER) pair launched since the
  * previous harvest (blocking on the pending events; up to cap entries; count in n_out);

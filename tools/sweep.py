@@ -18,6 +18,7 @@ for n in sizes:
     idx = _native.NativeIndex(D, "bf16", "cosine")
     idx.reserve(n)
     idx.add_synthetic(0, 0, n)
+    idx.set_scan_timing(1)
     qs = torch.from_numpy(np.stack([synth.planted_queries(0, n, D, B, qseed=i)[0] for i in range(13)])).cuda()
     ss = ShardedSearch(idx, 0, max_batch=B)
     for i in range(3):
@@ -29,6 +30,7 @@ for n in sizes:
         ss.search(qs[i], K)
         cands.append(idx.last_candidates())
     idx.take_scan_times()
+    idx.set_scan_timing(4)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(3, 13):  # pipelined pass: the timed one

@@ -37,6 +37,7 @@ __global__ __launch_bounds__(256) void k_exact_all(const uint8_t* __restrict__ r
         return;
     }
     double p = 0.0;
+#pragma unroll 8
     for (int d = lane; d < dpad; d += 64) p = p + (double)hr::load_elem<DT>(rows, S, r, d) * (double)qv[d];
     p = hr::wave_butterfly_sum(p);
     if (lane == 0) {

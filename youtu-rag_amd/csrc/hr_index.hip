@@ -83,6 +83,8 @@ struct hr_index {
     std::vector<ScanEvents> ev_free;
     std::deque<ScanEvents> ev_pending;
     float last_sample_ms = 0.f, last_filter_ms = 0.f;
+    int time_every = 0;               // record events around every Nth main pass (0 = never)
+    int64_t main_passes = 0;
     int n_cu = 256;
     std::mutex mu;
     // search workspace
@@ -379,7 +381,9 @@ static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds
 
 template <int MT, int DT, int MODE>
 static int launch_scan_p(hr_index* h, const Plan& pl, const ScanArgs& a, hipStream_t st) {
-    const int lds = scan_lds_bytes(h, pl.QB);
+    int lds = scan_lds_bytes(h, pl.QB);
+    // SAMPLE reduces its waves' group maxima in LDS: 8 waves x QB*16*64 floats + 8 part ids
+    if (MODE == SCAN_SAMPLE) lds = std::max(lds, (kScanThreads / 64) * pl.QB * 16 * 64 * 4 + 64);
 #define HR_SCAN_CASE(QBv, Pv) \
     if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, a, st, lds);
     if constexpr (MODE == SCAN_COLLECT) {  // the fallback runs one query at a time
@@ -493,12 +497,18 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     static const int refresh_env = getenv("HIPRAG_REFRESH") ? atoi(getenv("HIPRAG_REFRESH")) : 0;
     a.publish = (dbg & 8) ? 0 : (dbg & 16) ? 2 : 1;
     a.private_bufs = mode == 0 ? 1 : 0;
+    static const int wm_env = getenv("HIPRAG_WAVE_MAJOR") ? atoi(getenv("HIPRAG_WAVE_MAJOR")) : 1;
+    a.wave_major = wm_env;
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     if (n_tiles > 0) {
         hr_index::ScanEvents ev{};
-        if (groups) {  // time the main pass only, not fallbacks
+        // time the main pass only, not fallbacks, and only every time_every-th one: each event
+        // record costs a ~6 us bubble between kernels on the stream
+        const bool timed = groups && h->time_every > 0 && (h->main_passes % h->time_every) == 0;
+        if (groups) h->main_passes++;
+        if (timed) {
             if (h->ev_free.empty()) {
                 for (auto& x : ev.e) HIP_TRY(hipEventCreate(&x));
             } else {
@@ -508,19 +518,22 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             ev.sampled = false;
         }
         if (groups && !(dbg & 4)) {
-            const int64_t target = std::max<int64_t>(512, n_tiles / 64);
+            static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
+            static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
+            const int64_t target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048,
+                                                     n_tiles / (sdiv_env > 0 ? sdiv_env : 64));
             a.sample_stride = std::max<int64_t>(1, n_tiles / target);
             a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
-            HIP_TRY(hipEventRecord(ev.e[0], st));
+            if (timed) HIP_TRY(hipEventRecord(ev.e[0], st));
             if (int rc = launch_scan(h, pl, a, SCAN_SAMPLE, st)) return rc;
-            HIP_TRY(hipEventRecord(ev.e[1], st));
+            if (timed) HIP_TRY(hipEventRecord(ev.e[1], st));
             ev.sampled = true;
         }
         a.sample_stride = 1;
         a.n_units = n_tiles;
-        if (groups) HIP_TRY(hipEventRecord(ev.e[2], st));
+        if (timed) HIP_TRY(hipEventRecord(ev.e[2], st));
         if (int rc = launch_scan(h, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
-        if (groups) {
+        if (timed) {
             HIP_TRY(hipEventRecord(ev.e[3], st));
             h->ev_pending.push_back(ev);
             while (h->ev_pending.size() > 4096) {  // nobody is harvesting: recycle the oldest
@@ -602,7 +615,7 @@ static int launch_merge(int device, const Cand* cand, const double* bounds, int 
                         int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st) {
     int p2 = 1;
     while (p2 < G * kc) p2 <<= 1;
-    const int lds = p2 * 16;
+    const int lds = p2 * 16 + 16;
     if (lds > 160 * 1024) return set_err(HR_E_INVALID, "too many candidates to merge");
     static bool merge_attr[64] = {};
     if (!merge_attr[device & 63]) {
@@ -948,6 +961,14 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
         ++k;
     }
     if (n) *n = k;
+    return HR_OK;
+}
+
+extern "C" int hr_index_set_scan_timing(hr_index* h, int every) {
+    if (!h || every < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->time_every = every;
+    h->main_passes = 0;
     return HR_OK;
 }
 

@@ -117,6 +117,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     bool scale = false;
     if (metric == COSINE) {
         double p = 0.0;
+#pragma unroll 8
         for (int d = lane; d < dim; d += 64) {
             double x = (double)src(d);
             p = p + x * x;
@@ -129,6 +130,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     }
     double e1 = 0.0, nh = 0.0;
     const int qb = b >> 5;
+#pragma unroll 8
     for (int d = lane; d < dpad; d += 64) {
         float x = src(d);
         float v = scale ? (float)((double)x * inv) : x;
@@ -150,6 +152,21 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
 }
 
 // ---------------------------------------------------------------- K3: the scan
+// global -> LDS copy of n 16-byte vectors by the whole block, U loads in flight per thread
+__device__ inline void stage_lds(u32x4* dst, const u32x4* src, int n) {
+    constexpr int U = 8;
+    const int st = blockDim.x;
+    int i = threadIdx.x;
+    for (; i + (U - 1) * st < n; i += U * st) {
+        u32x4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) v[j] = src[i + j * st];
+#pragma unroll
+        for (int j = 0; j < U; ++j) dst[i + j * st] = v[j];
+    }
+    for (; i < n; i += st) dst[i] = src[i];
+}
+
 struct ScanArgs {
     const uint8_t* rows;     // tiled corpus
     const uint32_t* live;    // one word per tile
@@ -174,6 +191,7 @@ struct ScanArgs {
     // query index a compile-time offset from a wave-uniform base (no hoisted per-query
     // pointers: those cost ~150 VGPRs of spills in the fully unrolled epilogue).
     int private_bufs;
+    int wave_major;          // unit ranges numbered wave-major across workgroups (spreads the tail)
     float2* pbuf;
     uint32_t* pcnt;
     int capw;
@@ -251,29 +269,39 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const int half = lane >> 5;
     const int g = lane & 31;
 
-    // stage the query fragments (QB*S KiB) into LDS once per launch
-    {
-        const int nvec = a.S * QB * 64;  // 16-byte vectors
-        const u32x4* src = (const u32x4*)a.qfrag;
-        u32x4* dst = (u32x4*)lds;
-        for (int i = tid; i < nvec; i += blockDim.x) dst[i] = src[i];
+    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6);  // slot of this wave's outputs
+    // unit range: contiguous per wave, numbered wave-major across workgroups so the waves that
+    // get one extra unit sit on different CUs (the tail is then one tile per CU, not a
+    // handful of fully loaded CUs finishing a tile after everyone else)
+    const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * gridDim.x + blockIdx.x : w;
+    const int64_t base = a.n_units / W, rem = a.n_units % W;
+    const int64_t u0 = wr * base + (wr < rem ? wr : rem);
+    const int64_t u1 = u0 + base + (wr < rem ? 1 : 0);
+    const int64_t stride = FILTER ? 1 : a.sample_stride;
+    const int S = a.S;
+
+    // first loads of the corpus stream go out before the query staging, so their HBM latency
+    // overlaps it
+    XFrag<MT, DT> ring[P];
+    if (u0 < u1) {
+        const int64_t c0 = (u0 * stride) * S;
+#pragma unroll
+        for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
     }
+
+    // stage the query fragments (QB*S KiB) into LDS once per launch; 8 loads in flight per
+    // thread (a load->store loop pays one L2 round trip per 8 KiB)
+    stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
     __syncthreads();
 
-    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
-    const int64_t base = a.n_units / W, rem = a.n_units % W;
-    const int64_t u0 = w * base + (w < rem ? w : rem);
-    const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
-    if (u0 >= u1) {
+    if (u0 >= u1 && FILTER) {
         if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = 0;
         return;
-    }
+    }  // an idle SAMPLE wave stays: it takes part in the workgroup reduction below
     uint32_t mycnt = 0;  // private mode: lane q counts the candidates of query q in this wave
     float2* const wave_buf = priv ? a.pbuf + w * (QB * 32) * a.capw : nullptr;
 
-    const int64_t stride = FILTER ? 1 : a.sample_stride;
-    const int S = a.S;
     const u32x4* qs = (const u32x4*)lds;
 
     float th[QB][16], gmax[QB][16];
@@ -371,12 +399,6 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     };
     if (FILTER) refresh(false);
 
-    XFrag<MT, DT> ring[P];
-    {
-        const int64_t c0 = (u0 * stride) * S;
-#pragma unroll
-        for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
-    }
 
     for (int64_t u = u0; u < u1; ++u) {
         const int64_t t = u * stride;
@@ -465,7 +487,44 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     }
 
     if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;
-    if (!FILTER) flush();  // SAMPLE: publish the group maxima
+    if (!FILTER) {
+        // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope
+        // atomics from 8 XCDs), where same-address atomics serialise, so the workgroup's 8 waves
+        // first reduce in LDS (the query tile is no longer needed): one atomic per address per
+        // workgroup instead of one per wave.  Waves in different row parts flush on their own.
+        constexpr int NE = QB * 16 * 64;  // entries per wave
+        float* red = (float*)lds;
+        int64_t* partw = (int64_t*)(red + 8 * NE);
+        const int wv = tid >> 6;
+        __syncthreads();  // every wave is done reading the query fragments
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) red[wv * NE + (qb * 16 + i) * 64 + lane] = gmax[qb][i];
+        if (lane == 0) partw[wv] = u0 < u1 ? part : -1;
+        __syncthreads();
+        int64_t p0 = -1;
+        bool same = true;
+        const int nw = blockDim.x >> 6;
+        for (int v = 0; v < nw; ++v) {
+            if (partw[v] < 0) continue;
+            if (p0 < 0) p0 = partw[v];
+            same = same && partw[v] == p0;
+        }
+        if (!same) {
+            flush();
+        } else if (p0 >= 0) {
+            for (int e = tid; e < NE; e += blockDim.x) {
+                float m = -__builtin_inff();
+                for (int v = 0; v < nw; ++v) m = fmaxf(m, red[v * NE + e]);
+                if (m > -__builtin_inff()) {
+                    const int l = e & 63, ri = (e >> 6) & 15, qb = e >> 10;
+                    const int q = qb * 32 + 4 * (l >> 5) + (ri & 3) + 8 * (ri >> 2);
+                    atomicMax(a.mkeys + p0 * a.pstride + q * 32 + (l & 31), f2key(m));
+                }
+            }
+        }
+    }
 }
 
 
@@ -477,8 +536,7 @@ template <int MT, int DT, int QB>
 __global__ __launch_bounds__(256) void k_debug_approx(const uint8_t* __restrict__ rows, const uint16_t* __restrict__ qfrag,
                                                       int S, int64_t n_tiles, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int nvec = S * QB * 64;
-    for (int i = threadIdx.x; i < nvec; i += blockDim.x) ((u32x4*)lds)[i] = ((const u32x4*)qfrag)[i];
+    stage_lds((u32x4*)lds, (const u32x4*)qfrag, S * QB * 64);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -524,6 +582,8 @@ __device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of t
         }
     }
 }
+
+constexpr int kRankMax = 1024;  // candidate sets up to this size are ranked by counting, larger ones sorted
 
 __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
                                                  int cap, const uint32_t* __restrict__ pcnt,
@@ -584,12 +644,32 @@ __global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cn
     if (ovf) atomicOr(&ovf_sh, 1);
     __syncthreads();
     const int m = m_sh < cap ? m_sh : cap;
+    const int keep = m < kc ? m : kc;
+    if (m <= kRankMax) {
+        // rank by counting: keys are distinct (row in the low word), so a key's rank is the number of
+        // larger keys; every thread reads the same LDS word per step (broadcast), no sort stages
+        uint64_t* kth_sh = (uint64_t*)(smem + 8);  // reuses thr_sh's slot (thr already read)
+        for (int i = tid; i < m; i += blockDim.x) {
+            const uint64_t key = keys[i];
+            int rank = 0;
+            for (int j = 0; j < m; ++j) rank += keys[j] > key ? 1 : 0;
+            if (rank < kc) sel_rows[q * kc + rank] = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu);
+            if (rank == kc - 1) *kth_sh = key;
+        }
+        for (int i = keep + tid; i < kc; i += blockDim.x) sel_rows[q * kc + i] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid == 0) {
+            sel_cnt[q] = keep;
+            bound_approx[q] = (m >= kc && kc > 0) ? key2f((uint32_t)(*kth_sh >> 32)) : thr;
+            overflow[q] = ovf_sh;
+        }
+        return;
+    }
     int p2 = 1;
     while (p2 < m) p2 <<= 1;
     for (int i = m + tid; i < p2; i += blockDim.x) keys[i] = 0;
     __syncthreads();
     if (p2 > 1) block_bitonic_desc(keys, p2);
-    const int keep = m < kc ? m : kc;
     for (int i = tid; i < kc; i += blockDim.x)
         sel_rows[q * kc + i] = i < keep ? 0xFFFFFFFFu - (uint32_t)(keys[i] & 0xFFFFFFFFu) : 0xFFFFFFFFu;
     if (tid == 0) {
@@ -629,6 +709,7 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
     const int64_t r = (int64_t)sel_rows[q * kc + c];
     const float* qv = q32 + (int64_t)q * dpad;
     double p = 0.0;
+#pragma unroll 8
     for (int d = lane; d < dpad; d += 64) p = p + (double)load_elem<DT>(rows, S, r, d) * (double)qv[d];
     p = wave_butterfly_sum(p);
     if (lane == 0) out[wid] = Cand{p, r + row_offset};
@@ -665,6 +746,55 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, co
         }
     }
     __syncthreads();
+    auto key_of = [](uint64_t key) {
+        uint64_t u = (key & 0x8000000000000000ull) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
+        return __builtin_bit_cast(double, u);
+    };
+    if (n <= kRankMax) {
+        // rank by counting over (score key desc, row asc); invalid slots (key 0, row INT64_MAX) rank last
+        // two scalars after the keys/rows (all LDS in the dynamic region, like k_select)
+        int& valid_sh = *(int*)(smem + (size_t)p2 * 16);
+        uint64_t& kth_key_sh = *(uint64_t*)(smem + (size_t)p2 * 16 + 8);
+        if (threadIdx.x == 0) {
+            valid_sh = 0;
+            kth_key_sh = 0;
+        }
+        __syncthreads();
+        int myvalid = 0;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t a = ks[i];
+            const int64_t ra = rs[i];
+            if (ra == INT64_MAX) continue;
+            ++myvalid;
+            int rank = 0;
+            for (int j = 0; j < n; ++j) {
+                const uint64_t b = ks[j];
+                rank += (b > a || (b == a && rs[j] < ra)) ? 1 : 0;
+            }
+            if (rank < k) {
+                scores_out[(int64_t)q * k + rank] = (float)key_of(a);
+                rows_out[(int64_t)q * k + rank] = ra;
+            }
+            if (rank == k - 1) kth_key_sh = a;
+        }
+        if (myvalid) atomicAdd(&valid_sh, myvalid);
+        __syncthreads();
+        const int valid = valid_sh;
+        for (int i = valid + threadIdx.x; i < k; i += blockDim.x) {
+            scores_out[(int64_t)q * k + i] = -__builtin_inff();
+            rows_out[(int64_t)q * k + i] = -1;
+        }
+        if (threadIdx.x == 0) {
+            double maxb = -__builtin_inf();
+            for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, bounds[(int64_t)gi * B + q]);
+            double sk = -__builtin_inf();
+            if (valid >= k && k > 0) sk = key_of(kth_key_sh);  // fewer than k: every remaining row is a candidate
+            kth_out[q] = sk;
+            bool fail = maxb > -__builtin_inf() && (valid < k || !(sk > maxb));
+            fail_out[q] = fail ? 1 : 0;
+        }
+        return;
+    }
     for (int kk = 2; kk <= p2; kk <<= 1) {
         for (int j = kk >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x; i < p2; i += blockDim.x) {
@@ -693,24 +823,14 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, co
         double sk = -__builtin_inf();
         for (int i = 0; i < k; ++i) {
             if (i < valid) {
-                uint64_t key = ks[i];
-                uint64_t u = (key & 0x8000000000000000ull) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
-                double s = __builtin_bit_cast(double, u);
-                scores_out[(int64_t)q * k + i] = (float)s;
+                scores_out[(int64_t)q * k + i] = (float)key_of(ks[i]);
                 rows_out[(int64_t)q * k + i] = rs[i];
-                if (i == k - 1) sk = s;
             } else {
                 scores_out[(int64_t)q * k + i] = -__builtin_inff();
                 rows_out[(int64_t)q * k + i] = -1;
             }
         }
-        if (valid >= k && k > 0) {
-            uint64_t key = ks[k - 1];
-            uint64_t u = (key & 0x8000000000000000ull) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
-            sk = __builtin_bit_cast(double, u);
-        } else if (valid > 0) {
-            sk = -__builtin_inf();  // fewer than k: every remaining row is a candidate
-        }
+        if (valid >= k && k > 0) sk = key_of(ks[k - 1]);  // fewer than k: every remaining row is a candidate
         kth_out[q] = sk;
         bool fail = maxb > -__builtin_inf() && (valid < k || !(sk > maxb));
         fail_out[q] = fail ? 1 : 0;

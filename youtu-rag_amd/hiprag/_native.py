@@ -36,7 +36,7 @@ EXPORTS = [
     "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_add_device",
     "hr_index_remove", "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows",
     "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_index_take_scan_times", "hr_index_last_scan_ms",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k",
 ]
@@ -89,6 +89,7 @@ def load_library(path: str | None = None):
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
             "hr_index_last_scan_ms": [vp, vp, vp],
             "hr_index_take_scan_times": [vp, vp, vp, i32, vp],
+            "hr_index_set_scan_timing": [vp, i32],
             "hr_device_count": [vp],
             "hr_index_debug_approx": [vp, vp, i32, vp, vp],
             "hr_index_last_candidates": [vp, vp, vp],
@@ -244,6 +245,10 @@ class NativeIndex:
         t, m = ctypes.c_int64(0), ctypes.c_int64(0)
         _check(self.lib.hr_index_last_candidates(self._h, ctypes.byref(t), ctypes.byref(m)))
         return t.value, m.value
+
+    def set_scan_timing(self, every: int) -> None:
+        """Record HIP events around every `every`-th main-pass scan (0 = off, the default)."""
+        _check(self.lib.hr_index_set_scan_timing(self._h, int(every)))
 
     def take_scan_times(self, cap: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
         """(sample_ms, filter_ms) of every main-pass scan since the previous harvest."""

@@ -97,6 +97,12 @@ int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const 
 int hr_merge_candidates(int device, const void* cand_dev /* G*B*kc records */, const double* bounds_dev /* G*B */,
                         int G, int B, int kc, int k, float* scores_out_dev, int64_t* rows_out_dev,
                         double* kth_out_dev, int32_t* fail_out_dev, void* stream);
+/* The same with explicit per-rank strides (bytes) between the ranks' candidate blocks and bound
+ * blocks, so one all-gather can move each rank's packed record [B*kc candidates][B bounds]
+ * (cand_rank_stride = bound_rank_stride = B*kc*16 + B*8). */
+int hr_merge_candidates_strided(int device, const void* cand_dev, const double* bounds_dev, int64_t cand_rank_stride,
+                                int64_t bound_rank_stride, int G, int B, int kc, int k, float* scores_out_dev,
+                                int64_t* rows_out_dev, double* kth_out_dev, int32_t* fail_out_dev, void* stream);
 
 /* K7: masked mean-pool of the first-dim hidden states with the first n_instr
  * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */

@@ -612,7 +612,10 @@ static int validate_search(hr_index* h, int B, int k) {
 }
 
 static int launch_merge(int device, const Cand* cand, const double* bounds, int G, int B, int kc, int k, float* s_out,
-                        int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st) {
+                        int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st, int64_t cstride = 0,
+                        int64_t bstride = 0) {
+    if (!cstride) cstride = (int64_t)B * kc * (int64_t)sizeof(Cand);
+    if (!bstride) bstride = (int64_t)B * 8;
     int p2 = 1;
     while (p2 < G * kc) p2 <<= 1;
     const int lds = p2 * 16 + 16;
@@ -622,8 +625,8 @@ static int launch_merge(int device, const Cand* cand, const double* bounds, int 
         HIP_TRY(hipFuncSetAttribute((const void*)k_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         merge_attr[device & 63] = true;
     }
-    hipLaunchKernelGGL(k_merge, dim3(B), dim3(256), lds, st, cand, bounds, G, B, kc, k, s_out, r_out, kth_out,
-                       fail_out);
+    hipLaunchKernelGGL(k_merge, dim3(B), dim3(256), lds, st, (const uint8_t*)cand, (const uint8_t*)bounds, cstride,
+                       bstride, G, B, kc, k, s_out, r_out, kth_out, fail_out);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }
@@ -756,6 +759,21 @@ extern "C" int hr_merge_candidates(int device, const void* cand_dev, const doubl
     HIP_TRY(hipSetDevice(device));
     return launch_merge(device, (const Cand*)cand_dev, bounds_dev, G, B, kc, k, scores_out_dev, rows_out_dev,
                         kth_out_dev, fail_out_dev, (hipStream_t)stream);
+}
+
+extern "C" int hr_merge_candidates_strided(int device, const void* cand_dev, const double* bounds_dev,
+                                           int64_t cand_rank_stride, int64_t bound_rank_stride, int G, int B, int kc,
+                                           int k, float* scores_out_dev, int64_t* rows_out_dev, double* kth_out_dev,
+                                           int32_t* fail_out_dev, void* stream) {
+    if (!cand_dev || !bounds_dev || !scores_out_dev || !rows_out_dev || !kth_out_dev || !fail_out_dev)
+        return set_err(HR_E_INVALID, "null argument");
+    if (G <= 0 || B <= 0 || kc <= 0 || k <= 0 || k > kc) return set_err(HR_E_INVALID, "bad sizes");
+    if (cand_rank_stride < (int64_t)B * kc * (int64_t)sizeof(Cand) || bound_rank_stride < (int64_t)B * 8 ||
+        cand_rank_stride % 8 || bound_rank_stride % 8)
+        return set_err(HR_E_INVALID, "rank strides smaller than one rank's records or misaligned");
+    HIP_TRY(hipSetDevice(device));
+    return launch_merge(device, (const Cand*)cand_dev, bounds_dev, G, B, kc, k, scores_out_dev, rows_out_dev,
+                        kth_out_dev, fail_out_dev, (hipStream_t)stream, cand_rank_stride, bound_rank_stride);
 }
 
 

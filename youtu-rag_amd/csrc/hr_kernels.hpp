@@ -210,11 +210,23 @@ __device__ inline f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c)
 // X fragment of k-step chunk c (flattened tile*S + s) for this lane, converted to MT
 template <int MT, int DT>
 struct XFrag;
+// corpus stream loads: every byte is read once per launch, so they go out non-temporal
+// (HR_CORPUS_NT=0 builds the default-policy variant for A/B timing)
+#ifndef HR_CORPUS_NT
+#define HR_CORPUS_NT 1
+#endif
+__device__ inline u32x4 corpus_load(const uint8_t* p) {
+#if HR_CORPUS_NT
+    return __builtin_nontemporal_load((const u32x4*)p);
+#else
+    return *(const u32x4*)p;
+#endif
+}
 template <int MT>
 struct XFrag<MT, BF16> {
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        v = *(const u32x4*)(rows + c * 1024 + lane * 16);
+        v = corpus_load(rows + c * 1024 + lane * 16);
     }
     __device__ inline u32x4 get() const { return v; }
 };
@@ -222,7 +234,7 @@ template <int MT>
 struct XFrag<MT, F16> {
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        v = *(const u32x4*)(rows + c * 1024 + lane * 16);
+        v = corpus_load(rows + c * 1024 + lane * 16);
     }
     __device__ inline u32x4 get() const { return v; }
 };
@@ -230,8 +242,8 @@ template <int MT>
 struct XFrag<MT, F32> {
     u32x4 a, b;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        a = *(const u32x4*)(rows + c * 2048 + lane * 16);
-        b = *(const u32x4*)(rows + c * 2048 + 1024 + lane * 16);
+        a = corpus_load(rows + c * 2048 + lane * 16);
+        b = corpus_load(rows + c * 2048 + 1024 + lane * 16);
     }
     // fp32 corpus -> MFMA operand: packed hardware RNE conversion (v_cvt_pk_*).  Only the
     // error-bounded approximate score depends on it (the exact rescoring reads fp32).
@@ -717,7 +729,10 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
 
 // ---------------------------------------------------------------- K4/C1: merge shards
 // One block per query over G*kc exact candidates.  Sort key: (d2key(score) desc, row asc).
-__global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, const double* __restrict__ bounds, int G,
+// Rank g's candidates start at cand + g*cstride bytes, its bounds at bounds + g*bstride bytes (one
+// packed all-gather record per rank: [B*kc Cand][B double]).
+__global__ __launch_bounds__(256) void k_merge(const uint8_t* __restrict__ cand, const uint8_t* __restrict__ bounds,
+                                               int64_t cstride, int64_t bstride, int G,
                                                int B, int kc, int k, float* __restrict__ scores_out,
                                                int64_t* __restrict__ rows_out, double* __restrict__ kth_out,
                                                int32_t* __restrict__ fail_out) {
@@ -732,7 +747,7 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, co
     for (int i = threadIdx.x; i < p2; i += blockDim.x) {
         if (i < n) {
             const int gi = i / kc, ci = i % kc;
-            Cand e = cand[((int64_t)gi * B + q) * kc + ci];
+            Cand e = ((const Cand*)(cand + gi * cstride))[(int64_t)q * kc + ci];
             if (e.row < 0) {
                 ks[i] = 0;
                 rs[i] = INT64_MAX;
@@ -786,7 +801,7 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, co
         }
         if (threadIdx.x == 0) {
             double maxb = -__builtin_inf();
-            for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, bounds[(int64_t)gi * B + q]);
+            for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, ((const double*)(bounds + gi * bstride))[q]);
             double sk = -__builtin_inf();
             if (valid >= k && k > 0) sk = key_of(kth_key_sh);  // fewer than k: every remaining row is a candidate
             kth_out[q] = sk;
@@ -819,7 +834,7 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, co
         int valid = 0;
         for (int i = 0; i < p2 && rs[i] != INT64_MAX; ++i) ++valid;
         double maxb = -__builtin_inf();
-        for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, bounds[(int64_t)gi * B + q]);
+        for (int gi = 0; gi < G; ++gi) maxb = fmax(maxb, ((const double*)(bounds + gi * bstride))[q]);
         double sk = -__builtin_inf();
         for (int i = 0; i < k; ++i) {
             if (i < valid) {

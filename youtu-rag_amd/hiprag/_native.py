@@ -38,7 +38,7 @@ EXPORTS = [
     "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
     "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
-    "hr_kc_for_k",
+    "hr_kc_for_k", "hr_merge_candidates_strided",
 ]
 
 _lib = None
@@ -64,7 +64,7 @@ def load_library(path: str | None = None):
             import torch  # noqa: F401
         except ImportError:
             pass
-        p = path or LIB_PATH
+        p = path or os.environ.get("HIPRAG_LIB_OVERRIDE") or LIB_PATH  # override: A/B timing builds only
         if not os.path.exists(p):
             raise OSError(f"{p} not found; build it with `make -C youtu-rag_amd/csrc` or __graft_entry__.build()")
         L = ctypes.CDLL(p)
@@ -86,6 +86,7 @@ def load_library(path: str | None = None):
             "hr_index_search_shard": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp],
             "hr_index_search_shard_collect": [vp, vp, i32, vp, i32, vp, i64, vp, vp, vp],
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
+            "hr_merge_candidates_strided": [i32, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
             "hr_index_last_scan_ms": [vp, vp, vp],
             "hr_index_take_scan_times": [vp, vp, vp, i32, vp],
@@ -278,11 +279,21 @@ class NativeIndex:
 
 
 def merge_candidates(device: int, cand_ptr: int, bounds_ptr: int, G: int, B: int, kc: int, k: int, scores_ptr: int,
-                     rows_ptr: int, kth_ptr: int, fail_ptr: int, stream: int = 0) -> None:
-    _check(load_library().hr_merge_candidates(int(device), ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bounds_ptr),
-                                              int(G), int(B), int(kc), int(k), ctypes.c_void_p(scores_ptr),
-                                              ctypes.c_void_p(rows_ptr), ctypes.c_void_p(kth_ptr),
-                                              ctypes.c_void_p(fail_ptr), ctypes.c_void_p(stream or None)))
+                     rows_ptr: int, kth_ptr: int, fail_ptr: int, stream: int = 0, cand_rank_stride: int = 0,
+                     bound_rank_stride: int = 0) -> None:
+    """Merge G ranks' candidates; strides (bytes) default to the dense [G][B][kc] / [G][B] layouts."""
+    L = load_library()
+    if cand_rank_stride or bound_rank_stride:
+        _check(L.hr_merge_candidates_strided(int(device), ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bounds_ptr),
+                                             int(cand_rank_stride or B * kc * 16), int(bound_rank_stride or B * 8),
+                                             int(G), int(B), int(kc), int(k), ctypes.c_void_p(scores_ptr),
+                                             ctypes.c_void_p(rows_ptr), ctypes.c_void_p(kth_ptr),
+                                             ctypes.c_void_p(fail_ptr), ctypes.c_void_p(stream or None)))
+        return
+    _check(L.hr_merge_candidates(int(device), ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bounds_ptr),
+                                 int(G), int(B), int(kc), int(k), ctypes.c_void_p(scores_ptr),
+                                 ctypes.c_void_p(rows_ptr), ctypes.c_void_p(kth_ptr),
+                                 ctypes.c_void_p(fail_ptr), ctypes.c_void_p(stream or None)))
 
 
 def pool_normalize(hidden_ptr: int, dtype: str, mask_ptr: int, B: int, T: int, H: int, n_instr: int, out_ptr: int,

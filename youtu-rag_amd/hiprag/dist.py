@@ -4,8 +4,9 @@ The corpus is split into contiguous row ranges, one per rank (global row =
 shard offset + local row).  Every rank scans its shard for the same replicated
 query batch and produces, per query, its exact top-kc candidates (fp64 canonical
 scores + global rows) and a bound on the score of every row it did NOT return.
-One ``all_gather`` moves B·kc·16 bytes per rank (32 KB at B=64, kc=32 -- latency-
-bound, so one collective per batch and nothing else crosses xGMI); each rank then
+One ``all_gather`` moves each rank's packed record -- B·kc 16-byte candidates followed by
+its B bounds, 33 KB at B=64, kc=32 -- latency-bound, so exactly one collective per batch
+and nothing else crosses xGMI; each rank then
 merges the G·kc candidates on its own GPU with the same (score desc, row asc)
 order and the same guard, so all ranks hold identical results.  Queries whose
 guard fails (top-k not provably complete) are re-scanned in collect mode: every
@@ -29,13 +30,22 @@ from . import _native
 FALLBACK_CAP = 512
 
 
+def _record_len(B: int, kc: int) -> int:
+    """float64 words of one rank's packed all-gather record: B*kc {score, row} pairs, then B bounds."""
+    return B * kc * 2 + B
+
+
+def _record_views(rec, B: int, kc: int):
+    """(cand (..., B, kc, 2), bound (..., B)) views of packed records rec (..., _record_len)."""
+    n = B * kc * 2
+    return rec[..., :n].view(*rec.shape[:-1], B, kc, 2), rec[..., n:n + B]
+
+
 class _Slot:
     def __init__(self, torch, device, G, B, kc, pinned):
         f64 = dict(dtype=torch.float64, device=device)
-        self.cand = torch.empty((B, kc, 2), **f64)  # {score, row bits} records (hr::Cand)
-        self.bound = torch.empty((B,), **f64)
-        self.cand_all = torch.empty((G, B, kc, 2), **f64) if G > 1 else None
-        self.bound_all = torch.empty((G, B), **f64) if G > 1 else None
+        self.rec = torch.empty((_record_len(B, kc),), **f64)  # this rank's packed record
+        self.rec_all = torch.empty((G, _record_len(B, kc)), **f64) if G > 1 else None
         self.kth = torch.empty((B,), **f64)
         self.fail = torch.empty((B,), dtype=torch.int32, device=device)
         self.fail_h = torch.empty((B,), dtype=torch.int32, pin_memory=pinned)
@@ -68,8 +78,11 @@ class ShardedSearch:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
     def _merge(self, cand_all, bound_all, G, B, kc, k, s_out, r_out, kth, fail):
+        # cand_all (G, B, kc, 2) / bound_all (G, B): views into packed per-rank records (rank stride
+        # = stride(0)); the kernel reads them in place
         _native.merge_candidates(self.device.index or 0, cand_all.data_ptr(), bound_all.data_ptr(), G, B, kc, k,
-                                 s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream())
+                                 s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream(),
+                                 cand_rank_stride=cand_all.stride(0) * 8, bound_rank_stride=bound_all.stride(0) * 8)
 
     def _shard_search(self, q, k, cand, bound, mask_ptr):
         self.index.search_shard(q.data_ptr(), q.shape[0], k, self.kc, self.row_offset, cand.data_ptr(),
@@ -110,17 +123,16 @@ class ShardedSearch:
         q = q.contiguous()
         s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
         r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
-        cand, bound = slot.cand[:B], slot.bound[:B]
+        L = _record_len(B, self.kc)
+        rec = slot.rec[:L]
+        cand, bound = _record_views(rec, B, self.kc)
         self._shard_search(q, k, cand, bound, mask_ptr)
         if self.G == 1:  # nothing to exchange: merge straight from this shard's candidates
-            cand_all, bound_all = cand.view(1, B, self.kc, 2), bound.view(1, B)
-        else:
-            full = B == self.max_batch
-            cand_all = slot.cand_all if full else torch.empty((self.G, B, self.kc, 2), dtype=torch.float64,
-                                                              device=self.device)
-            bound_all = slot.bound_all if full else torch.empty((self.G, B), dtype=torch.float64, device=self.device)
-            self._all_gather(cand_all, cand)
-            self._all_gather(bound_all, bound)
+            rec_all = rec.view(1, L)
+        else:  # ONE collective per batch: every rank's packed record
+            rec_all = slot.rec_all.view(-1)[: self.G * L].view(self.G, L)
+            self._all_gather(rec_all, rec)
+        cand_all, bound_all = _record_views(rec_all, B, self.kc)
         kth, fail = slot.kth[:B], slot.fail[:B]
         self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
         if slot.event is not None:
@@ -161,13 +173,13 @@ class ShardedSearch:
         qf = q[idx].contiguous()
         kf = kth[idx].contiguous()
         Bf, cap = len(failed), FALLBACK_CAP
-        cand = torch.empty((Bf, cap, 2), dtype=torch.float64, device=self.device)
-        bound = torch.empty((Bf,), dtype=torch.float64, device=self.device)
+        L = _record_len(Bf, cap)
+        rec = torch.empty((L,), dtype=torch.float64, device=self.device)
+        cand, bound = _record_views(rec, Bf, cap)
         self._shard_collect(qf, kf, cap, cand, bound, mask_ptr)
-        cand_all = torch.empty((self.G, Bf, cap, 2), dtype=torch.float64, device=self.device)
-        bound_all = torch.empty((self.G, Bf), dtype=torch.float64, device=self.device)
-        self._all_gather(cand_all, cand)
-        self._all_gather(bound_all, bound)
+        rec_all = torch.empty((self.G, L), dtype=torch.float64, device=self.device)
+        self._all_gather(rec_all, rec)
+        cand_all, bound_all = _record_views(rec_all, Bf, cap)
         s2 = torch.empty((Bf, k), dtype=torch.float32, device=self.device)
         r2 = torch.empty((Bf, k), dtype=torch.int64, device=self.device)
         kth2 = torch.empty((Bf,), dtype=torch.float64, device=self.device)

@@ -91,6 +91,15 @@ int hr_kc_for_k(int k);
 int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                           int64_t row_offset, void* cand_out_dev /* B*kc records */,
                           double* bound_out_dev /* B */, void* stream);
+/* Pipelined form of hr_index_search_shard: the scan (query prep, SAMPLE, FILTER) runs on
+ * scan_stream over all but a few CUs, select + exact rescoring on tail_stream, which waits for
+ * the scan by event; the outputs are ready in tail_stream order.  Consecutive calls alternate
+ * between two workspaces, so batch i's tail (and whatever the caller queues after it on
+ * tail_stream: the all-gather, the merge) overlaps batch i+1's scan.  Same results as
+ * hr_index_search_shard. */
+int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
+                                int64_t row_offset, void* cand_out_dev, double* bound_out_dev, void* scan_stream,
+                                void* tail_stream);
 int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev /* B */,
                                   int cap, const uint64_t* row_mask_dev, int64_t row_offset,
                                   void* cand_out_dev /* B*cap records */, double* bound_out_dev, void* stream);

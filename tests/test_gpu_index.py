@@ -149,6 +149,42 @@ def test_large_k_vs_oracle(native, dim, dtype, n, B, k):
         _check(s, r, s_ref, r_ref)
 
 
+def test_dynamic_tail_and_pipelined_workspaces_vs_oracle(native):
+    """A shard large enough for the FILTER scan's dynamic tail (>= 8 tiles per wave; the pool has
+    an odd tile count, so the last run is one tile), searched synchronously and through the
+    pipelined two-workspace path (scan stream + tail stream) with several batches in flight,
+    with and without a row mask: every batch identical to the oracle."""
+    torch = pytest.importorskip("torch")
+    from hiprag.dist import ShardedSearch
+
+    dim, n, B, k = 64, 600_032, 64, 10
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add_synthetic(21, 0, n)
+    raw = R.gen_rows(21, 0, n, dim)
+    rng = np.random.default_rng(5)
+    qs = [np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+          for _ in range(4)]
+    stored = oracle.c_build_synthetic(21, 0, n, dim, "bf16", "cosine")
+    refs = [oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k) for q in qs]
+    for q, (s_ref, r_ref) in zip(qs, refs):
+        s, r = idx.search(q, k)
+        _check(s, r, s_ref, r_ref)
+    ss = ShardedSearch(idx, 0, max_batch=B, device=torch.device("cuda", 0))
+    assert ss.tail is not None
+    s_out = torch.empty((len(qs), B, k), dtype=torch.float32, device="cuda")
+    r_out = torch.empty((len(qs), B, k), dtype=torch.int64, device="cuda")
+    for i, q in enumerate(qs):  # submit finalizes the slot it reuses
+        ss.submit(torch.from_numpy(q).cuda(), k, s_out=s_out[i], r_out=r_out[i])
+    ss.finalize_all()
+    torch.cuda.synchronize()
+    for i, (s_ref, r_ref) in enumerate(refs):
+        _check(s_out[i].cpu().numpy(), r_out[i].cpu().numpy(), s_ref, r_ref)
+    allowed = rng.random(n) < 0.5
+    mask = oracle.mask_from_bool(allowed)
+    s, r = idx.search(qs[0], k, mask)
+    _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(qs[0], "cosine"), k, mask))
+
+
 def test_large_k_massive_ties(native):
     """300 identical rows, k = 100: the 100 lowest duplicate rows, via the exact fallback."""
     dim, n = 128, 8000

@@ -20,7 +20,7 @@ for n in sizes:
     idx.add_synthetic(0, 0, n)
     idx.set_scan_timing(1)
     qs = torch.from_numpy(np.stack([synth.planted_queries(0, n, D, B, qseed=i)[0] for i in range(13)])).cuda()
-    ss = ShardedSearch(idx, 0, max_batch=B)
+    ss = ShardedSearch(idx, 0, max_batch=B, overlap=os.environ.get("HIPRAG_OVERLAP", "1") != "0")
     for i in range(3):
         ss.search(qs[i], K)
     torch.cuda.synchronize()

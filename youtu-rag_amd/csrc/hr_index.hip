@@ -65,6 +65,26 @@ static constexpr int kCap = 8192;       // candidate buffer per query (shared-bu
 static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
 static constexpr int kScanThreads = 512;
 
+// Per-batch search workspace.  Two sets ping-pong between consecutive pipelined batches
+// (hr_index_search_shard_async: batch i's select/rescore on the tail stream overlaps batch
+// i+1's scan on the scan stream); a third serves the synchronous and collect paths.
+struct Scratch {
+    DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q;
+    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
+    hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
+    hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
+    bool armed = false;               // `released` has been recorded at least once
+    void release_all() {
+        for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
+                          &overflow, &pbuf, &pcnt, &dyn_q})
+            b->release();
+        if (scanned) (void)hipEventDestroy(scanned);
+        if (released) (void)hipEventDestroy(released);
+        scanned = released = nullptr;
+    }
+};
+static constexpr int kSyncSet = 2;
+
 struct hr_index {
     int dim = 0, dpad = 0, S = 0, dtype = BF16, metric = COSINE, device = 0;
     int64_t n = 0, cap = 0, n_live = 0;
@@ -88,10 +108,11 @@ struct hr_index {
     int n_cu = 256;
     std::mutex mu;
     // search workspace
-    DevBuf q_in, q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, cand, bound,
-        kth, fail, fb_cand, fb_bound, stage, pbuf, pcnt, exh;
+    DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, stage, exh;
+    Scratch scr[3];
+    int flip = 0;                     // next ping-pong set of the pipelined path
+    const Scratch* last_scr = nullptr;  // set of the most recent FILTER launch (diagnostics)
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
-    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
     std::vector<float> floor_host;
 };
 
@@ -340,7 +361,7 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
 }
 
 template <int MT, int DT, int QB, int P, int MODE>
-static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds) {
+static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
     auto kern = k_scan<MT, DT, QB, P, MODE>;
     static std::mutex attr_mu;
     static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
@@ -361,18 +382,33 @@ static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds
         }
         per_cu = occ[dev][bucket];
     }
-    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu, (a.n_units + 7) / 8));
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * per_cu, (a.n_units + 7) / 8));
     ScanArgs args = a;
     if (MODE == SCAN_FILTER) {
         const int64_t W = blocks * (kScanThreads / 64);
         const int Bq = QB * 32;
-        HIP_TRY(h->pbuf.ensure((size_t)Bq * W * kCapW * sizeof(float2)));
-        HIP_TRY(h->pcnt.ensure((size_t)Bq * W * 4));
-        args.pbuf = h->pbuf.as<float2>();
-        args.pcnt = h->pcnt.as<uint32_t>();
+        HIP_TRY(sc.pbuf.ensure((size_t)Bq * W * kCapW * sizeof(float2)));
+        HIP_TRY(sc.pcnt.ensure((size_t)Bq * W * 4));
+        args.pbuf = sc.pbuf.as<float2>();
+        args.pcnt = sc.pcnt.as<uint32_t>();
         args.capw = kCapW;
-        h->last_W = W;
-        h->last_Bp = Bq;
+        sc.last_W = W;
+        sc.last_Bp = Bq;
+        h->last_scr = &sc;
+        // dynamic tail: the last dyn_frac of the units go out in runs from the counter, but only
+        // when every wave still gets a long static run (HIPRAG_DYN_PCT / HIPRAG_DYN_CHUNK: A/B)
+        static const int pct_env = getenv("HIPRAG_DYN_PCT") ? atoi(getenv("HIPRAG_DYN_PCT")) : -1;
+        static const int chunk_env = getenv("HIPRAG_DYN_CHUNK") ? atoi(getenv("HIPRAG_DYN_CHUNK")) : 0;
+        const int pct = pct_env >= 0 ? pct_env : 10;
+        const int64_t per_wave = a.n_units / W;
+        args.dyn_start = a.n_units;
+        if (pct > 0 && per_wave >= 8 && sc.dyn_q.p) {
+            // static runs and dynamic runs are >= 2 units (the grab is issued one unit early)
+            const int64_t s_per = per_wave - std::max<int64_t>(2, per_wave * pct / 100);
+            args.dyn_start = s_per * W;
+            args.dyn_chunk = std::max(2, chunk_env > 0 ? chunk_env : 2);
+            args.dyn_q = sc.dyn_q.as<uint32_t>();
+        }
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kScanThreads), lds, st, args);
     HIP_TRY(hipGetLastError());
@@ -380,12 +416,12 @@ static int launch_scan_t(hr_index* h, const ScanArgs& a, hipStream_t st, int lds
 }
 
 template <int MT, int DT, int MODE>
-static int launch_scan_p(hr_index* h, const Plan& pl, const ScanArgs& a, hipStream_t st) {
+static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, hipStream_t st) {
     int lds = scan_lds_bytes(h, pl.QB);
     // SAMPLE reduces its waves' group maxima in LDS: 8 waves x QB*16*64 floats + 8 part ids
     if (MODE == SCAN_SAMPLE) lds = std::max(lds, (kScanThreads / 64) * pl.QB * 16 * 64 * 4 + 64);
 #define HR_SCAN_CASE(QBv, Pv) \
-    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, a, st, lds);
+    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, sc, cus, a, st, lds);
     if constexpr (MODE == SCAN_COLLECT) {  // the fallback runs one query at a time
         HR_SCAN_CASE(1, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4)
     } else if constexpr (DT == F32) {
@@ -398,14 +434,24 @@ static int launch_scan_p(hr_index* h, const Plan& pl, const ScanArgs& a, hipStre
     return set_err(HR_E_INVALID, "no scan variant for this plan");
 }
 
-static int launch_scan(hr_index* h, const Plan& pl, const ScanArgs& a, int mode, hipStream_t st) {
+static int launch_scan(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, int mode,
+                       hipStream_t st) {
     return dispatch_dt(h->dtype, [&](auto dt) -> int {
         constexpr int DT = decltype(dt)::value;
         constexpr int MT = DT == F16 ? F16 : BF16;
-        if (mode == SCAN_SAMPLE) return launch_scan_p<MT, DT, SCAN_SAMPLE>(h, pl, a, st);
-        if (mode == SCAN_FILTER) return launch_scan_p<MT, DT, SCAN_FILTER>(h, pl, a, st);
-        return launch_scan_p<MT, DT, SCAN_COLLECT>(h, pl, a, st);
+        if (mode == SCAN_SAMPLE) return launch_scan_p<MT, DT, SCAN_SAMPLE>(h, sc, cus, pl, a, st);
+        if (mode == SCAN_FILTER) return launch_scan_p<MT, DT, SCAN_FILTER>(h, sc, cus, pl, a, st);
+        return launch_scan_p<MT, DT, SCAN_COLLECT>(h, sc, cus, pl, a, st);
     });
+}
+
+// CUs left to the tail stream while a pipelined scan runs: the scan reads HBM at the same rate
+// on 224 of the 256 CUs (measured: 6.85 vs 6.81 TB/s at 10M rows, 0.434 vs 0.427 ms at 1.25M),
+// so select/rescore, the RCCL all-gather and the merge of the previous batch run beside it
+static int tail_cus(const hr_index* h) {
+    static const int env = getenv("HIPRAG_TAIL_CUS") ? atoi(getenv("HIPRAG_TAIL_CUS")) : -1;
+    const int want = env >= 0 ? env : 32;
+    return std::max(0, std::min(want, h->n_cu - 8));
 }
 
 // error-bound constants for the approximate (MFMA) scores, see DESIGN.md "Exactness guard"
@@ -417,37 +463,52 @@ static double storage_u(const hr_index* h) {
 
 // One chunk of <= Bp queries on this shard.  mode 0: top-kc via SAMPLE+FILTER(groups);
 // mode 1: collect every row with approx >= floor (exact fallback).
+// st_tail: stream of select + rescore (the outputs are ready in its order).  st_tail != st:
+// pipelined (mode 0 only) -- ping-pong scratch set, the scan leaves tail_cus() CUs free and the
+// tail waits for this batch's FILTER by event; st_tail == st: one stream, the synchronous set.
 static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
                        const double* kth_dev_host /* mode 1: host array of kth, B */, int mode, int cap_out,
-                       Cand* cand_out, double* bound_out, hipStream_t st) {
+                       Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail) {
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     const int Bp = pl.Bp;
-    HIP_TRY(h->q32.ensure((size_t)Bp * h->dpad * 4));
-    HIP_TRY(h->qfrag.ensure((size_t)h->S * pl.QB * 1024));
-    HIP_TRY(h->qerr.ensure((size_t)Bp * 2 * 8));
+    const bool piped = st_tail != st && mode == 0;
+    if (!piped) st_tail = st;
+    Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
+    if (piped) {
+        h->flip ^= 1;
+        if (!sc.scanned) HIP_TRY(hipEventCreateWithFlags(&sc.scanned, hipEventDisableTiming));
+        if (!sc.released) HIP_TRY(hipEventCreateWithFlags(&sc.released, hipEventDisableTiming));
+        // the set's previous batch must be through select/rescore before its buffers are rewritten
+        if (sc.armed) HIP_TRY(hipStreamWaitEvent(st, sc.released, 0));
+    }
+    const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
+    HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
+    HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
+    HIP_TRY(sc.qerr.ensure((size_t)Bp * 2 * 8));
     // row parts for the group-max bound: 32 groups bound the 32nd best, so kc > 32 needs ceil(kc/32) parts
     const int np = mode == 0 ? (kc + 31) / 32 : 1;
-    HIP_TRY(h->mkeys.ensure((size_t)np * Bp * 32 * 4));
-    HIP_TRY(h->floor_q.ensure((size_t)Bp * 4));
-    HIP_TRY(h->cnt.ensure((size_t)Bp * 4));
-    HIP_TRY(h->buf.ensure((size_t)Bp * kCap * 8));
-    HIP_TRY(h->sel_rows.ensure((size_t)Bp * std::max(kc, cap_out) * 4));
-    HIP_TRY(h->sel_cnt.ensure((size_t)Bp * 4));
-    HIP_TRY(h->bound_approx.ensure((size_t)Bp * 4));
-    HIP_TRY(h->overflow.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.mkeys.ensure((size_t)np * Bp * 32 * 4));
+    HIP_TRY(sc.floor_q.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.cnt.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.buf.ensure((size_t)Bp * kCap * 8));
+    HIP_TRY(sc.sel_rows.ensure((size_t)Bp * std::max(kc, cap_out) * 4));
+    HIP_TRY(sc.sel_cnt.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.bound_approx.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.overflow.ensure((size_t)Bp * 4));
+    HIP_TRY(sc.dyn_q.ensure(256));
 
     static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int MT = mfma_type(h->dtype);
-    float* fl = (mode == 0 && !(dbg & 1)) ? h->floor_q.as<float>() : nullptr;  // else uploaded below
+    float* fl = (mode == 0 && !(dbg & 1)) ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad,
-                           h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           h->mkeys.as<uint32_t>(), np, h->cnt.as<uint32_t>(), fl);
+                           h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                           sc.mkeys.as<uint32_t>(), np, sc.cnt.as<uint32_t>(), fl, sc.dyn_q.as<uint32_t>());
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
-                           pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           h->mkeys.as<uint32_t>(), np, h->cnt.as<uint32_t>(), fl);
+                           pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                           sc.mkeys.as<uint32_t>(), np, sc.cnt.as<uint32_t>(), fl, sc.dyn_q.as<uint32_t>());
     HIP_TRY(hipGetLastError());
 
     // floors: padded queries never collect; mode 1 uses kth - E (computed on the host from qerr)
@@ -456,7 +517,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
     if (mode == 1) {
         std::vector<double> qerr((size_t)Bp * 2);
-        HIP_TRY(hipMemcpyAsync(qerr.data(), h->qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         for (int b = 0; b < B; ++b) {
             const double kth = kth_dev_host[b];
@@ -476,7 +537,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     if (!fl) {
         if (dbg & 1)
             for (auto& f : h->floor_host) f = INFINITY;
-        HIP_TRY(hipMemcpyAsync(h->floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(sc.floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
     }
 
     const int64_t n_tiles = (h->n + 31) / 32;
@@ -484,15 +545,15 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.rows = h->rows;
     a.live = h->live;
     a.mask = (const uint32_t*)mask_dev;
-    a.qfrag = h->qfrag.as<uint16_t>();
+    a.qfrag = sc.qfrag.as<uint16_t>();
     a.S = h->S;
-    a.mkeys = h->mkeys.as<uint32_t>();
+    a.mkeys = sc.mkeys.as<uint32_t>();
     a.np = np;
     a.part_tiles = np > 1 ? std::max<int64_t>(1, (n_tiles + np - 1) / np) : ((int64_t)1 << 62);
     a.pstride = (int64_t)Bp * 32;
-    a.floor_q = h->floor_q.as<float>();
-    a.cnt = h->cnt.as<uint32_t>();
-    a.buf = h->buf.as<float2>();
+    a.floor_q = sc.floor_q.as<float>();
+    a.cnt = sc.cnt.as<uint32_t>();
+    a.buf = sc.buf.as<float2>();
     a.cap = kCap;
     static const int refresh_env = getenv("HIPRAG_REFRESH") ? atoi(getenv("HIPRAG_REFRESH")) : 0;
     a.publish = (dbg & 8) ? 0 : (dbg & 16) ? 2 : 1;
@@ -525,14 +586,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             a.sample_stride = std::max<int64_t>(1, n_tiles / target);
             a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], st));
-            if (int rc = launch_scan(h, pl, a, SCAN_SAMPLE, st)) return rc;
+            if (int rc = launch_scan(h, sc, cus, pl, a, SCAN_SAMPLE, st)) return rc;
             if (timed) HIP_TRY(hipEventRecord(ev.e[1], st));
             ev.sampled = true;
         }
         a.sample_stride = 1;
         a.n_units = n_tiles;
         if (timed) HIP_TRY(hipEventRecord(ev.e[2], st));
-        if (int rc = launch_scan(h, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
+        if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
         if (timed) {
             HIP_TRY(hipEventRecord(ev.e[3], st));
             h->ev_pending.push_back(ev);
@@ -541,6 +602,10 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
                 h->ev_pending.pop_front();
             }
         }
+    }
+    if (piped) {  // the tail stream picks the batch up once its FILTER is done
+        HIP_TRY(hipEventRecord(sc.scanned, st));
+        HIP_TRY(hipStreamWaitEvent(st_tail, sc.scanned, 0));
     }
     // select
     const int kc_sel = mode == 0 ? kc : cap_out;
@@ -551,28 +616,32 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         sel_attr[h->device & 63] = true;
     }
     const bool priv = a.private_bufs && n_tiles > 0;
-    hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st, h->cnt.as<uint32_t>(), h->buf.as<float2>(),
-                       kCap, priv ? h->pcnt.as<uint32_t>() : nullptr, priv ? h->pbuf.as<float2>() : nullptr,
-                       (int)h->last_W, kCapW, Bp, h->mkeys.as<uint32_t>(), np, h->floor_q.as<float>(), a.use_groups, B, kc_sel,
-                       h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), h->bound_approx.as<float>(),
-                       h->overflow.as<int>());
+    hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st_tail, sc.cnt.as<uint32_t>(), sc.buf.as<float2>(),
+                       kCap, priv ? sc.pcnt.as<uint32_t>() : nullptr, priv ? sc.pbuf.as<float2>() : nullptr,
+                       (int)sc.last_W, kCapW, Bp, sc.mkeys.as<uint32_t>(), np, sc.floor_q.as<float>(), a.use_groups, B, kc_sel,
+                       sc.sel_rows.as<uint32_t>(), sc.sel_cnt.as<int>(), sc.bound_approx.as<float>(),
+                       sc.overflow.as<int>());
     HIP_TRY(hipGetLastError());
     // rescore
     const int64_t nw = (int64_t)B * kc_sel;
     int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
-        hipLaunchKernelGGL((k_rescore<decltype(dt)::value>), dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st, h->rows,
-                           h->S, h->dpad, h->q32.as<float>(), h->sel_rows.as<uint32_t>(), h->sel_cnt.as<int>(), B,
-                           kc_sel, row_offset, h->bound_approx.as<float>(), h->qerr.as<double>(), max_norm,
-                           acc_gamma(h), storage_u(h), h->overflow.as<int>(), cand_out, bound_out);
+        hipLaunchKernelGGL((k_rescore<decltype(dt)::value>), dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st_tail, h->rows,
+                           h->S, h->dpad, sc.q32.as<float>(), sc.sel_rows.as<uint32_t>(), sc.sel_cnt.as<int>(), B,
+                           kc_sel, row_offset, sc.bound_approx.as<float>(), sc.qerr.as<double>(), max_norm,
+                           acc_gamma(h), storage_u(h), sc.overflow.as<int>(), cand_out, bound_out);
         HIP_TRY(hipGetLastError());
         return HR_OK;
     });
     if (rc) return rc;
+    if (piped) {
+        HIP_TRY(hipEventRecord(sc.released, st_tail));
+        sc.armed = true;
+    }
     if (mode == 1) {
         // collect mode is complete unless the candidate buffer overflowed: bound = -inf, or +inf on overflow
         std::vector<int> ovf((size_t)B), selc((size_t)B);
-        HIP_TRY(hipMemcpyAsync(ovf.data(), h->overflow.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(selc.data(), h->sel_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(ovf.data(), sc.overflow.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(selc.data(), sc.sel_cnt.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         std::vector<double> bh((size_t)B, -INFINITY);
         for (int b = 0; b < B; ++b) {
@@ -580,7 +649,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             // the window held more rows than the buffer: exact top-cap_out of the whole shard instead
             // (complete by construction, so the bound stays -inf)
             HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
-            if (int rc2 = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, h->q32.as<float>() + (int64_t)b * h->dpad,
+            if (int rc2 = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
                                           h->live, (const uint32_t*)mask_dev, h->n, row_offset, cap_out,
                                           cand_out + (int64_t)b * cap_out, h->exh.p, h->exh.bytes, st))
                 return set_err(rc2, "exhaustive exact pass failed");
@@ -593,13 +662,13 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
 }
 
 static int shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
-                        Cand* cand_out, double* bound_out, hipStream_t st) {
+                        Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail) {
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     for (int b0 = 0; b0 < B; b0 += pl.Bp) {
         const int bc = std::min(pl.Bp, B - b0);
         if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, kc, mask_dev, row_offset, nullptr, 0, 0,
-                                 cand_out + (int64_t)b0 * kc, bound_out + b0, st))
+                                 cand_out + (int64_t)b0 * kc, bound_out + b0, st, st_tail))
             return rc;
     }
     return HR_OK;
@@ -642,7 +711,8 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     HIP_TRY(h->bound.ensure((size_t)B * 8));
     HIP_TRY(h->kth.ensure((size_t)B * 8));
     HIP_TRY(h->fail.ensure((size_t)B * 4));
-    if (int rc = shard_search(h, q_dev, B, kc, mask_dev, 0, h->cand.as<Cand>(), h->bound.as<double>(), st)) return rc;
+    if (int rc = shard_search(h, q_dev, B, kc, mask_dev, 0, h->cand.as<Cand>(), h->bound.as<double>(), st, st))
+        return rc;
     if (int rc = launch_merge(h->device, h->cand.as<Cand>(), h->bound.as<double>(), 1, B, kc, k, s_out, r_out,
                               h->kth.as<double>(), h->fail.as<int32_t>(), st))
         return rc;
@@ -662,7 +732,7 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
         HIP_TRY(h->fb_bound.ensure(64));
         double kb = kth[(size_t)b];
         if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, kc2, mask_dev, 0, &kb, 1, kc2,
-                                 h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), st))
+                                 h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), st, st))
             return rc;
         double bd = 0;
         HIP_TRY(hipMemcpyAsync(&bd, h->fb_bound.p, 8, hipMemcpyDeviceToHost, st));
@@ -727,7 +797,20 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
-    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st);
+    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st, st);
+}
+
+extern "C" int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc,
+                                           const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                           double* bound_out_dev, void* scan_stream, void* tail_stream) {
+    if (!h || !q_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
+    if (scan_stream == tail_stream) return set_err(HR_E_INVALID, "scan and tail streams must differ");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    if (int rc = validate_search(h, B, k)) return rc;
+    if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
+    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev,
+                        (hipStream_t)scan_stream, (hipStream_t)tail_stream);
 }
 
 extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev, int cap,
@@ -744,7 +827,7 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
     Cand* out = (Cand*)cand_out_dev;
     for (int b = 0; b < B; ++b) {
         if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, cap, row_mask_dev, row_offset, &kth[(size_t)b], 1,
-                                 cap, out + (int64_t)b * cap, bound_out_dev + b, st))
+                                 cap, out + (int64_t)b * cap, bound_out_dev + b, st, st))
             return rc;
     }
     return HR_OK;
@@ -785,23 +868,24 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     hipStream_t st = h->stream;
+    Scratch& sc = h->scr[kSyncSet];
     const int Bp = pl.Bp;
     const int64_t n_tiles = (h->n + 31) / 32;
     HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
-    HIP_TRY(h->q32.ensure((size_t)Bp * h->dpad * 4));
-    HIP_TRY(h->qfrag.ensure((size_t)h->S * pl.QB * 1024));
-    HIP_TRY(h->qerr.ensure((size_t)Bp * 2 * 8));
+    HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
+    HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
+    HIP_TRY(sc.qerr.ensure((size_t)Bp * 2 * 8));
     HIP_TRY(h->stage.ensure((size_t)Bp * n_tiles * 32 * 4 + 16));
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     const int MT = mfma_type(h->dtype);
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
-                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           nullptr, 1, nullptr, nullptr);
+                           h->dpad, h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                           nullptr, 1, nullptr, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
-                           h->dpad, h->S, pl.QB, h->metric, h->q32.as<float>(), h->qfrag.as<uint16_t>(), h->qerr.as<double>(),
-                           nullptr, 1, nullptr, nullptr);
+                           h->dpad, h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                           nullptr, 1, nullptr, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
     const int lds = scan_lds_bytes(h, pl.QB);
     int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
@@ -812,7 +896,7 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
         auto kern = pl.QB == 1 ? k1 : k2;
         HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         hipLaunchKernelGGL(kern, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), lds, st, h->rows,
-                           h->qfrag.as<uint16_t>(), h->S, n_tiles, h->stage.as<float>());
+                           sc.qfrag.as<uint16_t>(), h->S, n_tiles, h->stage.as<float>());
         HIP_TRY(hipGetLastError());
         return HR_OK;
     });
@@ -820,7 +904,7 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     std::vector<float> tmp((size_t)Bp * n_tiles * 32);
     std::vector<double> qerr((size_t)Bp * 2);
     HIP_TRY(hipMemcpyAsync(tmp.data(), h->stage.p, tmp.size() * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(qerr.data(), h->qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
     for (int b = 0; b < B; ++b) {
@@ -948,10 +1032,10 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->rows) (void)hipFree(h->rows);
     if (h->live) (void)hipFree(h->live);
     if (h->norm_bits) (void)hipFree(h->norm_bits);
-    for (DevBuf* b : {&h->q_in, &h->q32, &h->qfrag, &h->qerr, &h->mkeys, &h->floor_q, &h->cnt, &h->buf, &h->sel_rows,
-                      &h->sel_cnt, &h->bound_approx, &h->overflow, &h->cand, &h->bound, &h->kth, &h->fail,
-                      &h->fb_cand, &h->fb_bound, &h->stage, &h->pbuf, &h->pcnt, &h->exh})
+    (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
+    for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->stage, &h->exh})
         b->release();
+    for (auto& sc : h->scr) sc.release_all();
     for (auto* list : {&h->ev_free})
         for (auto& ev : *list)
             for (auto& x : ev.e) (void)hipEventDestroy(x);
@@ -1014,11 +1098,15 @@ extern "C" int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* ma
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
     // private per-wave counts of the last FILTER scan: pcnt[W][Bp]
-    const int64_t n = h->last_W * h->last_Bp;
+    const Scratch* sc = h->last_scr;
+    const int64_t n = sc ? sc->last_W * sc->last_Bp : 0;
     std::vector<uint32_t> c((size_t)n);
-    if (n) HIP_TRY(hipMemcpy(c.data(), h->pcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-    std::vector<int64_t> per_q((size_t)h->last_Bp, 0);
-    for (int64_t i = 0; i < n; ++i) per_q[(size_t)(i % h->last_Bp)] += c[(size_t)i];
+    if (n) {
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(c.data(), sc->pcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> per_q((size_t)(sc ? sc->last_Bp : 0), 0);
+    for (int64_t i = 0; i < n; ++i) per_q[(size_t)(i % sc->last_Bp)] += c[(size_t)i];
     int64_t t = 0, m = 0;
     for (int64_t v : per_q) {
         t += v;

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
                                                 int QB, int metric, float* __restrict__ q32,
                                                 uint16_t* __restrict__ qfrag, double* __restrict__ qerr,
                                                 uint32_t* __restrict__ mkeys, int np, uint32_t* __restrict__ cnt,
-                                                float* __restrict__ floor_q) {
+                                                float* __restrict__ floor_q, uint32_t* __restrict__ dyn_q) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
@@ -109,6 +109,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     if (mkeys && lane < 32)
         for (int p = 0; p < np; ++p) mkeys[((int64_t)p * Bp + b) * 32 + lane] = HR_KEY_NEG_INF;
     if (lane == 0) {
+        if (dyn_q && b == 0) *dyn_q = 0;
         if (cnt) cnt[b] = 0;
         if (floor_q) floor_q[b] = b < B ? -__builtin_inff() : __builtin_inff();
     }
@@ -195,6 +196,13 @@ struct ScanArgs {
     float2* pbuf;
     uint32_t* pcnt;
     int capw;
+    // dynamic tail (FILTER): waves run at rates that differ by +-6 % (two waves share a SIMD and
+    // are not served fairly), so a static split ends with the slowest wave.  Units [0, dyn_start)
+    // are split statically; the rest are handed out in runs of dyn_chunk units from a counter
+    // (zeroed by k_prep_q), grabbed while a wave works on the last unit of its current run.
+    int64_t dyn_start;       // == n_units: no dynamic part
+    int dyn_chunk;
+    uint32_t* dyn_q;
 };
 
 template <int MT>
@@ -287,7 +295,9 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     // get one extra unit sit on different CUs (the tail is then one tile per CU, not a
     // handful of fully loaded CUs finishing a tile after everyone else)
     const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * gridDim.x + blockIdx.x : w;
-    const int64_t base = a.n_units / W, rem = a.n_units % W;
+    const bool dyn = MODE == SCAN_FILTER && a.dyn_start < a.n_units;  // launch-uniform
+    const int64_t n_static = dyn ? a.dyn_start : a.n_units;
+    const int64_t base = n_static / W, rem = n_static % W;
     const int64_t u0 = wr * base + (wr < rem ? wr : rem);
     const int64_t u1 = u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
@@ -412,9 +422,36 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     if (FILTER) refresh(false);
 
 
-    for (int64_t u = u0; u < u1; ++u) {
+    // grab the next dynamic run: first unit, or -1 when the pool is exhausted
+    // The grab is issued one unit before its result is needed (runs are >= 2 units long): the
+    // returned value then sits behind a whole unit of ring loads, so reading it costs no wait.
+    // (Reading it at once makes the compiler drain every outstanding load: vmcnt(0).)
+    auto grab_issue = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(a.dyn_q, 1u);
+        return v;
+    };
+    auto grab_resolve = [&](uint32_t v) -> int64_t {
+        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        const int64_t u = a.dyn_start + (int64_t)v * a.dyn_chunk;
+        return u < a.n_units ? u : -1;
+    };
+    int64_t u = u0, u_end = u1, pend = -1, done = 0;
+    uint32_t graw = 0;
+    bool issued = false;  // this run's grab is in flight (exactly one grab per run)
+    if (dyn && u0 >= u1) {  // no static units (tiny launches): start in the pool
+        u = grab_resolve(grab_issue());
+        if (u < 0) u = u_end = 0;
+        else u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
+    }
+    while (u < u_end) {
+        if (dyn && !issued && u + 2 >= u_end) {  // a 1-unit run issues and resolves at once
+            graw = grab_issue();
+            issued = true;
+        }
+        if (dyn && u + 1 == u_end) pend = grab_resolve(graw);  // this unit's last k-steps prefetch its first unit
         const int64_t t = u * stride;
-        const int64_t tn = (u + 1 < u1) ? (u + 1) * stride : t;
+        const int64_t tn = (u + 1 < u_end) ? (u + 1) * stride : (pend >= 0 ? pend * stride : t);
         if (t >= part_end) {  // wave-uniform; never taken with one part
             if (MODE != SCAN_COLLECT && a.use_groups) flush();
             const int64_t np_ = t / a.part_tiles;
@@ -495,7 +532,18 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
                     }
                 }
         }
-        if (MODE == SCAN_FILTER && ((u - u0 + 1) % a.refresh_every) == 0) refresh(true);
+        ++done;
+        if (MODE == SCAN_FILTER && (done % a.refresh_every) == 0) refresh(true);
+        if (u + 1 < u_end) {
+            ++u;
+        } else if (pend >= 0 && done < a.n_units) {  // (done bound: termination even if the counter were corrupt)
+            u = pend;
+            u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
+            pend = -1;
+            issued = false;
+        } else {
+            break;
+        }
     }
 
     if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;

@@ -13,10 +13,13 @@ guard fails (top-k not provably complete) are re-scanned in collect mode: every
 shard returns all rows whose approximate score could still reach the k-th exact
 score, and a second merge is exact by construction.
 
-Batches can be pipelined: ``submit`` enqueues a whole batch (scan, gather, merge,
-a non-blocking copy of the guard flags) and returns a ticket; ``finalize`` waits for
-that batch's flags only and runs the (rare) fallback.  With ``depth`` tickets in
-flight the host's per-batch work overlaps the GPU's.
+Batches are pipelined at two levels.  On the GPU, each batch's scan runs on the caller's
+stream over all but a few CUs, while the previous batch's select/rescore, all-gather and
+merge run on a second ("tail") stream on the CUs left free -- the scan reads HBM as fast
+on 224 CUs as on 256, so the tail costs no scan time.  On the host, ``submit`` enqueues a
+whole batch (scan, tail, a non-blocking copy of the guard flags) and returns a ticket;
+``finalize`` waits for that batch's flags only and runs the (rare) fallback.  With
+``depth`` tickets in flight the host's per-batch work overlaps the GPU's.
 
 The reference is single-process (SURVEY.md §2 "Parallelism strategies: none");
 this module is the C1 collective of the SURVEY kernel inventory.
@@ -57,7 +60,7 @@ class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
     def __init__(self, index, row_offset: int, max_batch: int, kc: int | None = None, group=None,
-                 device=None, depth: int = 2, max_k: int = 32):
+                 device=None, depth: int = 2, max_k: int = 32, overlap: bool = True):
         import torch
         import torch.distributed as dist
 
@@ -72,6 +75,8 @@ class ShardedSearch:
         pinned = self.device.type == "cuda"
         self.slots = [_Slot(torch, self.device, self.G, self.max_batch, self.kc, pinned) for _ in range(max(1, depth))]
         self._next = 0
+        # tail stream: select/rescore, all-gather, merge and the flag copy of each batch
+        self.tail = torch.cuda.Stream(self.device) if (overlap and pinned) else None
 
     # hooks (overridden in CPU tests of the orchestration logic)
     def _stream(self) -> int:
@@ -85,8 +90,9 @@ class ShardedSearch:
                                  cand_rank_stride=cand_all.stride(0) * 8, bound_rank_stride=bound_all.stride(0) * 8)
 
     def _shard_search(self, q, k, cand, bound, mask_ptr):
+        tail = self.tail.cuda_stream if self.tail is not None else None
         self.index.search_shard(q.data_ptr(), q.shape[0], k, self.kc, self.row_offset, cand.data_ptr(),
-                                bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+                                bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream(), tail_stream=tail)
 
     def _shard_collect(self, q, kth, cap, cand, bound, mask_ptr):
         self.index.search_shard_collect(q.data_ptr(), q.shape[0], kth.data_ptr(), cap, self.row_offset,
@@ -127,6 +133,18 @@ class ShardedSearch:
         rec = slot.rec[:L]
         cand, bound = _record_views(rec, B, self.kc)
         self._shard_search(q, k, cand, bound, mask_ptr)
+        if self.tail is not None:
+            # the caller's writes to s_out/r_out (allocation, earlier use) happen on its stream
+            self.tail.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.tail):
+                self._exchange_and_merge(slot, rec, L, B, k, s_out, r_out)
+        else:
+            self._exchange_and_merge(slot, rec, L, B, k, s_out, r_out)
+        slot.ticket = (q, k, s_out, r_out, mask_ptr, B)
+        return slot
+
+    def _exchange_and_merge(self, slot, rec, L, B, k, s_out, r_out):
+        torch = self.torch
         if self.G == 1:  # nothing to exchange: merge straight from this shard's candidates
             rec_all = rec.view(1, L)
         else:  # ONE collective per batch: every rank's packed record
@@ -140,8 +158,6 @@ class ShardedSearch:
             slot.event.record(torch.cuda.current_stream(self.device))
         else:
             slot.fail_h[:B].copy_(fail)
-        slot.ticket = (q, k, s_out, r_out, mask_ptr, B)
-        return slot
 
     def finalize(self, slot) -> tuple:
         """Wait for a submitted batch's guard flags (only those) and run its fallback if needed."""

@@ -34,7 +34,7 @@
  * and run on the given hipStream_t (NULL = the null stream, which is also
  * PyTorch's default stream); host-pointer calls use the handle's own stream and
  * return after synchronising it.  Scores follow the
- * reference's similarity convention (cosine/dot: inner product).  Result order:
+ * reference's similarity convention (cosine/dot: inner product; euclidean: 1 - |q - x|^2).  Result order:
  * score descending, then row ascending; unfilled slots hold score -inf, row -1.
  */
 #ifndef HIPRAG_H
@@ -49,7 +49,10 @@ extern "C" {
 typedef struct hr_index hr_index;
 
 enum { HR_F32 = 0, HR_BF16 = 1, HR_F16 = 2 };         /* storage dtype */
-enum { HR_COSINE = 0, HR_IP = 1, HR_L2 = 2 };         /* distance metric (L2: not yet on the GPU path) */
+/* distance metric (chroma_store.py:48-53): cosine (rows + queries L2-normalised, score = inner
+ * product), ip ("dot": raw inner product), l2 ("euclidean": score = 1 - squared distance, Chroma's
+ * similarity = 1 - distance, :135) */
+enum { HR_COSINE = 0, HR_IP = 1, HR_L2 = 2 };
 enum {
     HR_OK = 0,
     HR_E_INVALID = -1,   /* bad argument -> Python ValueError */

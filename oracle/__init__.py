@@ -25,7 +25,7 @@ from . import ref_numpy  # noqa: F401
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libhr_oracle.so")
 DTYPES = {"f32": 0, "bf16": 1, "f16": 2}
-METRICS = {"cosine": 0, "ip": 1}
+METRICS = {"cosine": 0, "ip": 1, "dot": 1, "l2": 2, "euclidean": 2}
 _lib = None
 
 
@@ -45,10 +45,10 @@ def lib():
         L.hro_normalize_rows.argtypes = [vp, i64, i32, vp]
         L.hro_quantize.argtypes = [vp, i64, i32, i32, vp]
         L.hro_build_synthetic.argtypes = [u64, i64, i64, i32, i32, i32, vp, i32]
-        L.hro_search.argtypes = [vp, i32, i64, i32, vp, i32, i32, vp, i64, vp, vp, i32]
+        L.hro_search.argtypes = [vp, i32, i64, i32, vp, i32, i32, vp, i64, vp, vp, i32, i32]
         L.hro_search_synthetic.argtypes = [u64, i64, i64, i32, i32, i32, vp, i32, i32, vp, vp, i32]
         L.hro_search_synthetic.restype = i32
-        L.hro_score_pairs.argtypes = [vp, i32, i32, vp, vp, vp, i64, vp]
+        L.hro_score_pairs.argtypes = [vp, i32, i32, vp, vp, vp, i64, vp, i32]
         L.hro_norm2.argtypes = [vp, i32]
         L.hro_norm2.restype = ctypes.c_double
         _lib = L
@@ -95,8 +95,9 @@ def c_build_synthetic(seed: int, row0: int, n: int, dim: int, dtype: str, metric
 
 
 def c_search(stored: np.ndarray, dtype: str, q: np.ndarray, k: int, mask: np.ndarray | None = None,
-             row_offset: int = 0, nthreads: int | None = None):
-    """Exact top-k over stored rows; q must already be processed (normalised for cosine)."""
+             row_offset: int = 0, nthreads: int | None = None, metric: str = "cosine"):
+    """Exact top-k over stored rows; q must already be processed (normalised for cosine).
+    cosine / ip score = inner product; l2 (euclidean) score = 1 - squared distance."""
     stored = np.ascontiguousarray(stored)
     q = np.ascontiguousarray(q, np.float32)
     B, dim = q.shape
@@ -104,7 +105,8 @@ def c_search(stored: np.ndarray, dtype: str, q: np.ndarray, k: int, mask: np.nda
     r = np.empty((B, k), np.int64)
     m = None if mask is None else np.ascontiguousarray(mask, np.uint64)
     lib().hro_search(_p(stored), DTYPES[dtype], stored.shape[0], dim, _p(q), B, k,
-                     None if m is None else _p(m), row_offset, _p(s), _p(r), nthreads or default_threads())
+                     None if m is None else _p(m), row_offset, _p(s), _p(r), nthreads or default_threads(),
+                     METRICS[metric])
     return s, r
 
 
@@ -121,13 +123,15 @@ def c_search_synthetic(seed: int, row0: int, n: int, dim: int, dtype: str, metri
     return s, r
 
 
-def c_score_pairs(stored: np.ndarray, dtype: str, q: np.ndarray, qidx: np.ndarray, rows: np.ndarray) -> np.ndarray:
+def c_score_pairs(stored: np.ndarray, dtype: str, q: np.ndarray, qidx: np.ndarray, rows: np.ndarray,
+                  metric: str = "cosine") -> np.ndarray:
     stored = np.ascontiguousarray(stored)
     q = np.ascontiguousarray(q, np.float32)
     qi = np.ascontiguousarray(qidx, np.int32)
     rr = np.ascontiguousarray(rows, np.int64)
     out = np.empty(len(rr), np.float64)
-    lib().hro_score_pairs(_p(stored), DTYPES[dtype], q.shape[1], _p(q), _p(qi), _p(rr), len(rr), _p(out))
+    lib().hro_score_pairs(_p(stored), DTYPES[dtype], q.shape[1], _p(q), _p(qi), _p(rr), len(rr), _p(out),
+                          METRICS[metric])
     return out
 
 

@@ -15,6 +15,12 @@
  *     an exhaustive inner-product scan returning the k largest scores.
  *   - Chroma's hnsw "ip" space for distance_metric="dot" (chroma_store.py:48-53,
  *     similarity = 1 - distance = inner product, :135).
+ *   - Chroma's hnsw "l2" space for distance_metric="euclidean" (chroma_store.py:48-53):
+ *     distance = squared L2 (hnswlib's l2 space), similarity = 1 - distance (:135);
+ *     rows and queries are stored raw.  chromadb 1.3.4 (uv.lock:764-765) is not vendored
+ *     and its HNSW is approximate; the exact restatement ranks every row by
+ *       score = 1 - ((|q|^2 - 2 q.x) + |x|^2)
+ *     with the three terms canonical fp64 sums (below) combined in that order.
  *
  * Canonical arithmetic (shared bit-for-bit with the HIP kernels):
  *   - every dot product / squared norm is an fp64 sum in a fixed order:
@@ -48,6 +54,7 @@
 
 #define HRO_COSINE 0
 #define HRO_IP 1
+#define HRO_L2 2
 
 uint64_t hro_mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -249,12 +256,22 @@ static inline int row_allowed(const uint64_t* mask, int64_t r) {
  */
 typedef void (*row_source_fn)(void* ctx, int64_t r, double* dst);
 
+/* score of one row: inner product (cosine on normalised rows, ip), or the euclidean similarity */
+static inline double row_score(const double* xr, const double* qv, int dim, int metric, double qn2) {
+    double dot = hro_canon_dot(xr, qv, dim);
+    if (metric != HRO_L2) return dot;
+    double xn2 = hro_canon_dot(xr, xr, dim);
+    return 1.0 - ((qn2 - 2.0 * dot) + xn2);
+}
+
 static void search_generic(row_source_fn src, void* ctx, int64_t n, int dim, const float* q, int B, int k,
                            const uint64_t* mask, int64_t row_offset, double* scores_out, int64_t* rows_out,
-                           int nthreads) {
+                           int nthreads, int metric) {
     int nt = nthreads > 0 ? nthreads : 1;
     double* qd = (double*)malloc(sizeof(double) * (size_t)B * dim);
     for (size_t i = 0; i < (size_t)B * dim; ++i) qd[i] = (double)q[i];
+    double* qn2 = (double*)malloc(sizeof(double) * (size_t)B);
+    for (int b = 0; b < B; ++b) qn2[b] = hro_canon_dot(qd + (size_t)b * dim, qd + (size_t)b * dim, dim);
     double* all_s = (double*)malloc(sizeof(double) * (size_t)nt * B * k);
     int64_t* all_r = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt * B * k);
     int* all_c = (int*)calloc((size_t)nt * B, sizeof(int));
@@ -273,7 +290,7 @@ static void search_generic(row_source_fn src, void* ctx, int64_t n, int dim, con
             if (!row_allowed(mask, r)) continue;
             src(ctx, r, xr);
             for (int b = 0; b < B; ++b) {
-                double s = hro_canon_dot(xr, qd + (size_t)b * dim, dim);
+                double s = row_score(xr, qd + (size_t)b * dim, dim, metric, qn2[b]);
                 topk_insert(ls + (size_t)b * k, lr + (size_t)b * k, lc + b, k, s, r + row_offset);
             }
         }
@@ -294,6 +311,7 @@ static void search_generic(row_source_fn src, void* ctx, int64_t n, int dim, con
         }
     }
     free(qd);
+    free(qn2);
     free(all_s);
     free(all_r);
     free(all_c);
@@ -310,9 +328,10 @@ static void stored_src(void* c, int64_t r, double* dst) {
 }
 
 void hro_search(const void* stored, int dtype, int64_t n, int dim, const float* q, int B, int k,
-                const uint64_t* mask, int64_t row_offset, double* scores_out, int64_t* rows_out, int nthreads) {
+                const uint64_t* mask, int64_t row_offset, double* scores_out, int64_t* rows_out, int nthreads,
+                int metric) {
     stored_ctx c = {stored, dtype, dim};
-    search_generic(stored_src, &c, n, dim, q, B, k, mask, row_offset, scores_out, rows_out, nthreads);
+    search_generic(stored_src, &c, n, dim, q, B, k, mask, row_offset, scores_out, rows_out, nthreads, metric);
 }
 
 typedef struct {
@@ -341,22 +360,22 @@ int hro_search_synthetic(uint64_t seed, int64_t row0, int64_t n, int dim, int dt
                          int B, int k, double* scores_out, int64_t* rows_out, int nthreads) {
     if (dim > 4096) return -1;
     synth_ctx c = {seed, row0, dim, dtype, metric};
-    search_generic(synth_src, &c, n, dim, q, B, k, NULL, row0, scores_out, rows_out, nthreads);
+    search_generic(synth_src, &c, n, dim, q, B, k, NULL, row0, scores_out, rows_out, nthreads, metric);
     return 0;
 }
 
 /* Exact canonical scores of explicit (query, row) pairs against stored rows. */
 void hro_score_pairs(const void* stored, int dtype, int dim, const float* q, const int32_t* qidx, const int64_t* rows,
-                     int64_t npairs, double* out) {
+                     int64_t npairs, double* out, int metric) {
     double* xr = (double*)malloc(sizeof(double) * (size_t)dim);
     double* qd = (double*)malloc(sizeof(double) * (size_t)dim);
     for (int64_t i = 0; i < npairs; ++i) {
         load_row_f64(stored, dtype, rows[i], dim, xr);
         for (int d = 0; d < dim; ++d) qd[d] = (double)q[(size_t)qidx[i] * dim + d];
-        out[i] = hro_canon_dot(xr, qd, dim);
+        out[i] = row_score(xr, qd, dim, metric, hro_canon_dot(qd, qd, dim));
     }
     free(xr);
     free(qd);
 }
 
-int hro_abi_version(void) { return 1; }
+int hro_abi_version(void) { return 2; }

@@ -7,6 +7,8 @@ It restates the same algorithm as oracle/hr_oracle.c (which it cross-checks):
   * faiss ``normalize_L2`` + ``IndexFlatIP`` semantics of the reference's exact
     store, utu/rag/storage/implementations/faiss_store.py:102-108 (add),
     :148-154 (query + search), :179-180 (similarity = inner product);
+  * Chroma's "l2" space for distance_metric="euclidean" (chroma_store.py:48-53, :135):
+    similarity = 1 - squared distance, exact;
   * the canonical fp64 summation order (64 strided lanes, then the butterfly
     p[i] += p[i+off], off = 32..1) that makes GPU and CPU scores bit-identical;
   * result order (score desc, row asc).
@@ -122,17 +124,24 @@ def process_queries(q: np.ndarray, metric: str) -> np.ndarray:
     return normalize_rows(q) if metric == "cosine" else q.copy()
 
 
-def exact_scores(stored: np.ndarray, dtype: str, q: np.ndarray) -> np.ndarray:
-    """B×N canonical fp64 scores of processed queries against stored rows."""
+def exact_scores(stored: np.ndarray, dtype: str, q: np.ndarray, metric: str = "cosine") -> np.ndarray:
+    """B×N canonical fp64 scores of processed queries against stored rows: the inner product
+    (cosine, ip), or for l2 / euclidean Chroma's similarity 1 - squared distance, evaluated as
+    1 - ((|q|^2 - 2 q.x) + |x|^2) with canonical terms (chroma_store.py:48-53, :135)."""
     x = dequantize(stored, dtype).astype(np.float64)
     qd = np.asarray(q, np.float32).astype(np.float64)
-    return canon_sum(qd[:, None, :] * x[None, :, :])
+    dot = canon_sum(qd[:, None, :] * x[None, :, :])
+    if metric not in ("l2", "euclidean"):
+        return dot
+    qn2 = canon_sum(qd * qd)
+    xn2 = canon_sum(x * x)
+    return 1.0 - ((qn2[:, None] - 2.0 * dot) + xn2[None, :])
 
 
 def search(stored: np.ndarray, dtype: str, q: np.ndarray, k: int, allowed: np.ndarray | None = None,
-           row_offset: int = 0):
+           row_offset: int = 0, metric: str = "cosine"):
     """Exact top-k: (scores f64 B×k, rows i64 B×k), order (score desc, row asc), -inf/-1 padding."""
-    s = exact_scores(stored, dtype, q)
+    s = exact_scores(stored, dtype, q, metric)
     n = s.shape[1]
     rows = np.arange(n, dtype=np.int64)
     B = s.shape[0]

@@ -45,7 +45,7 @@ class OracleIndex:
             bits = np.unpackbits(np.asarray(mask, np.uint64).view(np.uint8), bitorder="little")[: len(allowed)]
             allowed &= bits.astype(bool)
         s, r = oracle.c_search(self.rows, self.dtype, R.process_queries(q, self.metric), k,
-                               oracle.mask_from_bool(allowed), nthreads=2)
+                               oracle.mask_from_bool(allowed), nthreads=2, metric=self.metric)
         return s.astype(np.float32), r
 
     def close(self):

@@ -415,3 +415,100 @@ def test_approx_error_within_guard_bound(native, dim, dtype, B):
     err = np.abs(approx.astype(np.float64) - exact).max(axis=1)
     print(f"{dim}/{dtype}: max |approx-exact| = {err.max():.3e}, min E = {E.min():.3e}")
     assert np.all(err <= E), (err, E)
+
+
+# ---------------------------------------------------------------- euclidean (Chroma hnsw "l2")
+# similarity = 1 - squared L2 distance (chroma_store.py:48-53, :135) over raw vectors; the oracle's
+# exact restatement (hr_oracle.c row_score) is the reference for ids and bits.  chromadb is not
+# importable here, so the L2 convention is pinned by the reference's own mapping, not a fixture.
+def _embedding_like(rng, n, dim, scale=1.0):
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    return (x * (scale * (0.5 + rng.random((n, 1))))).astype(np.float32)  # norms spread over [0.5, 1.5]·scale
+
+
+L2_CASES = [(128, "bf16", 5000, 16, 10), (768, "f16", 20000, 64, 10), (1024, "f32", 8000, 33, 5),
+            (256, "bf16", 9000, 20, 100), (96, "bf16", 700, 5, 32), (1024, "bf16", 600_000 // 20, 64, 10)]
+
+
+@pytest.mark.parametrize("dim,dtype,n,B,k", L2_CASES)
+def test_euclidean_vs_oracle(native, dim, dtype, n, B, k):
+    rng = np.random.default_rng(dim * 3 + k)
+    x = _embedding_like(rng, n, dim, scale=3.0)
+    idx = native.NativeIndex(dim, dtype, "l2")
+    idx.add(x)
+    j = rng.choice(n, B // 2, replace=False)
+    q = np.concatenate([x[j] + 0.05 * rng.standard_normal((len(j), dim)).astype(np.float32),
+                        _embedding_like(rng, B - B // 2, dim, scale=3.0)]).astype(np.float32)
+    stored = R.process_rows(x, "l2", dtype)
+    allowed = rng.random(n) < 0.6
+    for mask in (None, oracle.mask_from_bool(allowed)):
+        s, r = idx.search(q, k, mask)
+        s_ref, r_ref = oracle.c_search(stored, dtype, q, k, mask, metric="l2")
+        _check(s, r, s_ref, r_ref)
+    np.testing.assert_array_equal(r[: len(j), 0][allowed[j]], j[allowed[j]])  # a planted row is its query's nearest
+
+
+@pytest.mark.parametrize("dim,dtype", [(128, "bf16"), (768, "f16"), (200, "f32")])
+def test_euclidean_approx_error_within_guard_bound(native, dim, dtype):
+    """Scan score 2 q̂.x - |x|^2 (fp32) within E of the exact 2 q.x - |x|^2 for every row."""
+    rng = np.random.default_rng(dim)
+    n, B = 3000, 24
+    x = _embedding_like(rng, n, dim, scale=2.0)
+    idx = native.NativeIndex(dim, dtype, "l2")
+    idx.add(x)
+    q = _embedding_like(rng, B, dim, scale=2.0)
+    approx, E = idx.debug_approx(q)
+    xs = R.dequantize(R.process_rows(x, "l2", dtype), dtype).astype(np.float64)
+    qd = q.astype(np.float64)
+    exact = 2.0 * R.canon_sum(qd[:, None, :] * xs[None]) - R.canon_sum(xs * xs)[None, :]
+    err = np.abs(approx.astype(np.float64) - exact).max(axis=1)
+    print(f"l2 {dim}/{dtype}: max |approx-exact| = {err.max():.3e}, min E = {E.min():.3e}")
+    assert np.all(err <= E), (err, E)
+
+
+def test_euclidean_ties_save_load_and_shards(native, tmp_path):
+    """300 identical rows (exhaustive exact pass for k = 100), a save/load round trip (row norms
+    rebuilt on load) and a two-shard device merge, all equal to the oracle."""
+    torch = pytest.importorskip("torch")
+    dim, n = 128, 8000
+    rng = np.random.default_rng(11)
+    x = _embedding_like(rng, n, dim)
+    dups = np.sort(rng.choice(n, 300, replace=False))
+    x[dups] = x[dups[0]]
+    idx = native.NativeIndex(dim, "bf16", "l2")
+    idx.add(x)
+    stored = R.process_rows(x, "l2", "bf16")
+    s, r = idx.search(x[dups[:1]].copy(), 100)
+    s_ref, r_ref = oracle.c_search(stored, "bf16", x[dups[:1]], 100, metric="l2")
+    _check(s, r, s_ref, r_ref)
+    np.testing.assert_array_equal(r[0], dups[:100])
+    p = str(tmp_path / "l2.hri")
+    idx.save(p)
+    idx2 = native.NativeIndex.load(p, dim=dim, dtype="bf16", metric="l2")
+    q = _embedding_like(rng, 24, dim)
+    s1, r1 = idx.search(q, 10)
+    s2, r2 = idx2.search(q, 10)
+    np.testing.assert_array_equal(r1, r2)
+    np.testing.assert_array_equal(s1, s2)
+    _check(s1, r1, *oracle.c_search(stored, "bf16", q, 10, metric="l2"))
+    cut, kc, B, k = 3001, 32, 24, 10
+    shards = [native.NativeIndex(dim, "bf16", "l2") for _ in range(2)]
+    shards[0].add(x[:cut])
+    shards[1].add(x[cut:])
+    qd = torch.from_numpy(q).cuda()
+    cand = torch.empty((2, B, kc, 2), dtype=torch.float64, device="cuda")
+    bounds = torch.empty((2, B), dtype=torch.float64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for g, (sh, off) in enumerate(zip(shards, [0, cut])):
+        sh.search_shard(qd.data_ptr(), B, k, kc, off, cand[g].data_ptr(), bounds[g].data_ptr(), stream=st)
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    rd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kth = torch.empty(B, dtype=torch.float64, device="cuda")
+    fail = torch.empty(B, dtype=torch.int32, device="cuda")
+    native.merge_candidates(0, cand.data_ptr(), bounds.data_ptr(), 2, B, kc, k, sd.data_ptr(), rd.data_ptr(),
+                            kth.data_ptr(), fail.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert fail.sum().item() == 0
+    np.testing.assert_array_equal(rd.cpu().numpy(), r1)
+    np.testing.assert_array_equal(sd.cpu().numpy(), s1)

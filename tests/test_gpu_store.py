@@ -60,3 +60,22 @@ def test_store_retriever_golden(tmp_path, golden_dir, dtype):
     assert [[c.id for c, _ in res] for res in before] == [[c.id for c, _ in res] for res in after]
     asyncio.run(store2.delete_by_document_id("doc_0"))
     assert asyncio.run(HipVectorStore(cfg).count()) == 990
+
+
+def test_euclidean_store_vs_oracle(tmp_path, golden_dir):
+    """distance_metric="euclidean" through the whole store: Chroma's l2 similarity 1 - |q - x|^2
+    (chroma_store.py:48-53, :135), exact ids and bits of the oracle."""
+    import oracle
+    from oracle import ref_numpy as R
+
+    d = dict(np.load(os.path.join(golden_dir, "c1_retrieval.npz")))
+    meta = json.load(open(os.path.join(golden_dir, "c1_retrieval.json")))
+    cfg = VectorStoreConfig(backend="hip", collection_name="c1l2", persist_directory=str(tmp_path),
+                            distance_metric="euclidean", index_params={"dtype": "f32"})
+    store = VectorStoreFactory.create(cfg)
+    asyncio.run(store.add_chunks(_chunks(d, meta)))
+    s_ref, r_ref = oracle.c_search(R.process_rows(d["corpus"], "l2", "f32"), "f32", d["queries"], 5, metric="l2")
+    for b, q in enumerate(d["queries"]):
+        res = asyncio.run(store.search(query_embedding=q.tolist(), top_k=5))
+        assert [c.id for c, _ in res] == [f"chunk_{x}" for x in r_ref[b]]
+        np.testing.assert_array_equal(np.array([s for _, s in res], np.float32), s_ref[b].astype(np.float32))

@@ -127,8 +127,25 @@ def test_factory_and_config():
     with pytest.raises(ValueError):
         VectorStoreFactory.create(cfg.model_copy(update={"backend": "milvus"}))
     assert "***" in repr(VectorStoreConfig(api_key="secret")) and "secret" not in repr(VectorStoreConfig(api_key="secret"))
-    with pytest.raises(NotImplementedError):
-        HipVectorStore(VectorStoreConfig(distance_metric="euclidean"), index_factory=lambda d: None)
+    # distance_metric -> index metric (chroma_store.py:48-53: euclidean = hnsw "l2", dot = "ip")
+    assert HipVectorStore(VectorStoreConfig(distance_metric="euclidean", index_params={"persist": False}),
+                          index_factory=lambda d: None).metric == "l2"
+    assert HipVectorStore(VectorStoreConfig(distance_metric="dot", index_params={"persist": False}),
+                          index_factory=lambda d: None).metric == "ip"
+
+
+def test_euclidean_store_semantics():
+    """euclidean: similarity = 1 - squared L2 distance (Chroma l2 space, chroma_store.py:48-53, :135),
+    nearest rows first, raw (unnormalised) vectors."""
+    store = HipVectorStore(VectorStoreConfig(distance_metric="euclidean", index_params={"persist": False,
+                                                                                            "dtype": "f32"}),
+                           index_factory=lambda d: OracleIndex(d, "f32", "l2"))
+    vecs = [[0.0, 0.0], [1.0, 0.0], [3.0, 4.0], [0.5, 0.5]]
+    asyncio.run(store.add_chunks([Chunk(id=f"e{i}", content=str(i), document_id="d", chunk_index=i, embedding=v)
+                                  for i, v in enumerate(vecs)]))
+    res = asyncio.run(store.search(query_embedding=[1.0, 0.0], top_k=3))
+    assert [c.id for c, _ in res] == ["e1", "e3", "e0"]
+    np.testing.assert_allclose([s for _, s in res], [1.0, 0.5, 0.0])
 
 
 def test_chunker_golden(golden_dir):

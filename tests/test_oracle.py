@@ -28,6 +28,28 @@ def test_c_and_numpy_agree_bitwise():
             assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
 
 
+def test_euclidean_c_numpy_and_direct_formula():
+    """l2 (euclidean): C and numpy restatements agree bit-for-bit, and the canonical
+    1 - ((|q|^2 - 2 q.x) + |x|^2) matches Chroma's similarity 1 - squared distance computed
+    directly (chroma_store.py:48-53 hnsw "l2", :135) to fp64 rounding."""
+    rng = np.random.default_rng(3)
+    for dim in (7, 64, 130):
+        x = rng.standard_normal((400, dim)).astype(np.float32)
+        for dt in ("f32", "bf16", "f16"):
+            st = R.process_rows(x, "l2", dt)
+            q = rng.standard_normal((5, dim)).astype(np.float32)
+            allowed = rng.random(400) < 0.8
+            s1, r1 = oracle.c_search(st, dt, q, 9, oracle.mask_from_bool(allowed), metric="l2")
+            s2, r2 = R.search(st, dt, q, 9, allowed, metric="l2")
+            assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
+            xs = R.dequantize(st, dt).astype(np.float64)
+            direct = 1.0 - ((q.astype(np.float64)[:, None, :] - xs[None]) ** 2).sum(-1)
+            np.testing.assert_allclose(np.take_along_axis(direct, r1, 1), s1, rtol=0, atol=1e-9 * dim)
+            assert np.all(np.diff(s1, axis=1) <= 0)
+            pairs = oracle.c_score_pairs(st, dt, q, np.repeat(np.arange(5), 9), r1.reshape(-1), metric="l2")
+            assert np.array_equal(pairs.reshape(5, 9), s1)
+
+
 def test_quantizers_edge_values():
     v = np.array([0.0, -0.0, 1e-40, -1e-40, 6e-8, 3e-8, 2.98e-8, 65504, 65519, 65520, 1e30, -1e30, np.inf, -np.inf,
                   1.0 + 2 ** -8, 1.0 + 3 * 2 ** -9], np.float32)

@@ -114,6 +114,24 @@ __device__ inline float gen_elem(uint64_t seed, int64_t row, int dim, int d) {
     return (float)v;
 }
 
+// Guard bound on |approx - exact| of the scan score of query q (DESIGN.md "Exactness guard"):
+// inner product E = max|x| (|q - q̂| + (gamma + u_x) |q̂|); euclidean (scan score 2 q̂.x - |x|^2 in
+// fp32) adds the doubled dot error, the fp32 rounding of |x|^2 and of the fused multiply-add.
+__device__ __host__ inline double guard_e(const double* qe, double max_norm, double gamma, double u_x, int metric) {
+    const double E = max_norm * (qe[0] * (1.0 + 1e-6) + (gamma + u_x) * qe[1]) + 1e-9;
+    if (metric != L2) return E;
+    return 2.0 * E + 0x1p-22 * (max_norm * max_norm + 2.0 * max_norm * qe[1]) + 1e-9;
+}
+
+// Exact euclidean similarity 1 - ((|q|^2 - 2 q.x) + |x|^2) from the canonical terms (oracle
+// row_score); monotone in s = 2 q.x - |x|^2 up to fp64 rounding, whose size euclid_slack bounds.
+__device__ __host__ inline double euclid_score(double qn2, double dot, double xn2) {
+    return 1.0 - ((qn2 - 2.0 * dot) + xn2);
+}
+__device__ __host__ inline double euclid_slack(double qn2, double max_norm) {
+    return 0x1p-50 * (1.0 + qn2 + max_norm * max_norm + 2.0 * max_norm * __builtin_sqrt(qn2));
+}
+
 __device__ inline double wave_butterfly_sum(double p) {  // canonical: p[i] + p[i ^ off], off = 32..1
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {

@@ -21,7 +21,8 @@ namespace {
 // one wave per row; key 0 (below d2key(-inf)) marks rows that are deleted or masked out
 template <int DT>
 __global__ __launch_bounds__(256) void k_exact_all(const uint8_t* __restrict__ rows, int S, int dpad,
-                                                   const float* __restrict__ qv, const uint32_t* __restrict__ live,
+                                                   const float* __restrict__ qv, int metric, double qn2,
+                                                   const uint32_t* __restrict__ live,
                                                    const uint32_t* __restrict__ mask, int64_t n,
                                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const int lane = threadIdx.x & 63;
@@ -36,10 +37,15 @@ __global__ __launch_bounds__(256) void k_exact_all(const uint8_t* __restrict__ r
         }
         return;
     }
-    double p = 0.0;
+    double p = 0.0, x2 = 0.0;
 #pragma unroll 8
-    for (int d = lane; d < dpad; d += 64) p = p + (double)hr::load_elem<DT>(rows, S, r, d) * (double)qv[d];
+    for (int d = lane; d < dpad; d += 64) {
+        const double x = (double)hr::load_elem<DT>(rows, S, r, d);
+        p = p + x * (double)qv[d];
+        if (metric == hr::L2) x2 = x2 + x * x;
+    }
     p = hr::wave_butterfly_sum(p);
+    if (metric == hr::L2) p = hr::euclid_score(qn2, p, hr::wave_butterfly_sum(x2));
     if (lane == 0) {
         keys[r] = hr::d2key(p);
         vals[r] = (uint32_t)r;
@@ -71,7 +77,8 @@ size_t exhaustive_scratch_bytes(int64_t n) {
 }
 
 // exact top-m (score desc, row asc) of query qv over rows [0, n) into out[0..m); empty slots -inf / -1
-int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, const uint32_t* live,
+int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
+                    const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
                     size_t scratch_bytes, hipStream_t st) {
     if (n <= 0 || m <= 0) return HR_E_INVALID;
@@ -86,9 +93,9 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
     size_t tmp_bytes = scratch_bytes - (size_t)(tmp - p);
     const dim3 grid((unsigned)((n + 3) / 4));
     switch (dtype) {
-        case HR_F32: hipLaunchKernelGGL(k_exact_all<F32>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
-        case HR_BF16: hipLaunchKernelGGL(k_exact_all<BF16>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
-        case HR_F16: hipLaunchKernelGGL(k_exact_all<F16>, grid, dim3(256), 0, st, rows, S, dpad, qv, live, mask, n, k_in, v_in); break;
+        case HR_F32: hipLaunchKernelGGL(k_exact_all<F32>, grid, dim3(256), 0, st, rows, S, dpad, qv, metric, qn2, live, mask, n, k_in, v_in); break;
+        case HR_BF16: hipLaunchKernelGGL(k_exact_all<BF16>, grid, dim3(256), 0, st, rows, S, dpad, qv, metric, qn2, live, mask, n, k_in, v_in); break;
+        case HR_F16: hipLaunchKernelGGL(k_exact_all<F16>, grid, dim3(256), 0, st, rows, S, dpad, qv, metric, qn2, live, mask, n, k_in, v_in); break;
         default: return HR_E_INVALID;
     }
     if (hipGetLastError() != hipSuccess) return HR_E_HIP;

@@ -56,7 +56,8 @@ struct DevBuf {
 
 namespace hr {  // hr_exhaustive.hip
 size_t exhaustive_scratch_bytes(int64_t n);
-int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, const uint32_t* live,
+int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
+                    const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
                     size_t scratch_bytes, hipStream_t st);
 }  // namespace hr
@@ -91,6 +92,7 @@ struct hr_index {
     double max_norm2 = 0.0;
     uint8_t* rows = nullptr;        // tiled corpus
     uint32_t* live = nullptr;       // one word per tile
+    float* xnorm = nullptr;         // euclidean only: fp32 |x|^2 per stored row (approximate scan score)
     std::vector<uint32_t> live_host;
     unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
     hipStream_t stream = nullptr;
@@ -143,8 +145,7 @@ extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const 
     *out = nullptr;
     if (dim <= 0 || dim > 4096) return set_err(HR_E_INVALID, "dim must be in [1, 4096]");
     if (dtype < F32 || dtype > F16) return set_err(HR_E_INVALID, "dtype must be HR_F32, HR_BF16 or HR_F16");
-    if (metric == L2) return set_err(HR_E_UNSUPPORTED, "metric 'euclidean' (L2) is not implemented on the HIP path yet");
-    if (metric != COSINE && metric != IP) return set_err(HR_E_INVALID, "unknown metric");
+    if (metric != COSINE && metric != IP && metric != L2) return set_err(HR_E_INVALID, "unknown metric");
     if (n_dev != 1) return set_err(HR_E_UNSUPPORTED, "one device per handle (shard across processes for multi-GPU)");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -183,6 +184,12 @@ static int grow(hr_index* h, int64_t need_rows) {
     HIP_TRY(hipMemsetAsync(nr, 0, (size_t)(new_cap / 32) * tb, h->stream));
     HIP_TRY(hipMalloc(&nl, (size_t)(new_cap / 32) * 4));
     HIP_TRY(hipMemsetAsync(nl, 0, (size_t)(new_cap / 32) * 4, h->stream));
+    float* nx = nullptr;
+    if (h->metric == L2) {
+        HIP_TRY(hipMalloc(&nx, (size_t)new_cap * 4));
+        HIP_TRY(hipMemsetAsync(nx, 0, (size_t)new_cap * 4, h->stream));
+        if (h->xnorm) HIP_TRY(hipMemcpyAsync(nx, h->xnorm, (size_t)h->cap * 4, hipMemcpyDeviceToDevice, h->stream));
+    }
     if (h->rows) {
         HIP_TRY(hipMemcpyAsync(nr, h->rows, (size_t)(h->cap / 32) * tb, hipMemcpyDeviceToDevice, h->stream));
         HIP_TRY(hipMemcpyAsync(nl, h->live, (size_t)(h->cap / 32) * 4, hipMemcpyDeviceToDevice, h->stream));
@@ -190,8 +197,13 @@ static int grow(hr_index* h, int64_t need_rows) {
         HIP_TRY(hipFree(h->rows));
         HIP_TRY(hipFree(h->live));
     }
+    if (h->xnorm) {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipFree(h->xnorm));
+    }
     h->rows = nr;
     h->live = nl;
+    h->xnorm = nx;
     h->cap = new_cap;
     h->live_host.resize((size_t)(new_cap / 32), 0u);
     return HR_OK;
@@ -225,6 +237,17 @@ static int finish_add(hr_index* h) {
     return HR_OK;
 }
 
+// euclidean: fp32 |x|^2 of stored rows [r0, r0 + n) for the approximate scan score
+static int update_row_norms(hr_index* h, int64_t r0, int64_t n) {
+    if (h->metric != L2 || n <= 0) return HR_OK;
+    return dispatch_dt(h->dtype, [&](auto dt) -> int {
+        hipLaunchKernelGGL((k_row_norms<decltype(dt)::value>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream,
+                           h->rows, h->S, h->dpad, r0, n, h->xnorm);
+        HIP_TRY(hipGetLastError());
+        return HR_OK;
+    });
+}
+
 // SRC: where the fp32 rows come from (host memory staged through h->stage, the generator, or device memory).
 enum { ADD_HOST = 0, ADD_SYNTH = 1, ADD_DEVICE = 2 };
 
@@ -256,6 +279,7 @@ static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t grow0
         if (rc) return rc;
     }
     h->n = r0 + n;
+    if (int rc = update_row_norms(h, r0, n)) return rc;
     if (int rc = mark_live(h, r0, n)) return rc;
     if (int rc = finish_add(h)) return rc;
     if (first) *first = r0;
@@ -485,7 +509,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
-    HIP_TRY(sc.qerr.ensure((size_t)Bp * 2 * 8));
+    HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
     // row parts for the group-max bound: 32 groups bound the 32nd best, so kc > 32 needs ceil(kc/32) parts
     const int np = mode == 0 ? (kc + 31) / 32 : 1;
     HIP_TRY(sc.mkeys.ensure((size_t)np * Bp * 32 * 4));
@@ -516,7 +540,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     for (int b = B; b < Bp; ++b) h->floor_host[(size_t)b] = INFINITY;
     const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
     if (mode == 1) {
-        std::vector<double> qerr((size_t)Bp * 2);
+        std::vector<double> qerr((size_t)Bp * 4);
         HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         for (int b = 0; b < B; ++b) {
@@ -525,9 +549,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
                 h->floor_host[(size_t)b] = INFINITY;  // query not in the fallback
                 continue;
             }
-            const double E = max_norm * (qerr[2 * b] * (1.0 + 1e-6) + (acc_gamma(h) + storage_u(h)) * qerr[2 * b + 1]) + 1e-9;
-            float f = (float)(kth - E);
-            if ((double)f > kth - E) f = std::nextafter(f, -INFINITY);
+            const double E = guard_e(&qerr[4 * (size_t)b], max_norm, acc_gamma(h), storage_u(h), h->metric);
+            double lo = kth - E;
+            if (h->metric == L2) {  // similarity -> scan-score space, minus the rounding slack
+                const double qn2 = qerr[4 * (size_t)b + 2];
+                lo = (kth - (1.0 - qn2)) - E - euclid_slack(qn2, max_norm);
+            }
+            float f = (float)lo;
+            if ((double)f > lo) f = std::nextafter(f, -INFINITY);
             h->floor_host[(size_t)b] = f;
         }
     }
@@ -543,6 +572,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const int64_t n_tiles = (h->n + 31) / 32;
     ScanArgs a{};
     a.rows = h->rows;
+    a.xnorm = h->metric == L2 ? h->xnorm : nullptr;
     a.live = h->live;
     a.mask = (const uint32_t*)mask_dev;
     a.qfrag = sc.qfrag.as<uint16_t>();
@@ -628,7 +658,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         hipLaunchKernelGGL((k_rescore<decltype(dt)::value>), dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st_tail, h->rows,
                            h->S, h->dpad, sc.q32.as<float>(), sc.sel_rows.as<uint32_t>(), sc.sel_cnt.as<int>(), B,
                            kc_sel, row_offset, sc.bound_approx.as<float>(), sc.qerr.as<double>(), max_norm,
-                           acc_gamma(h), storage_u(h), sc.overflow.as<int>(), cand_out, bound_out);
+                           acc_gamma(h), storage_u(h), h->metric, sc.overflow.as<int>(), cand_out, bound_out);
         HIP_TRY(hipGetLastError());
         return HR_OK;
     });
@@ -649,8 +679,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             // the window held more rows than the buffer: exact top-cap_out of the whole shard instead
             // (complete by construction, so the bound stays -inf)
             HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
+            double qn2 = 0.0;  // euclidean: the query's |q|^2 (qerr slot 2)
+            if (h->metric == L2)
+                HIP_TRY(hipMemcpy(&qn2, sc.qerr.as<double>() + 4 * (size_t)b + 2, 8, hipMemcpyDeviceToHost));
             if (int rc2 = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
-                                          h->live, (const uint32_t*)mask_dev, h->n, row_offset, cap_out,
+                                          h->metric, qn2, h->live, (const uint32_t*)mask_dev, h->n, row_offset, cap_out,
                                           cand_out + (int64_t)b * cap_out, h->exh.p, h->exh.bytes, st))
                 return set_err(rc2, "exhaustive exact pass failed");
             h->n_exhaustive++;
@@ -874,7 +907,7 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
-    HIP_TRY(sc.qerr.ensure((size_t)Bp * 2 * 8));
+    HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
     HIP_TRY(h->stage.ensure((size_t)Bp * n_tiles * 32 * 4 + 16));
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     const int MT = mfma_type(h->dtype);
@@ -896,20 +929,21 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
         auto kern = pl.QB == 1 ? k1 : k2;
         HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         hipLaunchKernelGGL(kern, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), lds, st, h->rows,
-                           sc.qfrag.as<uint16_t>(), h->S, n_tiles, h->stage.as<float>());
+                           sc.qfrag.as<uint16_t>(), h->S, n_tiles, h->metric == L2 ? h->xnorm : nullptr,
+                           h->stage.as<float>());
         HIP_TRY(hipGetLastError());
         return HR_OK;
     });
     if (rc) return rc;
     std::vector<float> tmp((size_t)Bp * n_tiles * 32);
-    std::vector<double> qerr((size_t)Bp * 2);
+    std::vector<double> qerr((size_t)Bp * 4);
     HIP_TRY(hipMemcpyAsync(tmp.data(), h->stage.p, tmp.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const double max_norm = std::sqrt(h->max_norm2) * (1.0 + 1e-12);
     for (int b = 0; b < B; ++b) {
         std::memcpy(approx_out + (size_t)b * h->n, tmp.data() + (size_t)b * n_tiles * 32, (size_t)h->n * 4);
-        e_out[b] = max_norm * (qerr[2 * b] * (1.0 + 1e-6) + (acc_gamma(h) + storage_u(h)) * qerr[2 * b + 1]) + 1e-9;
+        e_out[b] = guard_e(&qerr[4 * (size_t)b], max_norm, acc_gamma(h), storage_u(h), h->metric);
     }
     return HR_OK;
 }
@@ -1018,6 +1052,11 @@ extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr
     h->n = hd.n;
     h->n_live = hd.n_live;
     h->max_norm2 = hd.max_norm2;
+    if (int rc2 = update_row_norms(h, 0, h->n)) {
+        hr_index_destroy(h);
+        return rc2;
+    }
+    (void)hipStreamSynchronize(h->stream);
     unsigned long long bits;
     std::memcpy(&bits, &hd.max_norm2, 8);
     (void)hipMemcpy(h->norm_bits, &bits, 8, hipMemcpyHostToDevice);
@@ -1031,6 +1070,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rows) (void)hipFree(h->rows);
     if (h->live) (void)hipFree(h->live);
+    if (h->xnorm) (void)hipFree(h->xnorm);
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->stage, &h->exh})

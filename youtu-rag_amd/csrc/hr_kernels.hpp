@@ -91,9 +91,30 @@ __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uin
     if (lane == 0) atomicMax(max_norm2_bits, (unsigned long long)__builtin_bit_cast(uint64_t, sq));
 }
 
+// ---------------------------------------------------------------- K1b: stored row norms (euclidean)
+// One wave per row: |x|^2 of the stored (quantised) row in the canonical order, as fp32.  Used
+// only by the approximate scan score 2 q.x - |x|^2 (its rounding is inside the guard's bound);
+// the exact rescoring recomputes the canonical fp64 value.
+template <int DT>
+__global__ __launch_bounds__(256) void k_row_norms(const uint8_t* __restrict__ rows, int S, int dpad, int64_t r0,
+                                                   int64_t n, float* __restrict__ xnorm) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= r0 + n) return;
+    double p = 0.0;
+#pragma unroll 8
+    for (int d = lane; d < dpad; d += 64) {
+        const double x = (double)load_elem<DT>(rows, S, r, d);
+        p = p + x * x;
+    }
+    p = wave_butterfly_sum(p);
+    if (lane == 0) xnorm[r] = (float)p;
+}
+
 // ---------------------------------------------------------------- K1: query prep
 // One wave per (padded) query.  q32: normalised fp32 queries [Bp][dpad] (exact rescoring
-// operand); qfrag: MFMA A-fragments [S][QB][64 lanes][8]; qerr[2b] = ||q - q̂||, [2b+1] = ||q̂||.
+// operand); qfrag: MFMA A-fragments [S][QB][64 lanes][8]; qerr[4b] = ||q - q̂||, [4b+1] = ||q̂||,
+// [4b+2] = |q|^2 (canonical fp64 of the processed query: the euclidean score's first term).
 template <int MT>
 __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int B, int Bp, int dim, int dpad, int S,
                                                 int QB, int metric, float* __restrict__ q32,
@@ -129,7 +150,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
             scale = true;
         }
     }
-    double e1 = 0.0, nh = 0.0;
+    double e1 = 0.0, nh = 0.0, qn = 0.0;
     const int qb = b >> 5;
 #pragma unroll 8
     for (int d = lane; d < dpad; d += 64) {
@@ -143,12 +164,16 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
         double e = (double)v - (double)dq;
         e1 += e * e;
         nh += (double)dq * (double)dq;
+        qn = qn + (double)v * (double)v;
     }
     e1 = wave_butterfly_sum(e1);
     nh = wave_butterfly_sum(nh);
+    qn = wave_butterfly_sum(qn);
     if (lane == 0) {
-        qerr[2 * b] = __builtin_sqrt(e1);
-        qerr[2 * b + 1] = __builtin_sqrt(nh);
+        qerr[4 * b] = __builtin_sqrt(e1);
+        qerr[4 * b + 1] = __builtin_sqrt(nh);
+        qerr[4 * b + 2] = qn;
+        qerr[4 * b + 3] = 0.0;
     }
 }
 
@@ -203,6 +228,8 @@ struct ScanArgs {
     int64_t dyn_start;       // == n_units: no dynamic part
     int dyn_chunk;
     uint32_t* dyn_q;
+    // euclidean: approximate score 2 q̂.x - |x|^2 (fp32 |x|^2 per row); nullptr for cosine / ip
+    const float* xnorm;
 };
 
 template <int MT>
@@ -465,6 +492,9 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
+        // euclidean: this tile's row norms, loaded before the k-loop so they are back by the epilogue
+        const float xs = a.xnorm ? a.xnorm[t * 32 + g] : 0.0f;
+        const float xmul = a.xnorm ? 2.0f : 1.0f;
 
         for (int sb = 0; sb < S; sb += P) {
             const bool same = sb + P < S;
@@ -481,7 +511,13 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
             }
         }
 
-        // epilogue: predicate, group max, threshold filter
+        // epilogue: (euclidean) approximate score, predicate, group max, threshold filter
+        if (a.xnorm) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[qb][i] = __builtin_fmaf(xmul, acc[qb][i], -xs);
+        }
         uint32_t allow = a.live[t];
         if (a.mask) allow &= a.mask[t];
         const bool ok = (allow >> g) & 1u;
@@ -594,7 +630,8 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
 // error-bound test: |approx - exact| <= E_q for every row).
 template <int MT, int DT, int QB>
 __global__ __launch_bounds__(256) void k_debug_approx(const uint8_t* __restrict__ rows, const uint16_t* __restrict__ qfrag,
-                                                      int S, int64_t n_tiles, float* __restrict__ out) {
+                                                      int S, int64_t n_tiles, const float* __restrict__ xnorm,
+                                                      float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     stage_lds((u32x4*)lds, (const u32x4*)qfrag, S * QB * 64);
     __syncthreads();
@@ -615,10 +652,13 @@ __global__ __launch_bounds__(256) void k_debug_approx(const uint8_t* __restrict_
         for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma32<MT>(qs[(s * QB + qb) * 64 + lane], xf, acc[qb]);
     }
     const int64_t ncol = n_tiles * 32;
+    const float xs = xnorm ? xnorm[t * 32 + (lane & 31)] : 0.0f;  // euclidean: same score as k_scan
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) out[(int64_t)acc_query(qb, i, lane >> 5) * ncol + t * 32 + (lane & 31)] = acc[qb][i];
+        for (int i = 0; i < 16; ++i)
+            out[(int64_t)acc_query(qb, i, lane >> 5) * ncol + t * 32 + (lane & 31)] =
+                xnorm ? __builtin_fmaf(2.0f, acc[qb][i], -xs) : acc[qb][i];
 }
 
 // ---------------------------------------------------------------- K4: select top-kc
@@ -748,17 +788,19 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
                                                  const int* __restrict__ sel_cnt, int B, int kc, int64_t row_offset,
                                                  const float* __restrict__ bound_approx,
                                                  const double* __restrict__ qerr, double max_norm, double gamma,
-                                                 double u_x, const int* __restrict__ overflow, Cand* __restrict__ out,
-                                                 double* __restrict__ bound_out) {
+                                                 double u_x, int metric, const int* __restrict__ overflow,
+                                                 Cand* __restrict__ out, double* __restrict__ bound_out) {
     const int lane = threadIdx.x & 63;
     const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= (int64_t)B * kc) return;
     const int q = (int)(wid / kc), c = (int)(wid % kc);
+    const double qn2 = qerr[4 * q + 2];
     if (c == 0 && lane == 0) {
         float ba = bound_approx[q];
-        double e1 = qerr[2 * q], nh = qerr[2 * q + 1];
-        double E = max_norm * (e1 * (1.0 + 1e-6) + (gamma + u_x) * nh) + 1e-9;
+        const double E = guard_e(qerr + 4 * q, max_norm, gamma, u_x, metric);
         double bd = (ba == -__builtin_inff()) ? -__builtin_inf() : (double)ba + E;
+        // euclidean: scan-score space -> similarity space (+ the rounding slack, an upper bound)
+        if (metric == L2 && bd > -__builtin_inf()) bd = (1.0 - qn2) + bd + euclid_slack(qn2, max_norm);
         if (overflow && overflow[q]) bd = __builtin_inf();
         bound_out[q] = bd;
     }
@@ -768,10 +810,18 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
     }
     const int64_t r = (int64_t)sel_rows[q * kc + c];
     const float* qv = q32 + (int64_t)q * dpad;
-    double p = 0.0;
+    double p = 0.0, x2 = 0.0;
 #pragma unroll 8
-    for (int d = lane; d < dpad; d += 64) p = p + (double)load_elem<DT>(rows, S, r, d) * (double)qv[d];
+    for (int d = lane; d < dpad; d += 64) {
+        const double x = (double)load_elem<DT>(rows, S, r, d);
+        p = p + x * (double)qv[d];
+        if (metric == L2) x2 = x2 + x * x;
+    }
     p = wave_butterfly_sum(p);
+    if (metric == L2) {
+        x2 = wave_butterfly_sum(x2);
+        p = euclid_score(qn2, p, x2);
+    }
     if (lane == 0) out[wid] = Cand{p, r + row_offset};
 }
 

@@ -7,7 +7,8 @@ the production store) with the exact-search semantics of FAISSVectorStore
     **non-None chunk.metadata}; ids already present are skipped with a warning,
     ids repeated inside one call raise ValueError (Chroma DuplicateIDError);
   * search (chroma :90-148): exact top-k on the GPU; cosine/"dot" similarity =
-    inner product (faiss :179-180; chroma's 1 - distance :135 for those spaces);
+    inner product (faiss :179-180; chroma's 1 - distance :135 for those spaces),
+    "euclidean" similarity = 1 - squared L2 distance (chroma's "l2" space, :48-53);
     ``filters`` are compiled to a row bitmap (plain dict or Chroma where-clause)
     and applied inside the scan, i.e. exact top-k among matching rows;
   * delete / delete_by_document_id / delete_by_metadata (chroma :150-222):
@@ -48,8 +49,6 @@ class HipVectorStore(BaseVectorStore):
         self.include_embeddings = bool(params.get("include_embeddings", False))
         self.persist = bool(params.get("persist", True))
         self.metric = _METRIC[config.distance_metric]
-        if self.metric == "l2":
-            raise NotImplementedError("distance_metric='euclidean' is not implemented by the HIP index yet")
         if self.dtype not in _native.DTYPES:
             raise ValueError(f"unknown index dtype {self.dtype!r}")
         self._factory = index_factory or (lambda dim: _native.NativeIndex(dim, self.dtype, self.metric, self.device))

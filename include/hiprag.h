@@ -74,6 +74,14 @@ int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global_row0, int6
  * vectors; returns once the rows are stored (rows_dev may then be reused).
  * Replaces embed_texts -> add_chunks in BaseProcessor._chunk_and_store (processors.py:413-418). */
 int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n, int64_t* first_row_out, void* stream);
+/* Store n fp32 device rows at explicit positions dest_dev[i] (< n_rows_after, previously unused),
+ * e.g. rows placed by list for an IVF index; the index then holds n_rows_after rows, positions
+ * never written stay dead.  Ordered after the work queued on `stream`; returns once stored. */
+int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_t n, const int64_t* dest_dev,
+                           int64_t n_rows_after, void* stream);
+/* The synthetic corpus generator (the one hr_index_add_synthetic and the oracle use) writing n fp32
+ * rows of dimension dim, row-major, to device memory on `stream`. */
+int hr_gen_rows_device(uint64_t seed, int64_t row0, int64_t n, int dim, float* out_dev, void* stream);
 int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n);
 int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
                     int64_t* rows_out);
@@ -115,6 +123,20 @@ int hr_merge_candidates(int device, const void* cand_dev /* G*B*kc records */, c
 int hr_merge_candidates_strided(int device, const void* cand_dev, const double* bounds_dev, int64_t cand_rank_stride,
                                 int64_t bound_rank_stride, int G, int B, int kc, int k, float* scores_out_dev,
                                 int64_t* rows_out_dev, double* kth_out_dev, int32_t* fail_out_dev, void* stream);
+
+/* IVF-flat lists search (BASELINE config 5 candidate generation): h holds
+ * the rows in list order (list l = tiles [list_tiles_dev[l], list_tiles_dev[l+1]) of 32 rows, pad
+ * rows dead), ids_dev the original id of every position (-1 for pads), centroids_dev the nlist
+ * processed fp32 centroids (row stride = dim rounded up to 64, zero padded).  Per query: exact top-
+ * nprobe lists by canonical fp64 score (ties: lower list first), then the exact top-k of the rows of
+ * those lists by canonical score (ties: lower id first), as B*k candidate records (global ids,
+ * (-inf, -1) padding) and bound = -inf (nothing unreturned can matter: the same merge as the exact
+ * search combines shards).  max_list_tiles: tiles of the largest list (sizes the unit buffer).
+ * probes_out_dev (nullable): the B*nprobe probed lists as records {score, list}.  Cosine / dot. */
+int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist, const int64_t* list_tiles_dev,
+                  int64_t max_list_tiles, const int64_t* ids_dev, const float* q_dev, int B, int nprobe, int k,
+                  const uint64_t* row_mask_dev, void* cand_out_dev, double* bound_out_dev, void* probes_out_dev,
+                  void* stream);
 
 /* K7: masked mean-pool of the first-dim hidden states with the first n_instr
  * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */

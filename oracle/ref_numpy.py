@@ -154,3 +154,33 @@ def search(stored: np.ndarray, dtype: str, q: np.ndarray, k: int, allowed: np.nd
         out_s[b, :len(order)] = sb[order]
         out_r[b, :len(order)] = sel[order] + row_offset
     return out_s, out_r
+
+
+def ivf_search(stored: np.ndarray, dtype: str, q: np.ndarray, centroids: np.ndarray, row_list: np.ndarray,
+               nprobe: int, k: int, ids: np.ndarray | None = None):
+    """IVF-flat restatement (FAISS IndexIVFFlat's published algorithm, faiss-cpu 1.12.0 per uv.lock:
+    coarse quantizer -> the nprobe best lists -> scan those lists -> keep the k best), with the
+    canonical arithmetic: coarse score = canonical fp64 q.c over the fp32 centroids, lists ordered
+    (score desc, list asc); rows of the probed lists scored canonically, ordered (score desc, id asc).
+    q: processed queries (B, dim); stored: processed rows (N, dim) in id order; row_list: list of
+    every row.  Returns (scores f64 (B, k), ids i64 (B, k), probes i64 (B, nprobe))."""
+    qd = np.asarray(q, np.float32).astype(np.float64)
+    c = np.asarray(centroids, np.float32).astype(np.float64)
+    coarse = canon_sum(qd[:, None, :] * c[None, :, :])
+    x = dequantize(stored, dtype).astype(np.float64)
+    ids = np.arange(len(stored), dtype=np.int64) if ids is None else np.asarray(ids, np.int64)
+    B = qd.shape[0]
+    out_s = np.full((B, k), -np.inf)
+    out_r = np.full((B, k), -1, np.int64)
+    probes = np.zeros((B, nprobe), np.int64)
+    lists = np.arange(c.shape[0])
+    for b in range(B):
+        probes[b] = lists[np.lexsort((lists, -coarse[b]))][:nprobe]
+        vis = np.nonzero(np.isin(row_list, probes[b]))[0]
+        if len(vis) == 0:
+            continue
+        s = canon_sum(qd[b][None, :] * x[vis])
+        order = np.lexsort((ids[vis], -s))[:k]
+        out_s[b, :len(order)] = s[order]
+        out_r[b, :len(order)] = ids[vis][order]
+    return out_s, out_r, probes

@@ -1,143 +1,14 @@
 // hr_index.hip -- host side of libhiprag.so: index handles, launch plumbing, C ABI.
 // Declarations and the reference call each entry replaces: include/hiprag.h.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <deque>
-#include <mutex>
-#include <string>
-#include <vector>
-
-#include "../../include/hiprag.h"
+#include "hr_internal.hpp"
 #include "hr_kernels.hpp"
-
-using namespace hr;
 
 // ---------------------------------------------------------------- errors
 static thread_local std::string g_err;
-static int set_err(int code, const std::string& msg) {
+int set_err(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
-#define HIP_TRY(expr)                                                                              \
-    do {                                                                                           \
-        hipError_t e_ = (expr);                                                                    \
-        if (e_ != hipSuccess)                                                                      \
-            return set_err(HR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
-    } while (0)
-
-// ---------------------------------------------------------------- device buffers
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    hipError_t ensure(size_t need) {
-        if (need <= bytes) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&p, need);
-        if (e == hipSuccess) bytes = need;
-        return e;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    template <class T>
-    T* as() const {
-        return (T*)p;
-    }
-};
-
-namespace hr {  // hr_exhaustive.hip
-size_t exhaustive_scratch_bytes(int64_t n);
-int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
-                    const uint32_t* live,
-                    const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
-                    size_t scratch_bytes, hipStream_t st);
-}  // namespace hr
-
-static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
-static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
-static constexpr int kScanThreads = 512;
-
-// Per-batch search workspace.  Two sets ping-pong between consecutive pipelined batches
-// (hr_index_search_shard_async: batch i's select/rescore on the tail stream overlaps batch
-// i+1's scan on the scan stream); a third serves the synchronous and collect paths.
-struct Scratch {
-    DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q;
-    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
-    hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
-    hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
-    bool armed = false;               // `released` has been recorded at least once
-    void release_all() {
-        for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
-                          &overflow, &pbuf, &pcnt, &dyn_q})
-            b->release();
-        if (scanned) (void)hipEventDestroy(scanned);
-        if (released) (void)hipEventDestroy(released);
-        scanned = released = nullptr;
-    }
-};
-static constexpr int kSyncSet = 2;
-
-struct hr_index {
-    int dim = 0, dpad = 0, S = 0, dtype = BF16, metric = COSINE, device = 0;
-    int64_t n = 0, cap = 0, n_live = 0;
-    double max_norm2 = 0.0;
-    uint8_t* rows = nullptr;        // tiled corpus
-    uint32_t* live = nullptr;       // one word per tile
-    float* xnorm = nullptr;         // euclidean only: fp32 |x|^2 per stored row (approximate scan score)
-    std::vector<uint32_t> live_host;
-    unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
-    hipStream_t stream = nullptr;
-    // per-launch timing of the main (SAMPLE, FILTER) scan pair: events are recorded on the
-    // search stream and harvested later, so batches can be pipelined (see hr_index_take_scan_times)
-    struct ScanEvents {
-        hipEvent_t e[4];
-        bool sampled;
-    };
-    std::vector<ScanEvents> ev_free;
-    std::deque<ScanEvents> ev_pending;
-    float last_sample_ms = 0.f, last_filter_ms = 0.f;
-    int time_every = 0;               // record events around every Nth main pass (0 = never)
-    int64_t main_passes = 0;
-    int n_cu = 256;
-    std::mutex mu;
-    // search workspace
-    DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, stage, exh;
-    Scratch scr[3];
-    int flip = 0;                     // next ping-pong set of the pipelined path
-    const Scratch* last_scr = nullptr;  // set of the most recent FILTER launch (diagnostics)
-    int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
-    std::vector<float> floor_host;
-};
-
-static size_t tile_bytes(const hr_index* h) { return (size_t)h->S * (h->dtype == F32 ? 2048 : 1024); }
-
-static int set_device(hr_index* h) {
-    HIP_TRY(hipSetDevice(h->device));
-    return HR_OK;
-}
-
-// ---------------------------------------------------------------- dispatch helpers
-template <class F>
-static int dispatch_dt(int dt, F&& f) {
-    switch (dt) {
-        case F32: return f(std::integral_constant<int, F32>{});
-        case BF16: return f(std::integral_constant<int, BF16>{});
-        case F16: return f(std::integral_constant<int, F16>{});
-    }
-    return set_err(HR_E_INVALID, "unknown dtype");
-}
-
-// MFMA operand type: f16 corpora use the f16 MFMA, bf16 and fp32 corpora the bf16 one
-static int mfma_type(int dtype) { return dtype == F16 ? F16 : BF16; }
 
 // ---------------------------------------------------------------- create / grow
 extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
@@ -307,6 +178,54 @@ extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global
         return HR_OK;
     }
     return add_impl<ADD_SYNTH>(h, nullptr, seed, global_row0, n, first_row_out);
+}
+
+extern "C" int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_t n, const int64_t* dest_dev,
+                                      int64_t n_rows_after, void* stream) {
+    if (!h || n < 0 || (n > 0 && (!rows_dev || !dest_dev))) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (n_rows_after < h->n || n_rows_after > ((int64_t)1 << 32) - 64)
+        return set_err(HR_E_INVALID, "n_rows_after must be >= the current size and < 2^32");
+    if (int rc = set_device(h)) return rc;
+    if (int rc = grow(h, n_rows_after)) return rc;
+    hipEvent_t ev;  // order after the producer of rows_dev / dest_dev on the caller's stream
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream, ev, 0));
+    HIP_TRY(hipEventDestroy(ev));
+    if (n > 0) {
+        int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+            hipLaunchKernelGGL((k_store<decltype(dt)::value, false>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                               h->stream, rows_dev, 0, 0, n, h->dim, h->S, h->metric, 0, h->rows, h->norm_bits, dest_dev);
+            HIP_TRY(hipGetLastError());
+            if (h->metric == L2)
+                hipLaunchKernelGGL((k_row_norms<decltype(dt)::value>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                                   h->stream, h->rows, h->S, h->dpad, 0, n, h->xnorm, dest_dev);
+            HIP_TRY(hipGetLastError());
+            return HR_OK;
+        });
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_mark_live, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, dest_dev, n, h->live);
+        HIP_TRY(hipGetLastError());
+    }
+    h->n = n_rows_after;
+    const int64_t words = (h->n + 31) / 32;
+    HIP_TRY(hipMemcpyAsync(h->live_host.data(), h->live, (size_t)words * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    int64_t live = 0;
+    for (int64_t w = 0; w < words; ++w) live += __builtin_popcount(h->live_host[(size_t)w]);
+    h->n_live = live;
+    return finish_add(h);
+}
+
+extern "C" int hr_gen_rows_device(uint64_t seed, int64_t row0, int64_t n, int dim, float* out_dev, void* stream) {
+    if (n < 0 || dim <= 0 || (n > 0 && !out_dev)) return set_err(HR_E_INVALID, "bad arguments");
+    if (n == 0) return HR_OK;
+    const int64_t total = n * dim;
+    hipLaunchKernelGGL(k_gen_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, seed, row0,
+                       n, dim, out_dev);
+    HIP_TRY(hipGetLastError());
+    return HR_OK;
 }
 
 extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n, int64_t* first_row_out,
@@ -1073,7 +992,8 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->xnorm) (void)hipFree(h->xnorm);
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
-    for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->stage, &h->exh})
+    for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->stage, &h->exh,
+                      &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();
     for (auto* list : {&h->ev_free})

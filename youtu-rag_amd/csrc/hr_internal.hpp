@@ -1,0 +1,139 @@
+// hr_internal.hpp -- host-side internals shared by the libhiprag.so translation units
+// (hr_index.hip: index handles and the exact search; hr_ivf.hip: the IVF lists search).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hiprag.h"
+#include "hr_common.hpp"
+
+using namespace hr;
+
+// ---------------------------------------------------------------- errors
+int set_err(int code, const std::string& msg);  // thread-local message for hr_last_error (hr_index.hip)
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_err(HR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// ---------------------------------------------------------------- device buffers
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+namespace hr {  // hr_exhaustive.hip
+size_t exhaustive_scratch_bytes(int64_t n);
+int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
+                    const uint32_t* live,
+                    const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
+                    size_t scratch_bytes, hipStream_t st);
+}  // namespace hr
+
+static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
+static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
+static constexpr int kScanThreads = 512;
+
+// Per-batch search workspace.  Two sets ping-pong between consecutive pipelined batches
+// (hr_index_search_shard_async: batch i's select/rescore on the tail stream overlaps batch
+// i+1's scan on the scan stream); a third serves the synchronous and collect paths.
+struct Scratch {
+    DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q;
+    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
+    hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
+    hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
+    bool armed = false;               // `released` has been recorded at least once
+    void release_all() {
+        for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
+                          &overflow, &pbuf, &pcnt, &dyn_q})
+            b->release();
+        if (scanned) (void)hipEventDestroy(scanned);
+        if (released) (void)hipEventDestroy(released);
+        scanned = released = nullptr;
+    }
+};
+static constexpr int kSyncSet = 2;
+
+struct hr_index {
+    int dim = 0, dpad = 0, S = 0, dtype = BF16, metric = COSINE, device = 0;
+    int64_t n = 0, cap = 0, n_live = 0;
+    double max_norm2 = 0.0;
+    uint8_t* rows = nullptr;        // tiled corpus
+    uint32_t* live = nullptr;       // one word per tile
+    float* xnorm = nullptr;         // euclidean only: fp32 |x|^2 per stored row (approximate scan score)
+    std::vector<uint32_t> live_host;
+    unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
+    hipStream_t stream = nullptr;
+    // per-launch timing of the main (SAMPLE, FILTER) scan pair: events are recorded on the
+    // search stream and harvested later, so batches can be pipelined (see hr_index_take_scan_times)
+    struct ScanEvents {
+        hipEvent_t e[4];
+        bool sampled;
+    };
+    std::vector<ScanEvents> ev_free;
+    std::deque<ScanEvents> ev_pending;
+    float last_sample_ms = 0.f, last_filter_ms = 0.f;
+    int time_every = 0;               // record events around every Nth main pass (0 = never)
+    int64_t main_passes = 0;
+    int n_cu = 256;
+    std::mutex mu;
+    // search workspace
+    DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, stage, exh;
+    DevBuf ivf_coarse, ivf_probe, ivf_units, ivf_uoff, ivf_out;  // IVF lists search (hr_ivf.hip)
+    Scratch scr[3];
+    int flip = 0;                     // next ping-pong set of the pipelined path
+    const Scratch* last_scr = nullptr;  // set of the most recent FILTER launch (diagnostics)
+    int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
+    std::vector<float> floor_host;
+};
+
+inline size_t tile_bytes(const hr_index* h) { return (size_t)h->S * (h->dtype == F32 ? 2048 : 1024); }
+
+inline int set_device(hr_index* h) {
+    HIP_TRY(hipSetDevice(h->device));
+    return HR_OK;
+}
+
+// ---------------------------------------------------------------- dispatch helpers
+template <class F>
+inline int dispatch_dt(int dt, F&& f) {
+    switch (dt) {
+        case F32: return f(std::integral_constant<int, F32>{});
+        case BF16: return f(std::integral_constant<int, BF16>{});
+        case F16: return f(std::integral_constant<int, F16>{});
+    }
+    return set_err(HR_E_INVALID, "unknown dtype");
+}
+
+// MFMA operand type: f16 corpora use the f16 MFMA, bf16 and fp32 corpora the bf16 one
+inline int mfma_type(int dtype) { return dtype == F16 ? F16 : BF16; }
+

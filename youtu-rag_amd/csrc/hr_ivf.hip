@@ -1,0 +1,390 @@
+// hr_ivf.hip -- IVF-flat lists search: BASELINE config 5's candidate generation (SURVEY.md
+// §8(f) rank 4).  The index is an ordinary hr_index whose rows sit in list order (each list
+// starts on a 32-row tile; pad rows are dead), plus fp32 centroids, the tile offset of every
+// list and the original id of every stored position.
+//
+// Search of one batch (<= 64 queries per chunk), all on the caller's stream:
+//   k_prep_q     processed fp32 queries (the exact operand), |q|^2
+//   k_coarse     exact canonical fp64 score of every (query, centroid) pair
+//   k_topk_cand  top-nprobe lists per query, (score desc, list asc)
+//   k_ivf_units  per-query unit list: (query, tile) for every tile of its probed lists
+//   k_ivf_scan   exact canonical fp64 score of every row of every unit, one wave per unit:
+//                the tile's 64 KiB stream is read coalesced exactly as the brute-force scan
+//                reads it, and the 64 canonical partial sums of each row live in the lane
+//                pair that holds the row (acc[s % 4][j] on lane r + 32h = partial 16(s%4)+8h+j)
+//   k_topk_cand  exact top-k per query, (score desc, id asc)
+// The candidates are exact over the visible rows (the rows of the probed lists), so every
+// shard returns bound = -inf and the usual merge needs no fallback.  Exact scoring costs no
+// more than an approximate pass here: each probed tile is read once per query either way
+// (lists are rarely probed by two queries of one batch), and 8 fp64 FMAs per 16 bytes keep
+// far below the fp64 VALU rate, so the scan stays HBM-bound.
+#include "hr_internal.hpp"
+#include "hr_kernels.hpp"
+
+namespace {
+
+// ---------------------------------------------------------------- K9: coarse scores
+// One wave per centroid, every query: the centroid row is read once, the queries come from L2.
+// Score = canonical fp64 dot of the processed query and the fp32 centroid (oracle order).
+__global__ __launch_bounds__(256) void k_coarse(const float* __restrict__ cent, int nlist, int dpad,
+                                                const float* __restrict__ q32, int B, Cand* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (l >= nlist) return;
+    const float* c = cent + (int64_t)l * dpad;
+    for (int b = 0; b < B; ++b) {
+        const float* qv = q32 + (int64_t)b * dpad;
+        double p = 0.0;
+#pragma unroll 8
+        for (int d = lane; d < dpad; d += 64) p = p + (double)c[d] * (double)qv[d];
+        p = wave_butterfly_sum(p);
+        if (lane == 0) out[(int64_t)b * nlist + l] = Cand{p, l};
+    }
+}
+
+// ---------------------------------------------------------------- K10: exact top-m per segment
+// One 1024-thread block per query.  Order (score desc, id asc); records with id < 0 are absent.
+// Radix select of the m-th largest score key (8 passes of 8 bits over the segment, histogram in
+// LDS), then, if the m-th place is tied, radix select of the smallest tied ids; the m winners are
+// bitonic-sorted in LDS.  Out: m records per query, padded with (-inf, -1).
+constexpr int kTopkMax = 1024;
+__device__ inline uint64_t cand_key(const Cand& e) { return e.row < 0 ? 0ull : d2key(e.score); }
+__device__ inline uint64_t id_key(int64_t id) { return (uint64_t)id ^ 0x8000000000000000ull; }
+
+__global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in, const int64_t* __restrict__ seg_off,
+                                                    int64_t seg_stride, int B, int m, Cand* __restrict__ out) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t sh_prefix;
+    __shared__ int64_t sh_need;
+    __shared__ int sh_cnt;
+    __shared__ uint64_t skey[kTopkMax];
+    __shared__ int64_t sid[kTopkMax];
+    __shared__ double ssc[kTopkMax];
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int tid = threadIdx.x;
+    const int64_t lo = seg_off ? seg_off[b] * 32 : (int64_t)b * seg_stride;
+    const int64_t hi = seg_off ? seg_off[b + 1] * 32 : lo + seg_stride;
+    const Cand* seg = in + lo;
+    const int64_t n = hi - lo;
+
+    // m-th largest key among valid records (radix select, MSB first)
+    auto select_key = [&](bool by_id, uint64_t key_eq, int64_t need0) -> uint64_t {
+        uint64_t prefix = 0, mask = 0;
+        if (tid == 0) sh_need = need0;
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+            __syncthreads();
+            for (int64_t i = tid; i < n; i += blockDim.x) {
+                const Cand e = seg[i];
+                const uint64_t k = cand_key(e);
+                if (k == 0) continue;
+                if (by_id && k != key_eq) continue;
+                const uint64_t v = by_id ? ~id_key(e.row) : k;  // ids: smallest first = largest complement
+                if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int64_t need = sh_need, above = 0;
+                int d = 255;
+                for (; d > 0; --d) {
+                    if (above + hist[d] >= need) break;
+                    above += hist[d];
+                }
+                sh_need = need - above;
+                sh_prefix = prefix | ((uint64_t)d << shift);
+            }
+            __syncthreads();
+            prefix = sh_prefix;
+            mask |= (uint64_t)255 << shift;
+        }
+        return prefix;
+    };
+
+    // valid records
+    if (tid == 0) sh_cnt = 0;
+    __syncthreads();
+    int my = 0;
+    for (int64_t i = tid; i < n; i += blockDim.x) my += cand_key(seg[i]) != 0;
+    if (my) atomicAdd(&sh_cnt, my);
+    __syncthreads();
+    const int64_t n_valid = sh_cnt;
+    __syncthreads();
+
+    uint64_t kth = 0, id_thr = ~0ull;  // take key > kth, or key == kth with ~id_key >= id_thr
+    if (n_valid > m) {
+        kth = select_key(false, 0, m);
+        const int64_t need_ties = sh_need;  // winners among records with key == kth
+        // are all ties needed?  count them
+        __syncthreads();
+        if (tid == 0) sh_cnt = 0;
+        __syncthreads();
+        int t = 0;
+        for (int64_t i = tid; i < n; i += blockDim.x) t += cand_key(seg[i]) == kth;
+        if (t) atomicAdd(&sh_cnt, t);
+        __syncthreads();
+        const int64_t n_ties = sh_cnt;
+        __syncthreads();
+        if (n_ties > need_ties) id_thr = select_key(true, kth, need_ties);
+        else id_thr = 0;
+    }
+    // gather the winners (exactly min(m, n_valid))
+    if (tid == 0) sh_cnt = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += blockDim.x) {
+        const Cand e = seg[i];
+        const uint64_t k = cand_key(e);
+        if (k == 0) continue;
+        bool win = n_valid <= m || k > kth || (k == kth && ~id_key(e.row) >= id_thr);
+        if (!win) continue;
+        const int p = atomicAdd(&sh_cnt, 1);
+        if (p < kTopkMax) {
+            skey[p] = k;
+            sid[p] = e.row;
+            ssc[p] = e.score;
+        }
+    }
+    __syncthreads();
+    const int cnt = sh_cnt < kTopkMax ? sh_cnt : kTopkMax;
+    int p2 = 1;
+    while (p2 < cnt) p2 <<= 1;
+    for (int i = cnt + tid; i < p2; i += blockDim.x) {
+        skey[i] = 0;
+        sid[i] = INT64_MAX;
+        ssc[i] = -__builtin_inf();
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= p2; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < p2; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const bool a_first = skey[i] > skey[ixj] || (skey[i] == skey[ixj] && sid[i] < sid[ixj]);
+                    const bool desc = (i & kk) == 0;
+                    if (desc ? !a_first : a_first) {
+                        uint64_t tk = skey[i];
+                        skey[i] = skey[ixj];
+                        skey[ixj] = tk;
+                        int64_t ti = sid[i];
+                        sid[i] = sid[ixj];
+                        sid[ixj] = ti;
+                        double ts = ssc[i];
+                        ssc[i] = ssc[ixj];
+                        ssc[ixj] = ts;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < m; i += blockDim.x)
+        out[(int64_t)b * m + i] = i < cnt ? Cand{ssc[i], sid[i]} : Cand{-__builtin_inf(), -1};
+}
+
+// ---------------------------------------------------------------- K11: unit lists
+// One block: unit = (query << 26) | tile for every tile of every probed list, query-major;
+// uoff[b] = first unit of query b, uoff[B] = total.  Units beyond cap are dropped (the host
+// sizes cap from the largest list, so this never happens).
+__global__ __launch_bounds__(1024) void k_ivf_units(const Cand* __restrict__ probes, int B, int nprobe,
+                                                    const int64_t* __restrict__ list_tiles,
+                                                    uint32_t* __restrict__ units, int64_t* __restrict__ uoff,
+                                                    int64_t cap) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int np = B * nprobe;
+    const int per = (np + blockDim.x - 1) / blockDim.x;  // pairs per thread, contiguous
+    int64_t mine = 0;
+    for (int j = 0; j < per; ++j) {
+        const int p = tid * per + j;
+        if (p >= np) break;
+        const int64_t l = probes[p].row;
+        mine += l >= 0 ? list_tiles[l + 1] - list_tiles[l] : 0;
+    }
+    part[tid] = mine;
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan over 1024 partials
+        int64_t acc = 0;
+        for (int i = 0; i < (int)blockDim.x; ++i) {
+            const int64_t v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    int64_t pos = part[tid];
+    for (int j = 0; j < per; ++j) {
+        const int p = tid * per + j;
+        if (p >= np) break;
+        const int b = p / nprobe;
+        if (p % nprobe == 0) uoff[b] = pos < cap ? pos : cap;
+        const int64_t l = probes[p].row;
+        if (l < 0) continue;
+        const int64_t t0 = list_tiles[l], t1 = list_tiles[l + 1];
+        for (int64_t t = t0; t < t1; ++t, ++pos)
+            if (pos < cap) units[pos] = ((uint32_t)b << 26) | (uint32_t)t;
+    }
+    if (tid == (int)blockDim.x - 1) uoff[B] = pos < cap ? pos : cap;
+}
+
+// ---------------------------------------------------------------- K12: exact scan of the units
+// One wave per unit at a time (static contiguous split of the unit list).  Lane l = r + 32h of a
+// k-step chunk holds elements 16s + 8h + j of row r, i.e. canonical partials c = 16(s%4) + 8h + j;
+// the oracle's butterfly (off 32, 16: local; 8: lanes r <-> r+32; 4, 2, 1: local) then gives the
+// canonical score of row r on lane r.
+template <int DT>
+__device__ inline void load_chunk(const uint8_t* rows, int64_t c, int lane, float (&x)[8]) {
+    if constexpr (DT == F32) {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const f32x4 a = __builtin_nontemporal_load((const f32x4*)(rows + c * 2048 + lane * 16));
+        const f32x4 b = __builtin_nontemporal_load((const f32x4*)(rows + c * 2048 + 1024 + lane * 16));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            x[j] = a[j];
+            x[4 + j] = b[j];
+        }
+    } else {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(rows + c * 1024 + lane * 16));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint16_t lo = (uint16_t)(v[j] & 0xFFFFu), hi = (uint16_t)(v[j] >> 16);
+            x[2 * j] = DT == BF16 ? bf16_to_f32(lo) : f16_to_f32(lo);
+            x[2 * j + 1] = DT == BF16 ? bf16_to_f32(hi) : f16_to_f32(hi);
+        }
+    }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ rows, int S,
+                                                  const uint32_t* __restrict__ live, const uint32_t* __restrict__ mask,
+                                                  const int64_t* __restrict__ ids, const float* __restrict__ q32,
+                                                  int dpad, const uint32_t* __restrict__ units,
+                                                  const int64_t* __restrict__ uoff, int B, Cand* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t n_units = uoff[B];
+    const int64_t base = n_units / W, rem = n_units % W;
+    const int64_t u0 = w * base + (w < rem ? w : rem);
+    const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
+    for (int64_t u = u0; u < u1; ++u) {
+        const uint32_t pk = units[u];
+        const int64_t t = pk & 0x3FFFFFFu;
+        const int b = (int)(pk >> 26);
+        const float* qv = q32 + (int64_t)b * dpad + 8 * h;
+        double acc[4][8];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[a][j] = 0.0;
+        for (int s4 = 0; s4 < S; s4 += 4) {
+            float x[4][8];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) load_chunk<DT>(rows, t * S + s4 + a, lane, x[a]);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const float4 q0 = *(const float4*)(qv + 16 * (s4 + a));
+                const float4 q1 = *(const float4*)(qv + 16 * (s4 + a) + 4);
+                const float qq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[a][j] = __builtin_fma((double)x[a][j], (double)qq[j], acc[a][j]);
+            }
+        }
+        // canonical butterfly over partial index c = 16a + 8h + j
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[0][j] = acc[0][j] + acc[2][j];  // off 32
+            acc[1][j] = acc[1][j] + acc[3][j];
+            acc[0][j] = acc[0][j] + acc[1][j];  // off 16
+            const double o = __shfl_xor(acc[0][j], 32, 64);  // off 8: lane r (h=0) takes r+32's
+            acc[0][j] = acc[0][j] + o;
+        }
+        double p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = acc[0][j];
+        p[0] = p[0] + p[4]; p[1] = p[1] + p[5]; p[2] = p[2] + p[6]; p[3] = p[3] + p[7];  // off 4
+        p[0] = p[0] + p[2]; p[1] = p[1] + p[3];                                          // off 2
+        p[0] = p[0] + p[1];                                                              // off 1
+        if (h == 0) {
+            uint32_t allow = live[t];
+            if (mask) allow &= mask[t];
+            const int64_t pos = t * 32 + r;
+            const bool ok = (allow >> r) & 1u;
+            out[u * 32 + r] = ok ? Cand{p[0], ids[pos]} : Cand{-__builtin_inf(), -1};
+        }
+    }
+}
+
+__global__ void k_fill_f64(double* __restrict__ p, int n, double v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist, const int64_t* list_tiles_dev,
+                             int64_t max_list_tiles, const int64_t* ids_dev, const float* q_dev, int B, int nprobe,
+                             int k, const uint64_t* row_mask_dev, void* cand_out_dev, double* bound_out_dev,
+                             void* probes_out_dev, void* stream) {
+    if (!h || !centroids_dev || !list_tiles_dev || !ids_dev || !q_dev || !cand_out_dev || !bound_out_dev)
+        return set_err(HR_E_INVALID, "null argument");
+    if (B <= 0 || nlist <= 0 || nprobe <= 0 || nprobe > nlist || nprobe > kTopkMax || k <= 0 || k > kTopkMax ||
+        max_list_tiles < 0)
+        return set_err(HR_E_INVALID, "bad sizes (need 1 <= nprobe <= min(nlist, 1024), 1 <= k <= 1024)");
+    if (h->metric == L2) return set_err(HR_E_UNSUPPORTED, "IVF lists support cosine and dot (inner product)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    Scratch& sc = h->scr[kSyncSet];
+    const int dpad = h->dpad;
+    for (int b0 = 0; b0 < B; b0 += 64) {
+        const int bc = std::min(64, B - b0);
+        const int Bp = bc > 32 ? 64 : 32, QB = Bp / 32;
+        const int64_t cap = (int64_t)bc * nprobe * std::max<int64_t>(1, max_list_tiles);
+        if (cap >= ((int64_t)1 << 31)) return set_err(HR_E_INVALID, "probed lists too large for one batch");
+        HIP_TRY(sc.q32.ensure((size_t)Bp * dpad * 4));
+        HIP_TRY(sc.qfrag.ensure((size_t)h->S * QB * 1024));
+        HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
+        HIP_TRY(h->ivf_coarse.ensure((size_t)bc * nlist * sizeof(Cand)));
+        HIP_TRY(h->ivf_probe.ensure((size_t)bc * nprobe * sizeof(Cand)));
+        HIP_TRY(h->ivf_units.ensure((size_t)cap * 4));
+        HIP_TRY(h->ivf_uoff.ensure((size_t)(bc + 1) * 8));
+        HIP_TRY(h->ivf_out.ensure((size_t)cap * 32 * sizeof(Cand)));
+        const float* qb = q_dev + (int64_t)b0 * h->dim;
+        if (mfma_type(h->dtype) == BF16)
+            hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, qb, bc, Bp, h->dim, dpad, h->S,
+                               QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                               nullptr, 1, nullptr, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, qb, bc, Bp, h->dim, dpad, h->S,
+                               QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
+                               nullptr, 1, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_coarse, dim3((nlist + 3) / 4), dim3(256), 0, st, centroids_dev, nlist, dpad,
+                           sc.q32.as<float>(), bc, h->ivf_coarse.as<Cand>());
+        hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_coarse.as<Cand>(), (const int64_t*)nullptr,
+                           (int64_t)nlist, bc, nprobe, h->ivf_probe.as<Cand>());
+        hipLaunchKernelGGL(k_ivf_units, dim3(1), dim3(1024), 0, st, h->ivf_probe.as<Cand>(), bc, nprobe,
+                           list_tiles_dev, h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), cap);
+        HIP_TRY(hipGetLastError());
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * 8, (cap + 3) / 4));
+        int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
+            hipLaunchKernelGGL((k_ivf_scan<decltype(dt)::value>), dim3((unsigned)blocks), dim3(256), 0, st, h->rows,
+                               h->S, h->live, (const uint32_t*)row_mask_dev, ids_dev, sc.q32.as<float>(), dpad,
+                               h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), bc, h->ivf_out.as<Cand>());
+            HIP_TRY(hipGetLastError());
+            return HR_OK;
+        });
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_out.as<Cand>(), h->ivf_uoff.as<int64_t>(),
+                           (int64_t)0, bc, k, (Cand*)cand_out_dev + (int64_t)b0 * k);
+        HIP_TRY(hipGetLastError());
+        if (probes_out_dev)
+            HIP_TRY(hipMemcpyAsync((Cand*)probes_out_dev + (int64_t)b0 * nprobe, h->ivf_probe.p,
+                                   (size_t)bc * nprobe * sizeof(Cand), hipMemcpyDeviceToDevice, st));
+    }
+    // exact over the visible rows: nothing unreturned can matter
+    hipLaunchKernelGGL(k_fill_f64, dim3((B + 255) / 256), dim3(256), 0, st, bound_out_dev, B, -INFINITY);
+    HIP_TRY(hipGetLastError());
+    return HR_OK;
+}

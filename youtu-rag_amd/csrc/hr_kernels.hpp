@@ -29,7 +29,8 @@ namespace hr {
 template <int DT, bool SYNTH>
 __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uint64_t seed, int64_t grow0, int64_t n,
                                                int dim, int S, int metric, int64_t lrow0, uint8_t* __restrict__ rows,
-                                               unsigned long long* max_norm2_bits) {
+                                               unsigned long long* max_norm2_bits,
+                                               const int64_t* __restrict__ dest = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n) return;
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uin
             scale = true;
         }
     }
-    const int64_t R = lrow0 + r;
+    const int64_t R = dest ? dest[r] : lrow0 + r;  // dest: explicit positions (IVF lists)
     const int nchunk = S * 2;  // 8-element chunks per row
     double sq = 0.0;
     for (int c = lane; c < nchunk; c += 64) {
@@ -97,10 +98,12 @@ __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uin
 // the exact rescoring recomputes the canonical fp64 value.
 template <int DT>
 __global__ __launch_bounds__(256) void k_row_norms(const uint8_t* __restrict__ rows, int S, int dpad, int64_t r0,
-                                                   int64_t n, float* __restrict__ xnorm) {
+                                                   int64_t n, float* __restrict__ xnorm,
+                                                   const int64_t* __restrict__ dest = nullptr) {
     const int lane = threadIdx.x & 63;
-    const int64_t r = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= r0 + n) return;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int64_t r = dest ? dest[i] : r0 + i;
     double p = 0.0;
 #pragma unroll 8
     for (int d = lane; d < dpad; d += 64) {
@@ -109,6 +112,18 @@ __global__ __launch_bounds__(256) void k_row_norms(const uint8_t* __restrict__ r
     }
     p = wave_butterfly_sum(p);
     if (lane == 0) xnorm[r] = (float)p;
+}
+
+// live bits of explicitly placed rows
+static __global__ __attribute__((unused)) void k_mark_live(const int64_t* __restrict__ dest, int64_t n, uint32_t* __restrict__ live) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicOr(&live[dest[i] >> 5], 1u << (dest[i] & 31));
+}
+
+// synthetic fp32 rows (the corpus generator of k_store / the oracle), row-major
+static __global__ __attribute__((unused)) void k_gen_rows(uint64_t seed, int64_t row0, int64_t n, int dim, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n * dim) out[i] = gen_elem(seed, row0 + i / dim, dim, (int)(i % dim));
 }
 
 // ---------------------------------------------------------------- K1: query prep
@@ -685,7 +700,7 @@ __device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of t
 
 constexpr int kRankMax = 1024;  // candidate sets up to this size are ranked by counting, larger ones sorted
 
-__global__ __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
+static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
                                                  int cap, const uint32_t* __restrict__ pcnt,
                                                  const float2* __restrict__ pbuf, int W, int capw, int Bp,
                                                  const uint32_t* __restrict__ mkeys, int np,
@@ -829,7 +844,7 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
 // One block per query over G*kc exact candidates.  Sort key: (d2key(score) desc, row asc).
 // Rank g's candidates start at cand + g*cstride bytes, its bounds at bounds + g*bstride bytes (one
 // packed all-gather record per rank: [B*kc Cand][B double]).
-__global__ __launch_bounds__(256) void k_merge(const uint8_t* __restrict__ cand, const uint8_t* __restrict__ bounds,
+static __global__ __attribute__((unused)) __launch_bounds__(256) void k_merge(const uint8_t* __restrict__ cand, const uint8_t* __restrict__ bounds,
                                                int64_t cstride, int64_t bstride, int G,
                                                int B, int kc, int k, float* __restrict__ scores_out,
                                                int64_t* __restrict__ rows_out, double* __restrict__ kth_out,

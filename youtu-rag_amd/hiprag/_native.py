@@ -38,7 +38,8 @@ EXPORTS = [
     "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
     "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
-    "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async",
+    "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
+    "hr_gen_rows_device", "hr_ivf_search",
 ]
 
 _lib = None
@@ -85,6 +86,9 @@ def load_library(path: str | None = None):
             "hr_index_load": [ctypes.c_char_p, i32, vp, pp],
             "hr_index_search_shard": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp],
             "hr_index_search_shard_async": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp, vp],
+            "hr_index_add_device_at": [vp, vp, i64, vp, i64, vp],
+            "hr_gen_rows_device": [u64, i64, i64, i32, vp, vp],
+            "hr_ivf_search": [vp, vp, i32, vp, i64, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_index_search_shard_collect": [vp, vp, i32, vp, i32, vp, i64, vp, vp, vp],
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_merge_candidates_strided": [i32, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp, vp],
@@ -179,6 +183,23 @@ class NativeIndex:
         _check(self.lib.hr_index_add_device(self._h, ctypes.c_void_p(int(rows_ptr)), int(n), ctypes.byref(first),
                                             ctypes.c_void_p(int(stream))))
         return first.value
+
+    def add_device_at(self, rows_ptr: int, n: int, dest_ptr: int, n_rows_after: int, stream: int = 0) -> None:
+        """Store n fp32 device rows at the int64 device positions dest (IVF list placement)."""
+        _check(self.lib.hr_index_add_device_at(self._h, ctypes.c_void_p(int(rows_ptr)), int(n),
+                                               ctypes.c_void_p(int(dest_ptr)), int(n_rows_after),
+                                               ctypes.c_void_p(int(stream))))
+
+    def ivf_search(self, centroids_ptr: int, nlist: int, list_tiles_ptr: int, max_list_tiles: int, ids_ptr: int,
+                   q_ptr: int, B: int, nprobe: int, k: int, cand_ptr: int, bound_ptr: int, probes_ptr: int = 0,
+                   mask_ptr: int = 0, stream: int = 0) -> None:
+        """IVF-flat search of the list-ordered rows of this index (hr_ivf_search)."""
+        _check(self.lib.hr_ivf_search(self._h, ctypes.c_void_p(centroids_ptr), int(nlist),
+                                      ctypes.c_void_p(list_tiles_ptr), int(max_list_tiles), ctypes.c_void_p(ids_ptr),
+                                      ctypes.c_void_p(q_ptr), int(B), int(nprobe), int(k),
+                                      ctypes.c_void_p(mask_ptr or None), ctypes.c_void_p(cand_ptr),
+                                      ctypes.c_void_p(bound_ptr), ctypes.c_void_p(probes_ptr or None),
+                                      ctypes.c_void_p(stream or None)))
 
     def add_synthetic(self, seed: int, global_row0: int, n: int) -> int:
         first = ctypes.c_int64(0)
@@ -286,6 +307,12 @@ class NativeIndex:
         dev = (ctypes.c_int * 1)(int(device))
         _check(L.hr_index_load(os.fsencode(path), 1, dev, ctypes.byref(h)))
         return cls(dim or 0, dtype or "bf16", metric or "cosine", device, _handle=h)
+
+
+def gen_rows_device(seed: int, row0: int, n: int, dim: int, out_ptr: int, stream: int = 0) -> None:
+    """Synthetic corpus rows [row0, row0 + n) as fp32 into device memory (the hr_index_add_synthetic generator)."""
+    _check(load_library().hr_gen_rows_device(int(seed), int(row0), int(n), int(dim), ctypes.c_void_p(out_ptr),
+                                             ctypes.c_void_p(stream or None)))
 
 
 def merge_candidates(device: int, cand_ptr: int, bounds_ptr: int, G: int, B: int, kc: int, k: int, scores_ptr: int,

@@ -138,6 +138,14 @@ int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist, const int6
                   const uint64_t* row_mask_dev, void* cand_out_dev, double* bound_out_dev, void* probes_out_dev,
                   void* stream);
 
+/* Exact top-m of B segments of {double score; int64 id} records, order (score desc, id asc), records
+ * with id < 0 absent; segment b = [seg_off_records_dev[b], seg_off_records_dev[b+1]) if given, else
+ * [b*seg_stride, (b+1)*seg_stride).  Out: B*m records, (-inf, -1) padding; m <= 1024.  The
+ * reranker's per-query selection (replaces the reranking service's sort + top_n, openai_reranker.py
+ * :92-110 / the /rerank response order). */
+int hr_topk_records(const void* in_dev, const int64_t* seg_off_records_dev, int64_t seg_stride, int B, int m,
+                    void* out_dev, void* stream);
+
 /* K7: masked mean-pool of the first-dim hidden states with the first n_instr
  * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */
 int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,

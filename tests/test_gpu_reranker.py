@@ -1,0 +1,93 @@
+"""GPU: hr_topk_records against numpy, and the in-process cross-encoder reranker on the MI355X
+(scores within 1e-5 of a torch fp32 pair-by-pair reference; per-query order = the kernel's (score
+desc, position asc) selection; batched == per-query; retriever integration)."""
+import asyncio
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_topk(scores, ids, m):
+    valid = ids >= 0
+    s, r = scores[valid], ids[valid]
+    order = np.lexsort((r, -s))[:m]
+    out_s = np.full(m, -np.inf)
+    out_r = np.full(m, -1, np.int64)
+    out_s[:len(order)] = s[order]
+    out_r[:len(order)] = r[order]
+    return out_s, out_r
+
+
+@pytest.mark.parametrize("m", [1, 10, 100, 1000])
+def test_topk_records_vs_numpy(m):
+    import torch
+
+    from hiprag import _native
+
+    rng = np.random.default_rng(m)
+    lens = [0, 1, 5, 999, 1000, 1001, 4096, 70000]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    n = int(offs[-1])
+    scores = np.round(rng.standard_normal(n), 2)  # many exact ties
+    ids = rng.permutation(n).astype(np.int64)
+    ids[rng.random(n) < 0.05] = -1  # absent records
+    rec = np.empty((n, 2), np.float64)
+    rec[:, 0] = scores
+    rec.view(np.int64)[:, 1] = ids
+    rd = torch.from_numpy(rec).cuda()
+    out = torch.empty((len(lens), m, 2), dtype=torch.float64, device="cuda")
+    seg = torch.from_numpy(offs).cuda()
+    _native.topk_records(rd.data_ptr(), len(lens), m, out.data_ptr(), seg_off_ptr=seg.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for b in range(len(lens)):
+        s_ref, r_ref = _ref_topk(scores[offs[b]:offs[b + 1]], ids[offs[b]:offs[b + 1]], m)
+        np.testing.assert_array_equal(got[b].view(np.int64)[:, 1], r_ref)
+        np.testing.assert_array_equal(got[b][:, 0], s_ref)
+
+
+def test_reranker_scores_order_and_retriever():
+    import torch
+
+    from hiprag.rag import BatchedVectorRetriever, Chunk, RetrievalResult, RetrieverConfig
+    from hiprag.rag.rerankers import TorchRocmReranker
+
+    rr = TorchRocmReranker(preset="tiny", dtype="float32", batch_size=7, max_length=64)
+    words = [f"w{i}" for i in range(300)]
+    rng = np.random.default_rng(0)
+    texts = [" ".join(rng.choice(words, rng.integers(1, 80))) for _ in range(60)]
+    results = [RetrievalResult(chunk=Chunk(id=f"c{i}", document_id="d", content=t, chunk_index=i), score=0.1, rank=i + 1)
+               for i, t in enumerate(texts)]
+    query = "w1 w2 w3 w17"
+    s = rr.score_pairs([query], [texts])[0].cpu().numpy()
+    q_ids = rr._text_ids(query, cache=False)
+    ref = []
+    with torch.inference_mode():
+        for t in texts:
+            ids, types = rr._pair(q_ids, rr._text_ids(t, cache=True))
+            logit = rr.model(input_ids=torch.tensor([ids], device="cuda"),
+                             token_type_ids=torch.tensor([types], device="cuda")).logits[0, 0]
+            ref.append(torch.sigmoid(logit.float()).item())
+    np.testing.assert_allclose(s, ref, rtol=0, atol=1e-5)
+    out = asyncio.run(rr.rerank(query, results, top_k=15))
+    order = np.lexsort((np.arange(len(s)), -s.astype(np.float64)))[:15]
+    assert [r.chunk.id for r in out] == [f"c{i}" for i in order]
+    assert [r.rank for r in out] == list(range(1, 16))
+    batch = rr.rerank_batch([query, "w5"], [results, results[:10]], top_k=15)
+    assert [r.chunk.id for r in batch[0]] == [r.chunk.id for r in out] and len(batch[1]) == 10
+
+    # through the retriever: 2*top_k candidates from the store, reranked to top_k (base_retriever.py:61-80)
+    class Store:
+        def search_batch(self, qvs, k, filters=None):
+            return [[(r.chunk, 0.9 - 0.01 * i) for i, r in enumerate(results[:k])] for _ in qvs]
+
+    class Emb:
+        async def embed_query(self, q):
+            return [0.0]
+
+    ret = BatchedVectorRetriever(Store(), Emb(), RetrieverConfig(top_k=5, similarity_threshold=0.0), reranker=rr)
+    got = asyncio.run(ret.batch_retrieve([query], top_k=5))[0]
+    want = asyncio.run(rr.rerank(query, results[:10], top_k=5))
+    assert [r.chunk.id for r in got] == [r.chunk.id for r in want]

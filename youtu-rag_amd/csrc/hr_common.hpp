@@ -60,9 +60,10 @@ __device__ inline float dequant_mt(uint16_t h) {
     return MT == BF16 ? bf16_to_f32(h) : f16_to_f32(h);
 }
 
-// order-preserving float <-> uint32 key (larger key = larger float)
+// order-preserving float <-> uint32 key (larger key = larger float); -0 and +0 share a key, as
+// they compare equal (the oracle orders with IEEE comparisons)
 __device__ __host__ inline uint32_t f2key(float f) {
-    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    uint32_t u = __builtin_bit_cast(uint32_t, f == 0.0f ? 0.0f : f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 __device__ __host__ inline float key2f(uint32_t k) {
@@ -72,7 +73,7 @@ __device__ __host__ inline float key2f(uint32_t k) {
 #define HR_KEY_NEG_INF 0x007FFFFFu  // f2key(-inf)
 
 __device__ __host__ inline uint64_t d2key(double d) {
-    uint64_t u = __builtin_bit_cast(uint64_t, d);
+    uint64_t u = __builtin_bit_cast(uint64_t, d == 0.0 ? 0.0 : d);
     return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 

@@ -52,7 +52,8 @@ __device__ inline uint64_t cand_key(const Cand& e) { return e.row < 0 ? 0ull : d
 __device__ inline uint64_t id_key(int64_t id) { return (uint64_t)id ^ 0x8000000000000000ull; }
 
 __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in, const int64_t* __restrict__ seg_off,
-                                                    int64_t seg_stride, int B, int m, Cand* __restrict__ out) {
+                                                    int seg_scale, int64_t seg_stride, int B, int m,
+                                                    Cand* __restrict__ out) {
     __shared__ uint32_t hist[256];
     __shared__ uint64_t sh_prefix;
     __shared__ int64_t sh_need;
@@ -63,8 +64,8 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
     const int b = blockIdx.x;
     if (b >= B) return;
     const int tid = threadIdx.x;
-    const int64_t lo = seg_off ? seg_off[b] * 32 : (int64_t)b * seg_stride;
-    const int64_t hi = seg_off ? seg_off[b + 1] * 32 : lo + seg_stride;
+    const int64_t lo = seg_off ? seg_off[b] * seg_scale : (int64_t)b * seg_stride;
+    const int64_t hi = seg_off ? seg_off[b + 1] * seg_scale : lo + seg_stride;
     const Cand* seg = in + lo;
     const int64_t n = hi - lo;
 
@@ -363,7 +364,7 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         hipLaunchKernelGGL(k_coarse, dim3((nlist + 3) / 4), dim3(256), 0, st, centroids_dev, nlist, dpad,
                            sc.q32.as<float>(), bc, h->ivf_coarse.as<Cand>());
         hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_coarse.as<Cand>(), (const int64_t*)nullptr,
-                           (int64_t)nlist, bc, nprobe, h->ivf_probe.as<Cand>());
+                           1, (int64_t)nlist, bc, nprobe, h->ivf_probe.as<Cand>());
         hipLaunchKernelGGL(k_ivf_units, dim3(1), dim3(1024), 0, st, h->ivf_probe.as<Cand>(), bc, nprobe,
                            list_tiles_dev, h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), cap);
         HIP_TRY(hipGetLastError());
@@ -377,7 +378,7 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         });
         if (rc) return rc;
         hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_out.as<Cand>(), h->ivf_uoff.as<int64_t>(),
-                           (int64_t)0, bc, k, (Cand*)cand_out_dev + (int64_t)b0 * k);
+                           32, (int64_t)0, bc, k, (Cand*)cand_out_dev + (int64_t)b0 * k);
         HIP_TRY(hipGetLastError());
         if (probes_out_dev)
             HIP_TRY(hipMemcpyAsync((Cand*)probes_out_dev + (int64_t)b0 * nprobe, h->ivf_probe.p,
@@ -385,6 +386,19 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
     }
     // exact over the visible rows: nothing unreturned can matter
     hipLaunchKernelGGL(k_fill_f64, dim3((B + 255) / 256), dim3(256), 0, st, bound_out_dev, B, -INFINITY);
+    HIP_TRY(hipGetLastError());
+    return HR_OK;
+}
+
+// Exact top-m records per segment, (score desc, id asc), ids < 0 absent: segment b is
+// [seg_off[b], seg_off[b+1]) records if seg_off (int64, in records) is given, else
+// [b * seg_stride, (b + 1) * seg_stride).  The reranker's per-query selection and the IVF stages.
+extern "C" int hr_topk_records(const void* in_dev, const int64_t* seg_off_records_dev, int64_t seg_stride, int B,
+                               int m, void* out_dev, void* stream) {
+    if (!in_dev || !out_dev || B <= 0 || m <= 0 || m > kTopkMax || (!seg_off_records_dev && seg_stride < 0))
+        return set_err(HR_E_INVALID, "bad arguments (need 1 <= m <= 1024)");
+    hipLaunchKernelGGL(k_topk_cand, dim3(B), dim3(1024), 0, (hipStream_t)stream, (const Cand*)in_dev,
+                       seg_off_records_dev, 1, seg_stride, B, m, (Cand*)out_dev);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }

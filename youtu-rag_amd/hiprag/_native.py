@@ -39,7 +39,7 @@ EXPORTS = [
     "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
-    "hr_gen_rows_device", "hr_ivf_search",
+    "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records",
 ]
 
 _lib = None
@@ -88,6 +88,7 @@ def load_library(path: str | None = None):
             "hr_index_search_shard_async": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp, vp],
             "hr_index_add_device_at": [vp, vp, i64, vp, i64, vp],
             "hr_gen_rows_device": [u64, i64, i64, i32, vp, vp],
+            "hr_topk_records": [vp, vp, i64, i32, i32, vp, vp],
             "hr_ivf_search": [vp, vp, i32, vp, i64, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_index_search_shard_collect": [vp, vp, i32, vp, i32, vp, i64, vp, vp, vp],
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
@@ -313,6 +314,14 @@ def gen_rows_device(seed: int, row0: int, n: int, dim: int, out_ptr: int, stream
     """Synthetic corpus rows [row0, row0 + n) as fp32 into device memory (the hr_index_add_synthetic generator)."""
     _check(load_library().hr_gen_rows_device(int(seed), int(row0), int(n), int(dim), ctypes.c_void_p(out_ptr),
                                              ctypes.c_void_p(stream or None)))
+
+
+def topk_records(in_ptr: int, B: int, m: int, out_ptr: int, seg_stride: int = 0, seg_off_ptr: int = 0,
+                 stream: int = 0) -> None:
+    """Exact top-m {score f64, id i64} records per segment, (score desc, id asc) (hr_topk_records)."""
+    _check(load_library().hr_topk_records(ctypes.c_void_p(in_ptr), ctypes.c_void_p(seg_off_ptr or None),
+                                          int(seg_stride), int(B), int(m), ctypes.c_void_p(out_ptr),
+                                          ctypes.c_void_p(stream or None)))
 
 
 def merge_candidates(device: int, cand_ptr: int, bounds_ptr: int, G: int, B: int, kc: int, k: int, scores_ptr: int,

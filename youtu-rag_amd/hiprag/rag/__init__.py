@@ -6,6 +6,7 @@ from .chunker import RecursiveTextSplitter
 from .config import (ChunkingConfig, EmbeddingConfig, KnowledgeBuilderConfig, MonitorConfig, RAGConfig,
                      RetrieverConfig, VectorStoreConfig)
 from .embeddings import EmbedderFactory, ServiceEmbedder, create_embedder
+from .rerankers import RerankerFactory, TorchRocmReranker
 from .retriever import BatchedVectorRetriever, HybridRetriever, VectorRetriever
 from .storage import HipVectorStore, VectorStoreFactory
 
@@ -15,5 +16,5 @@ __all__ = [
     "RetrievalResult", "RecursiveTextSplitter", "ChunkingConfig", "EmbeddingConfig", "KnowledgeBuilderConfig",
     "MonitorConfig", "RAGConfig", "RetrieverConfig", "VectorStoreConfig", "EmbedderFactory", "ServiceEmbedder",
     "create_embedder", "BatchedVectorRetriever", "HybridRetriever", "VectorRetriever", "HipVectorStore",
-    "VectorStoreFactory",
+    "VectorStoreFactory", "RerankerFactory", "TorchRocmReranker",
 ]

@@ -75,7 +75,17 @@ class BatchedVectorRetriever(VectorRetriever):
         embed_many = getattr(self.embedder, "embed_queries", None)
         qvs = await embed_many(queries) if embed_many else [await self.embedder.embed_query(q) for q in queries]
         hits = search_batch(qvs, top_k * 2 if self.reranker else top_k, kwargs.get("filters"))
-        return [await self._finish(q, self._to_results(h, threshold), top_k) for q, h in zip(queries, hits)]
+        results = [self._to_results(h, threshold) for h in hits]
+        rerank_batch = getattr(self.reranker, "rerank_batch", None)
+        if rerank_batch is not None:  # one set of cross-encoder batches for every query's pairs
+            idx = [i for i, r in enumerate(results) if r]
+            try:
+                for i, r in zip(idx, rerank_batch([queries[i] for i in idx], [results[i] for i in idx], top_k)):
+                    results[i] = r
+                return [r[:top_k] for r in results]
+            except Exception as e:  # per-query path keeps the reference's failure semantics
+                logger.error(f"batched reranking failed ({e}); reranking query by query")
+        return [await self._finish(q, r, top_k) for q, r in zip(queries, results)]
 
 
 class HybridRetriever(BaseRetriever):

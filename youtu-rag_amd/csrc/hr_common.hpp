@@ -87,11 +87,20 @@ __device__ __host__ inline double key2d(uint64_t k) {
 template <int DT>
 __device__ __host__ inline size_t chunk_bytes() { return DT == F32 ? 2048 : 1024; }
 
+// Slot swizzle: row r of tile t = r / 32 sits in tile slot (r + tile_rot(t)) % 32, i.e. in the
+// MFMA lane / group-max group of that slot.  The per-tile rotation is a Fibonacci hash of the tile,
+// so rows that share r % 32 (a document's k-th chunks, a cluster inserted with a period that is a
+// multiple of 32, ...) spread over all 32 groups instead of collapsing into one, which would leave
+// the other 31 group maxima to background rows and the scan threshold far below the top-k.
+__device__ __host__ inline int tile_rot(int64_t t) { return (int)((uint32_t)((uint64_t)t * 0x9E3779B1ull) >> 27); }
+__device__ __host__ inline int row_slot(int64_t r) { return (int)((r + tile_rot(r >> 5)) & 31); }
+__device__ __host__ inline int slot_row(int64_t t, int slot) { return (slot - tile_rot(t)) & 31; }  // row % 32
+
 // element (row r, column d) of the tiled corpus, as float
 template <int DT>
 __device__ inline float load_elem(const uint8_t* base, int S, int64_t r, int d) {
     int64_t chunk = (r >> 5) * S + (d >> 4);
-    int lane = (int)(r & 31) + 32 * ((d >> 3) & 1);
+    int lane = row_slot(r) + 32 * ((d >> 3) & 1);
     int j = d & 7;
     if (DT == F32) {
         const float* p = (const float*)(base + chunk * 2048 + (j >> 2) * 1024 + lane * 16);

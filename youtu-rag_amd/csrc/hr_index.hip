@@ -365,9 +365,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     if (MODE == SCAN_SAMPLE) lds = std::max(lds, (kScanThreads / 64) * pl.QB * 16 * 64 * 4 + 64);
 #define HR_SCAN_CASE(QBv, Pv) \
     if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, sc, cus, a, st, lds);
-    if constexpr (MODE == SCAN_COLLECT) {  // the fallback runs one query at a time
-        HR_SCAN_CASE(1, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4)
-    } else if constexpr (DT == F32) {
+    if constexpr (DT == F32) {
         HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
     } else {
         HR_SCAN_CASE(1, 16) HR_SCAN_CASE(2, 16) HR_SCAN_CASE(1, 8) HR_SCAN_CASE(2, 8) HR_SCAN_CASE(1, 4)
@@ -652,7 +650,7 @@ static int launch_merge(int device, const Cand* cand, const double* bounds, int 
     return HR_OK;
 }
 
-static constexpr int kFallbackCap = 512;
+static constexpr int kFallbackCap = 1024;
 
 // full single-shard search on device-resident queries, with the exact fallback
 static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
@@ -677,24 +675,44 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     for (int b = 0; b < B; ++b)
         if (fail[(size_t)b]) failed.push_back(b);
     if (failed.empty()) return HR_OK;
-    // exact fallback: re-scan the failing queries collecting every row with approx >= kth - E
-    for (int b : failed) {
-        const int kc2 = kFallbackCap;
-        HIP_TRY(h->fb_cand.ensure((size_t)kc2 * sizeof(Cand)));
-        HIP_TRY(h->fb_bound.ensure(64));
-        double kb = kth[(size_t)b];
-        if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, kc2, mask_dev, 0, &kb, 1, kc2,
-                                 h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), st, st))
-            return rc;
-        double bd = 0;
-        HIP_TRY(hipMemcpyAsync(&bd, h->fb_bound.p, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (bd > 0) return set_err(HR_E_OVERFLOW, "exact fallback overflowed its candidate buffer (massive ties?)");
-        if (int rc = launch_merge(h->device, h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), 1, 1, kc2, k,
-                                  s_out + (int64_t)b * k, r_out + (int64_t)b * k, h->kth.as<double>() + b,
-                                  h->fail.as<int32_t>() + b, st))
+    // exact fallback: ONE collect re-scan of all failing queries (every row with approx >= kth - E,
+    // rescored exactly), merged, then scattered back to the failing rows of the outputs
+    const int nf = (int)failed.size(), kc2 = kFallbackCap;
+    HIP_TRY(h->fb_q.ensure((size_t)nf * h->dim * 4));
+    HIP_TRY(h->fb_cand.ensure((size_t)nf * kc2 * sizeof(Cand)));
+    HIP_TRY(h->fb_bound.ensure((size_t)nf * 8));
+    HIP_TRY(h->fb_out.ensure((size_t)nf * k * 12 + (size_t)nf * 12 + 64));
+    float* fs = h->fb_out.as<float>();
+    int64_t* fr = (int64_t*)(h->fb_out.as<uint8_t>() + (((size_t)nf * k * 4 + 7) & ~(size_t)7));
+    double* fk = (double*)(fr + (size_t)nf * k);
+    int32_t* ff = (int32_t*)(fk + nf);
+    std::vector<double> kf((size_t)nf);
+    for (int i = 0; i < nf; ++i) {
+        kf[(size_t)i] = kth[(size_t)failed[(size_t)i]];
+        HIP_TRY(hipMemcpyAsync(h->fb_q.as<float>() + (int64_t)i * h->dim, q_dev + (int64_t)failed[(size_t)i] * h->dim,
+                               (size_t)h->dim * 4, hipMemcpyDeviceToDevice, st));
+    }
+    Plan pl;
+    if (int rc = make_plan(h, nf, &pl)) return rc;
+    for (int b0 = 0; b0 < nf; b0 += pl.Bp) {
+        const int bc = std::min(pl.Bp, nf - b0);
+        if (int rc = shard_chunk(h, h->fb_q.as<float>() + (int64_t)b0 * h->dim, bc, kc2, mask_dev, 0, &kf[(size_t)b0], 1,
+                                 kc2, h->fb_cand.as<Cand>() + (int64_t)b0 * kc2, h->fb_bound.as<double>() + b0, st, st))
             return rc;
     }
+    if (int rc = launch_merge(h->device, h->fb_cand.as<Cand>(), h->fb_bound.as<double>(), 1, nf, kc2, k, fs, fr, fk, ff,
+                              st))
+        return rc;
+    std::vector<int32_t> ff_h((size_t)nf);
+    HIP_TRY(hipMemcpyAsync(ff_h.data(), ff, (size_t)nf * 4, hipMemcpyDeviceToHost, st));
+    for (int i = 0; i < nf; ++i) {
+        const int b = failed[(size_t)i];
+        HIP_TRY(hipMemcpyAsync(s_out + (int64_t)b * k, fs + (int64_t)i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(r_out + (int64_t)b * k, fr + (int64_t)i * k, (size_t)k * 8, hipMemcpyDeviceToDevice, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < nf; ++i)
+        if (ff_h[(size_t)i]) return set_err(HR_E_OVERFLOW, "exact fallback overflowed its candidate buffer (massive ties?)");
     HIP_TRY(hipStreamSynchronize(st));
     return HR_OK;
 }
@@ -777,9 +795,12 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
     HIP_TRY(hipMemcpyAsync(kth.data(), kth_dev, (size_t)B * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     Cand* out = (Cand*)cand_out_dev;
-    for (int b = 0; b < B; ++b) {
-        if (int rc = shard_chunk(h, q_dev + (int64_t)b * h->dim, 1, cap, row_mask_dev, row_offset, &kth[(size_t)b], 1,
-                                 cap, out + (int64_t)b * cap, bound_out_dev + b, st, st))
+    Plan pl;
+    if (int rc = make_plan(h, B, &pl)) return rc;
+    for (int b0 = 0; b0 < B; b0 += pl.Bp) {  // one collect scan per chunk of queries
+        const int bc = std::min(pl.Bp, B - b0);
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, row_mask_dev, row_offset, &kth[(size_t)b0], 1,
+                                 cap, out + (int64_t)b0 * cap, bound_out_dev + b0, st, st))
             return rc;
     }
     return HR_OK;
@@ -905,7 +926,7 @@ extern "C" int hr_index_save(hr_index* h, const char* path) {
     FILE* f = std::fopen(path, "wb");
     if (!f) return set_err(HR_E_IO, std::string("cannot open ") + path);
     FileHeader hd{};
-    std::memcpy(hd.magic, "HIPRAG01", 8);
+    std::memcpy(hd.magic, "HIPRAG02", 8);  // 02: slot-swizzled tiles
     hd.version = 1;
     hd.dim = h->dim;
     hd.dtype = h->dtype;
@@ -937,7 +958,7 @@ extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr
     FILE* f = std::fopen(path, "rb");
     if (!f) return set_err(HR_E_IO, std::string("cannot open ") + path);
     FileHeader hd{};
-    if (std::fread(&hd, sizeof(hd), 1, f) != 1 || std::memcmp(hd.magic, "HIPRAG01", 8) != 0) {
+    if (std::fread(&hd, sizeof(hd), 1, f) != 1 || std::memcmp(hd.magic, "HIPRAG02", 8) != 0) {
         std::fclose(f);
         return set_err(HR_E_IO, "not a hiprag index file");
     }
@@ -992,7 +1013,8 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->xnorm) (void)hipFree(h->xnorm);
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
-    for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->stage, &h->exh,
+    for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
+                      &h->fb_out, &h->stage, &h->exh,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();

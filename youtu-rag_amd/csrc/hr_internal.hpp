@@ -107,7 +107,7 @@ struct hr_index {
     int n_cu = 256;
     std::mutex mu;
     // search workspace
-    DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, stage, exh;
+    DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, fb_q, fb_out, stage, exh;
     DevBuf ivf_coarse, ivf_probe, ivf_units, ivf_uoff, ivf_out;  // IVF lists search (hr_ivf.hip)
     Scratch scr[3];
     int flip = 0;                     // next ping-pong set of the pipelined path

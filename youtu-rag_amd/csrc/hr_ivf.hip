@@ -24,21 +24,54 @@
 namespace {
 
 // ---------------------------------------------------------------- K9: coarse scores
-// One wave per centroid, every query: the centroid row is read once, the queries come from L2.
-// Score = canonical fp64 dot of the processed query and the fp32 centroid (oracle order).
-__global__ __launch_bounds__(256) void k_coarse(const float* __restrict__ cent, int nlist, int dpad,
-                                                const float* __restrict__ q32, int B, Cand* __restrict__ out) {
+// Exact canonical fp64 score of every (query, centroid) pair (oracle order: lane-strided partial
+// sums + butterfly).  A 1024-thread workgroup = 16 waves = 16 centroids; the processed queries
+// are staged through LDS up to 32 at a time (128 KiB at dpad 1024), so L2 serves each query once per
+// workgroup instead of once per wave.
+__global__ __launch_bounds__(1024) void k_coarse(const float* __restrict__ cent, int nlist, int dpad,
+                                                 const float* __restrict__ q32, int B, int qgroup,
+                                                 Cand* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float qs[];  // [kCoarseQ][dpad]
     const int lane = threadIdx.x & 63;
-    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (l >= nlist) return;
-    const float* c = cent + (int64_t)l * dpad;
-    for (int b = 0; b < B; ++b) {
-        const float* qv = q32 + (int64_t)b * dpad;
-        double p = 0.0;
-#pragma unroll 8
-        for (int d = lane; d < dpad; d += 64) p = p + (double)c[d] * (double)qv[d];
-        p = wave_butterfly_sum(p);
-        if (lane == 0) out[(int64_t)b * nlist + l] = Cand{p, l};
+    const int l = blockIdx.x * 16 + (threadIdx.x >> 6);
+    const float* c = cent + (int64_t)(l < nlist ? l : 0) * dpad;
+    for (int b0 = 0; b0 < B; b0 += qgroup) {
+        const int nb = B - b0 < qgroup ? B - b0 : qgroup;
+        __syncthreads();  // previous group done with LDS
+        for (int i = threadIdx.x; i < nb * dpad / 4; i += blockDim.x)
+            ((float4*)qs)[i] = ((const float4*)(q32 + (int64_t)b0 * dpad))[i];
+        __syncthreads();
+        if (l < nlist) {
+            int b = 0;
+            for (; b + 4 <= nb; b += 4) {  // four independent sums and butterflies interleave (ILP)
+                double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+                for (int d = lane; d < dpad; d += 64) {
+                    const double cd = (double)c[d];
+                    p0 = p0 + cd * (double)qs[(b + 0) * dpad + d];
+                    p1 = p1 + cd * (double)qs[(b + 1) * dpad + d];
+                    p2 = p2 + cd * (double)qs[(b + 2) * dpad + d];
+                    p3 = p3 + cd * (double)qs[(b + 3) * dpad + d];
+                }
+                p0 = wave_butterfly_sum(p0);
+                p1 = wave_butterfly_sum(p1);
+                p2 = wave_butterfly_sum(p2);
+                p3 = wave_butterfly_sum(p3);
+                if (lane == 0) {
+                    Cand* o = out + (int64_t)(b0 + b) * nlist + l;
+                    o[0] = Cand{p0, l};
+                    o[nlist] = Cand{p1, l};
+                    o[2 * (int64_t)nlist] = Cand{p2, l};
+                    o[3 * (int64_t)nlist] = Cand{p3, l};
+                }
+            }
+            for (; b < nb; ++b) {
+                const float* qv = qs + b * dpad;
+                double p = 0.0;
+                for (int d = lane; d < dpad; d += 64) p = p + (double)c[d] * (double)qv[d];
+                p = wave_butterfly_sum(p);
+                if (lane == 0) out[(int64_t)(b0 + b) * nlist + l] = Cand{p, l};
+            }
+        }
     }
 }
 
@@ -113,7 +146,54 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
     __syncthreads();
 
     uint64_t kth = 0, id_thr = ~0ull;  // take key > kth, or key == kth with ~id_key >= id_thr
-    if (n_valid > m) {
+    bool done = n_valid <= m;
+    if (!done) {
+        // Level 1: the m-th largest of the keys' upper 32 bits (4 radix passes).  Usually only a few
+        // records share that prefix, so every record at or above it fits in LDS and one bitonic sort
+        // of (key, id) finishes the job; otherwise fall through to the full 64-bit + id selection.
+        uint64_t prefix = 0, mask = 0;
+        if (tid == 0) sh_need = m;
+        for (int shift = 56; shift >= 32; shift -= 8) {
+            for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+            __syncthreads();
+            for (int64_t i = tid; i < n; i += blockDim.x) {
+                const uint64_t k = cand_key(seg[i]);
+                if (k != 0 && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int64_t need = sh_need, above = 0;
+                int d = 255;
+                for (; d > 0; --d) {
+                    if (above + hist[d] >= need) break;
+                    above += hist[d];
+                }
+                sh_need = need - above;
+                sh_prefix = prefix | ((uint64_t)d << shift);
+            }
+            __syncthreads();
+            prefix = sh_prefix;
+            mask |= (uint64_t)255 << shift;
+        }
+        // records with upper key >= the m-th: gather if they fit
+        if (tid == 0) sh_cnt = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            const Cand e = seg[i];
+            const uint64_t k = cand_key(e);
+            if (k == 0 || (k & mask) < prefix) continue;
+            const int p = atomicAdd(&sh_cnt, 1);
+            if (p < kTopkMax) {
+                skey[p] = k;
+                sid[p] = e.row;
+                ssc[p] = e.score;
+            }
+        }
+        __syncthreads();
+        done = sh_cnt <= kTopkMax;
+        __syncthreads();
+    }
+    if (!done && n_valid > m) {
         kth = select_key(false, 0, m);
         const int64_t need_ties = sh_need;  // winners among records with key == kth
         // are all ties needed?  count them
@@ -129,7 +209,8 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
         if (n_ties > need_ties) id_thr = select_key(true, kth, need_ties);
         else id_thr = 0;
     }
-    // gather the winners (exactly min(m, n_valid))
+    // gather the winners (exactly min(m, n_valid)) unless level 1 already holds a superset in LDS
+    if (!done || n_valid <= m) {
     if (tid == 0) sh_cnt = 0;
     __syncthreads();
     for (int64_t i = tid; i < n; i += blockDim.x) {
@@ -144,6 +225,7 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
             sid[p] = e.row;
             ssc[p] = e.score;
         }
+    }
     }
     __syncthreads();
     const int cnt = sh_cnt < kTopkMax ? sh_cnt : kTopkMax;
@@ -231,35 +313,49 @@ __global__ __launch_bounds__(1024) void k_ivf_units(const Cand* __restrict__ pro
 // One wave per unit at a time (static contiguous split of the unit list).  Lane l = r + 32h of a
 // k-step chunk holds elements 16s + 8h + j of row r, i.e. canonical partials c = 16(s%4) + 8h + j;
 // the oracle's butterfly (off 32, 16: local; 8: lanes r <-> r+32; 4, 2, 1: local) then gives the
-// canonical score of row r on lane r.
+// canonical score of row r on lane r.  The chunk stream of a wave (its units back to back) goes
+// through a ring of P raw 16-byte loads (the same software pipeline as the brute-force scan), so
+// P KiB per wave stay in flight across unit boundaries.
 template <int DT>
-__device__ inline void load_chunk(const uint8_t* rows, int64_t c, int lane, float (&x)[8]) {
-    if constexpr (DT == F32) {
-        typedef float f32x4 __attribute__((ext_vector_type(4)));
-        const f32x4 a = __builtin_nontemporal_load((const f32x4*)(rows + c * 2048 + lane * 16));
-        const f32x4 b = __builtin_nontemporal_load((const f32x4*)(rows + c * 2048 + 1024 + lane * 16));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            x[j] = a[j];
-            x[4 + j] = b[j];
-        }
-    } else {
-        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(rows + c * 1024 + lane * 16));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint16_t lo = (uint16_t)(v[j] & 0xFFFFu), hi = (uint16_t)(v[j] >> 16);
-            x[2 * j] = DT == BF16 ? bf16_to_f32(lo) : f16_to_f32(lo);
-            x[2 * j + 1] = DT == BF16 ? bf16_to_f32(hi) : f16_to_f32(hi);
+struct RawChunk {  // one k-step chunk of this lane, undecoded
+    u32x4 a, b;
+    __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
+        if constexpr (DT == F32) {
+            a = __builtin_nontemporal_load((const u32x4*)(rows + c * 2048 + lane * 16));
+            b = __builtin_nontemporal_load((const u32x4*)(rows + c * 2048 + 1024 + lane * 16));
+        } else {
+            a = __builtin_nontemporal_load((const u32x4*)(rows + c * 1024 + lane * 16));
         }
     }
-}
+    __device__ inline void get(float (&x)[8]) const {
+        if constexpr (DT == F32) {
+            // whole-vector bit casts: hipcc (ROCm 7.2) mis-lowers bit casts of single ext-vector
+            // elements here (see XFrag<MT, F32> in hr_kernels.hpp)
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            const f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                x[j] = fa[j];
+                x[4 + j] = fb[j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint16_t lo = (uint16_t)(a[j] & 0xFFFFu), hi = (uint16_t)(a[j] >> 16);
+                x[2 * j] = DT == BF16 ? bf16_to_f32(lo) : f16_to_f32(lo);
+                x[2 * j + 1] = DT == BF16 ? bf16_to_f32(hi) : f16_to_f32(hi);
+            }
+        }
+    }
+};
 
-template <int DT>
+template <int DT, int P>
 __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ rows, int S,
                                                   const uint32_t* __restrict__ live, const uint32_t* __restrict__ mask,
                                                   const int64_t* __restrict__ ids, const float* __restrict__ q32,
                                                   int dpad, const uint32_t* __restrict__ units,
                                                   const int64_t* __restrict__ uoff, int B, Cand* __restrict__ out) {
+    static_assert(P % 4 == 0, "ring depth is a multiple of the 4-step canonical cycle");
     const int lane = threadIdx.x & 63;
     const int r = lane & 31, h = lane >> 5;
     const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -268,27 +364,34 @@ __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ ro
     const int64_t base = n_units / W, rem = n_units % W;
     const int64_t u0 = w * base + (w < rem ? w : rem);
     const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
+    if (u0 >= u1) return;
+    RawChunk<DT> ring[P];
+    int64_t t_next = units[u0] & 0x3FFFFFFu;
+#pragma unroll
+    for (int i = 0; i < P; ++i) ring[i].load(rows, t_next * S + i, lane);
     for (int64_t u = u0; u < u1; ++u) {
         const uint32_t pk = units[u];
         const int64_t t = pk & 0x3FFFFFFu;
         const int b = (int)(pk >> 26);
+        const int64_t tn = u + 1 < u1 ? (int64_t)(units[u + 1] & 0x3FFFFFFu) : t;  // prefetch target after t
         const float* qv = q32 + (int64_t)b * dpad + 8 * h;
         double acc[4][8];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[a][j] = 0.0;
-        for (int s4 = 0; s4 < S; s4 += 4) {
-            float x[4][8];
+        for (int s0 = 0; s0 < S; s0 += P) {
+            const int64_t nc = s0 + P < S ? t * S + s0 + P : tn * S;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) load_chunk<DT>(rows, t * S + s4 + a, lane, x[a]);
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const float4 q0 = *(const float4*)(qv + 16 * (s4 + a));
-                const float4 q1 = *(const float4*)(qv + 16 * (s4 + a) + 4);
+            for (int i = 0; i < P; ++i) {
+                float x[8];
+                ring[i].get(x);
+                ring[i].load(rows, nc + i, lane);
+                const float4 q0 = *(const float4*)(qv + 16 * (s0 + i));
+                const float4 q1 = *(const float4*)(qv + 16 * (s0 + i) + 4);
                 const float qq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[a][j] = __builtin_fma((double)x[a][j], (double)qq[j], acc[a][j]);
+                for (int j = 0; j < 8; ++j) acc[i % 4][j] = __builtin_fma((double)x[j], (double)qq[j], acc[i % 4][j]);
             }
         }
         // canonical butterfly over partial index c = 16a + 8h + j
@@ -306,11 +409,12 @@ __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ ro
         p[0] = p[0] + p[4]; p[1] = p[1] + p[5]; p[2] = p[2] + p[6]; p[3] = p[3] + p[7];  // off 4
         p[0] = p[0] + p[2]; p[1] = p[1] + p[3];                                          // off 2
         p[0] = p[0] + p[1];                                                              // off 1
-        if (h == 0) {
+        if (h == 0) {  // lane r holds the row of slot r (slot swizzle, hr_common.hpp)
+            const int rr = slot_row(t, r);
             uint32_t allow = live[t];
             if (mask) allow &= mask[t];
-            const int64_t pos = t * 32 + r;
-            const bool ok = (allow >> r) & 1u;
+            const int64_t pos = t * 32 + rr;
+            const bool ok = (allow >> rr) & 1u;
             out[u * 32 + r] = ok ? Cand{p[0], ids[pos]} : Cand{-__builtin_inf(), -1};
         }
     }
@@ -361,8 +465,14 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
             hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, qb, bc, Bp, h->dim, dpad, h->S,
                                QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
                                nullptr, 1, nullptr, nullptr, nullptr);
-        hipLaunchKernelGGL(k_coarse, dim3((nlist + 3) / 4), dim3(256), 0, st, centroids_dev, nlist, dpad,
-                           sc.q32.as<float>(), bc, h->ivf_coarse.as<Cand>());
+        static bool coarse_attr[64] = {};
+        if (!coarse_attr[h->device & 63]) {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_coarse, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            coarse_attr[h->device & 63] = true;
+        }
+        const int qgroup = std::max(1, std::min(32, (160 * 1024) / (dpad * 4)));  // queries per LDS stage
+        hipLaunchKernelGGL(k_coarse, dim3((nlist + 15) / 16), dim3(1024), (size_t)qgroup * dpad * 4, st,
+                           centroids_dev, nlist, dpad, sc.q32.as<float>(), bc, qgroup, h->ivf_coarse.as<Cand>());
         hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_coarse.as<Cand>(), (const int64_t*)nullptr,
                            1, (int64_t)nlist, bc, nprobe, h->ivf_probe.as<Cand>());
         hipLaunchKernelGGL(k_ivf_units, dim3(1), dim3(1024), 0, st, h->ivf_probe.as<Cand>(), bc, nprobe,
@@ -370,8 +480,14 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         HIP_TRY(hipGetLastError());
         const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * 8, (cap + 3) / 4));
         int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
-            hipLaunchKernelGGL((k_ivf_scan<decltype(dt)::value>), dim3((unsigned)blocks), dim3(256), 0, st, h->rows,
-                               h->S, h->live, (const uint32_t*)row_mask_dev, ids_dev, sc.q32.as<float>(), dpad,
+            constexpr int DT = decltype(dt)::value;
+            // ring depth (chunks in flight per wave): fp32 rows 4 (8 KiB; deeper rings spill), 16-bit
+            // rows 16 where the k-steps allow it (HIPRAG_IVF_RING=4|8|16: A/B timing)
+            static const int ring_env = getenv("HIPRAG_IVF_RING") ? atoi(getenv("HIPRAG_IVF_RING")) : 16;
+            const int ring = DT == F32 ? 4 : (h->S % ring_env == 0 ? ring_env : (h->S % 8 == 0 ? 8 : 4));
+            auto kern = ring == 16 ? k_ivf_scan<DT, 16> : ring == 8 ? k_ivf_scan<DT, 8> : k_ivf_scan<DT, 4>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, h->rows, h->S, h->live,
+                               (const uint32_t*)row_mask_dev, ids_dev, sc.q32.as<float>(), dpad,
                                h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), bc, h->ivf_out.as<Cand>());
             HIP_TRY(hipGetLastError());
             return HR_OK;

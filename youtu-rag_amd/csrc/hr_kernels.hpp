@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uin
         }
         const int s = c >> 1, h = c & 1;
         const int64_t chunk = (R >> 5) * S + s;
-        const int sl = (int)(R & 31) + 32 * h;
+        const int sl = row_slot(R) + 32 * h;
         if (DT == F32) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) sq += (double)v[j] * (double)v[j];
@@ -507,8 +507,10 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
+        // row held by this lane's slot (slot swizzle, hr_common.hpp)
+        const int rg = slot_row(t, g);
         // euclidean: this tile's row norms, loaded before the k-loop so they are back by the epilogue
-        const float xs = a.xnorm ? a.xnorm[t * 32 + g] : 0.0f;
+        const float xs = a.xnorm ? a.xnorm[t * 32 + rg] : 0.0f;
         const float xmul = a.xnorm ? 2.0f : 1.0f;
 
         for (int sb = 0; sb < S; sb += P) {
@@ -535,8 +537,8 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
         }
         uint32_t allow = a.live[t];
         if (a.mask) allow &= a.mask[t];
-        const bool ok = (allow >> g) & 1u;
-        const uint32_t row = (uint32_t)(t * 32 + g);
+        const bool ok = (allow >> rg) & 1u;
+        const uint32_t row = (uint32_t)(t * 32 + rg);
         uint64_t any = 0;
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
@@ -667,12 +669,13 @@ __global__ __launch_bounds__(256) void k_debug_approx(const uint8_t* __restrict_
         for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma32<MT>(qs[(s * QB + qb) * 64 + lane], xf, acc[qb]);
     }
     const int64_t ncol = n_tiles * 32;
-    const float xs = xnorm ? xnorm[t * 32 + (lane & 31)] : 0.0f;  // euclidean: same score as k_scan
+    const int rg = slot_row(t, lane & 31);
+    const float xs = xnorm ? xnorm[t * 32 + rg] : 0.0f;  // euclidean: same score as k_scan
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-            out[(int64_t)acc_query(qb, i, lane >> 5) * ncol + t * 32 + (lane & 31)] =
+            out[(int64_t)acc_query(qb, i, lane >> 5) * ncol + t * 32 + rg] =
                 xnorm ? __builtin_fmaf(2.0f, acc[qb][i], -xs) : acc[qb][i];
 }
 

@@ -30,7 +30,10 @@ import numpy as np
 
 from . import _native
 
-FALLBACK_CAP = 512
+def fallback_cap(G: int) -> int:
+    """Rows per query and shard the collect fallback may return: 1024, bounded so the merge of
+    G shards' records fits the merge kernel's LDS (G * cap <= 8192)."""
+    return max(64, min(1024, 8192 // max(1, G)))
 
 
 def _record_len(B: int, kc: int) -> int:
@@ -188,7 +191,7 @@ class ShardedSearch:
         idx = torch.as_tensor(failed, device=self.device)
         qf = q[idx].contiguous()
         kf = kth[idx].contiguous()
-        Bf, cap = len(failed), FALLBACK_CAP
+        Bf, cap = len(failed), fallback_cap(self.G)
         L = _record_len(Bf, cap)
         rec = torch.empty((L,), dtype=torch.float64, device=self.device)
         cand, bound = _record_views(rec, Bf, cap)

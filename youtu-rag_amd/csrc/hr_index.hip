@@ -529,7 +529,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
             static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
             const int64_t target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048,
-                                                     n_tiles / (sdiv_env > 0 ? sdiv_env : 64));
+                                                     n_tiles / (sdiv_env > 0 ? sdiv_env : 128));  // A/B: 128 beats 64 by 0.7 % at 10M
             a.sample_stride = std::max<int64_t>(1, n_tiles / target);
             a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], st));

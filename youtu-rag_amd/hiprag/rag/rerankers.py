@@ -124,6 +124,14 @@ class TorchRocmReranker(BaseReranker):
                 self._cache[text] = ids
         return ids
 
+    def warm(self, passages) -> int:
+        """Tokenise passages into the cache ahead of reranking (e.g. at ingest, where the chunk text is
+        tokenised for the embedder anyway); returns the number of newly cached passages."""
+        before = len(self._cache)
+        for p in passages:
+            self._text_ids(p, cache=True)
+        return len(self._cache) - before
+
     def _pair(self, q_ids: list[int], p_ids: list[int], passage_is_empty: bool = False
               ) -> tuple[list[int], list[int]]:
         cls_id = getattr(self.tokenizer, "cls_token_id", 101)

@@ -97,7 +97,8 @@ void hr_index_destroy(hr_index* h);
  * Candidate record = {double exact_score; int64 global_row} (16 bytes).
  * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_KC); the scan keeps
  * ceil(kc/32) row parts of group maxima.  hr_kc_for_k gives the kc the single-GPU search
- * uses: 32 for k <= 32, else k + 16 rounded up to a multiple of 32 (margin for the guard). */
+ * uses: 32 for k <= 32, else k + max(16, k/2) rounded up to a multiple of 32, at most
+ * HR_MAX_KC (margin for the guard). */
 int hr_kc_for_k(int k);
 int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                           int64_t row_offset, void* cand_out_dev /* B*kc records */,

@@ -23,8 +23,9 @@ HR_MAX_KC = 160
 
 
 def kc_for_k(k: int) -> int:
-    """Per-shard candidate count for top-k (hr_kc_for_k): 32 for k <= 32, else k + 16 rounded up to 32."""
-    return 32 if k <= 32 else min(HR_MAX_KC, (k + 16 + 31) // 32 * 32)
+    """Per-shard candidate count for top-k (hr_kc_for_k): 32 for k <= 32, else k + max(16, k // 2)
+    rounded up to 32, at most HR_MAX_KC (tests/test_native_abi.py checks it against the library)."""
+    return 32 if k <= 32 else min(HR_MAX_KC, (k + max(16, k // 2) + 31) // 32 * 32)
 
 
 CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand

@@ -512,3 +512,47 @@ def test_euclidean_ties_save_load_and_shards(native, tmp_path):
     assert fail.sum().item() == 0
     np.testing.assert_array_equal(rd.cpu().numpy(), r1)
     np.testing.assert_array_equal(sd.cpu().numpy(), s1)
+
+
+# ---------------------------------------------------------------- seeded fuzz over the parameter space
+def _fuzz_cases(n_cases=36, seed=2024):
+    rng = np.random.default_rng(seed)
+    dims = [1, 17, 63, 64, 65, 130, 255, 384, 1000, 1024, 2560]
+    out = []
+    for i in range(n_cases):
+        dim = int(rng.choice(dims))
+        dtype = str(rng.choice(["f32", "bf16", "f16"]))
+        metric = str(rng.choice(["cosine", "ip", "l2"]))
+        if dtype == "f32" and dim > 1280:
+            dim = 1000  # fp32 query tiles of 2560-d do not fit the LDS-resident plan
+        B = int(rng.choice([1, 7, 33, 64, 65, 100]))
+        k = int(rng.choice([1, 5, 10, 32, 33, 64, 100, 128]))
+        n = int(rng.integers(1, 12000))
+        out.append((i, dim, dtype, metric, B, k, n, bool(rng.random() < 0.4)))
+    return out
+
+
+@pytest.mark.parametrize("case", _fuzz_cases(), ids=lambda c: "-".join(map(str, c)))
+def test_fuzz_vs_oracle(native, case):
+    """Random (dim, dtype, metric, B, k, n, mask) combinations, including B > 64 (query chunks),
+    n < k, odd dims and every metric: ids and bits equal to the oracle."""
+    i, dim, dtype, metric, B, k, n, use_mask = case
+    rng = np.random.default_rng(i)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    if metric != "cosine":
+        x *= (0.5 + rng.random((n, 1))).astype(np.float32)
+    idx = native.NativeIndex(dim, dtype, metric)
+    try:
+        idx.add(x)
+    except ValueError:  # plan limits (dim x dtype) are reported, not silently degraded
+        pytest.skip("unsupported plan")
+    j = rng.integers(0, n, B)
+    q = (x[j] + 0.1 * rng.standard_normal((B, dim))).astype(np.float32)
+    mask = oracle.mask_from_bool(rng.random(n) < 0.5) if use_mask else None
+    try:
+        s, r = idx.search(q, k, mask)
+    except ValueError:
+        pytest.skip("unsupported plan")
+    stored = R.process_rows(x, metric, dtype)
+    s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, metric), k, mask, metric=metric)
+    _check(s, r, s_ref, r_ref)

@@ -35,6 +35,7 @@ import numpy as np  # noqa: E402
 METRIC = "retrieval QPS + recall@10 vs CPU ref, 10M×1024 corpus, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 HBM_COPY_GBS = 6290.0
+MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (no sparsity), MI355X_MICROARCH.md
 
 
 def parse():
@@ -144,6 +145,8 @@ def main():
     n_max_local = -(-N // G)
     alg_bytes = n_max_local * D * esz  # corpus bytes one filter-scan launch must read (largest shard)
     achieved = alg_bytes / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
+    mfma_flops = 2 * 32 * -(-B // 32) * n_max_local * D  # padded query slots x rows x dims per FILTER launch
+    mfma_tflops = mfma_flops / (scan_avg * 1e-3) / 1e12 if scan_avg > 0 else 0.0
 
     result = {
         "metric": METRIC,
@@ -165,6 +168,9 @@ def main():
                      "frac_of_copy_peak": round(achieved / HBM_COPY_GBS, 4), "traffic": None,
                      "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg, 4),
                      "sample_pass_ms": round(sample_avg, 4)},
+        # the Q·Xᵀ contraction of the same launch on the MFMA pipe (bf16 dense peak, MI355X_MICROARCH.md)
+        "mfma": {"achieved": round(mfma_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(mfma_tflops / MFMA_PEAK_TFLOPS, 4), "flops_per_launch": mfma_flops},
     }
 
     # PMC traffic of the same workload from the committed rocprofv3 summary (tools/profile.sh +
@@ -176,6 +182,9 @@ def main():
     if summaries and args.dtype == "bf16" and K == 10:
         with open(summaries[-1]) as f:
             prof = json.load(f)
+        if prof.get("k_scan_filter_mfma_busy_frac") is not None:
+            result["mfma"]["pmc_busy_frac"] = round(prof["k_scan_filter_mfma_busy_frac"], 4)
+            result["mfma"]["pmc_source"] = os.path.relpath(summaries[-1], REPO)
         if prof.get("k_scan_filter_hbm_read_bytes"):
             result["roofline"]["traffic"] = round(prof["k_scan_filter_hbm_read_bytes"] / 1e9, 3)
             result["roofline"]["traffic_unit"] = "GB per launch (HBM read, PMC)"

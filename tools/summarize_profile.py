@@ -32,6 +32,20 @@ def main(src, tag, alg_bytes=None):
     out = {"tag": tag, "kernels_ms_avg": {k: statistics.mean(v) for k, v in dur.items()},
            "k_scan_filter_ms_avg": statistics.mean(filt) if filt else None, "k_scan_filter_launches": len(filt),
            "k_scan_sample_ms_avg": statistics.mean(samp) if samp else None}
+    p = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
+    if os.path.exists(p):  # MFMA pipe busy fraction of the FILTER launches
+        shutil.copy(p, f"profiles/{tag}_pmc_mfma.csv")
+        per = {}
+        for r in rows(p):
+            if r["Kernel_Name"] != "k_scan":
+                continue
+            per.setdefault(r.get("Dispatch_Id") or r.get("Correlation_Id"), {})[r["Counter_Name"]] = float(r["Counter_Value"])
+        busy = [d for d in per.values() if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d]
+        big = [d for d in busy if d["GRBM_GUI_ACTIVE"] > max(x["GRBM_GUI_ACTIVE"] for x in busy) / 4] if busy else []
+        if big:
+            # busy cycles summed over the 1024 SIMDs vs (GUI_ACTIVE / 8 XCDs) cycles x 1024 SIMDs
+            frac = statistics.mean(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8 * 1024) for d in big)
+            out["k_scan_filter_mfma_busy_frac"] = frac
     for name, key in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
         p = os.path.join(src, name, "run_counter_collection.csv")
         if not os.path.exists(p):

@@ -41,7 +41,7 @@ MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (no sparsity), MI355X_MICROARCH.md
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=40)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=10_000_000)
     p.add_argument("--dim", type=int, default=1024)
@@ -59,7 +59,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-TIME_EVERY = 4
+TIME_EVERY = 8
 
 
 def main():
@@ -100,6 +100,8 @@ def main():
         q, _ = synth.planted_queries(args.seed, N, D, B, qseed=1000 + i)
         qs.append(q)
     q_dev = torch.from_numpy(np.stack(qs)).to(dev)
+    q_ready = torch.cuda.Event()  # the queries are resident from here on (lets the search prep them early)
+    q_ready.record()
     s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
     r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
     searcher = ShardedSearch(index, start, max_batch=B, device=dev)
@@ -109,20 +111,20 @@ def main():
     # batch submitted two steps earlier, so host work overlaps the GPU; every batch is fully
     # finalized (fallback included) before the clock stops.
     for i in range(args.warmup):
-        searcher.submit(q_dev[i], K, s_out=s_dev[i], r_out=r_dev[i])
+        searcher.submit(q_dev[i], K, s_out=s_dev[i], r_out=r_dev[i], q_ready=q_ready)
     searcher.finalize_all()
     torch.cuda.synchronize()
     index.take_scan_times()  # drop warmup launches
-    # HIP events around every 4th FILTER launch of the timed region (starting with the first):
-    # each event record leaves a ~6 us bubble on the stream, so timing every launch would
-    # slow the very steps being measured
+    # HIP events around every 8th SAMPLE+FILTER pair of the timed region (starting with the first;
+    # three records: before SAMPLE, between the two, after FILTER): each event record leaves a
+    # ~6 us bubble on the scan stream, so timing every launch would slow the steps being measured
     index.set_scan_timing(TIME_EVERY)
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.warmup, n_batches):
-        searcher.submit(q_dev[i], K, s_out=s_dev[i], r_out=r_dev[i])
+        searcher.submit(q_dev[i], K, s_out=s_dev[i], r_out=r_dev[i], q_ready=q_ready)
     searcher.finalize_all()
     torch.cuda.synchronize()
     if G > 1:

@@ -107,11 +107,21 @@ int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc,
  * scan_stream over all but a few CUs, select + exact rescoring on tail_stream, which waits for
  * the scan by event; the outputs are ready in tail_stream order.  Consecutive calls alternate
  * between two workspaces, so batch i's tail (and whatever the caller queues after it on
- * tail_stream: the all-gather, the merge) overlaps batch i+1's scan.  Same results as
- * hr_index_search_shard. */
+ * tail_stream: the all-gather, the merge) overlaps batch i+1's scan.  Everything the caller
+ * enqueued on scan_stream before the call is ordered before the tail-stream work (the tail waits
+ * for this batch's scan), so outputs written on scan_stream earlier need no extra sync.  Same
+ * results as hr_index_search_shard. */
 int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                                 int64_t row_offset, void* cand_out_dev, double* bound_out_dev, void* scan_stream,
                                 void* tail_stream);
+/* Same, with the event (hipEvent_t, nullable) after which the caller's queries q_dev are ready.
+ * With it, a large shard's query prep and SAMPLE pass run early, on the index's own stream over
+ * the CUs the previous batch's FILTER scan leaves free, instead of between the two FILTER scans
+ * on scan_stream (results identical; only the order of work changes).  Without it: as above. */
+int hr_index_search_shard_async_ev(hr_index* h, const float* q_dev, int B, int k, int kc,
+                                   const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                   double* bound_out_dev, void* scan_stream, void* tail_stream,
+                                   void* q_ready_event);
 int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev /* B */,
                                   int cap, const uint64_t* row_mask_dev, int64_t row_offset,
                                   void* cand_out_dev /* B*cap records */, double* bound_out_dev, void* stream);

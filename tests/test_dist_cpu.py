@@ -64,7 +64,7 @@ def _worker(rank, world, port, result_path):
         def _stream(self):
             return 0
 
-        def _shard_search(self, qt, k, cand, bound, mask_ptr):
+        def _shard_search(self, qt, k, cand, bound, mask_ptr, q_ready=None):
             s, r = oracle.c_search(stored, "bf16", qn[: qt.shape[0]], KC, row_offset=lo, nthreads=1)
             cand.view(torch.int64)[..., 1] = torch.from_numpy(r)
             cand[..., 0] = torch.from_numpy(s)

@@ -185,6 +185,42 @@ def test_dynamic_tail_and_pipelined_workspaces_vs_oracle(native):
     _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(qs[0], "cosine"), k, mask))
 
 
+def test_early_sample_pipelined_vs_oracle(native):
+    """Queries ready by event on a shard large enough (>= 16 sample sizes) for the early SAMPLE:
+    query prep + SAMPLE run on the index's pre stream beside the previous batch's FILTER.  Batches
+    of different shapes (B = 64 / 20 -> 2 / 1 query blocks, k = 10 / 100 -> 1 / 5 row parts, with
+    and without a device row mask) alternate over the two workspaces: all identical to the oracle."""
+    torch = pytest.importorskip("torch")
+    from hiprag.dist import ShardedSearch
+
+    dim, n = 64, 1_100_000
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add_synthetic(23, 0, n)
+    raw = R.gen_rows(23, 0, n, dim)
+    stored = oracle.c_build_synthetic(23, 0, n, dim, "bf16", "cosine")
+    rng = np.random.default_rng(8)
+    allowed = rng.random(n) < 0.6
+    mask_h = oracle.mask_from_bool(allowed)
+    mask_d = torch.from_numpy(mask_h.view(np.int64)).cuda()
+    plan = [(64, 10, False), (64, 10, True), (20, 10, False), (64, 100, False), (64, 10, False), (20, 100, True),
+            (64, 10, False), (64, 10, False)]
+    qs = [np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+          for B, _, _ in plan]
+    q_dev = [torch.from_numpy(q).cuda() for q in qs]
+    outs = [(torch.empty((B, k), dtype=torch.float32, device="cuda"), torch.empty((B, k), dtype=torch.int64, device="cuda"))
+            for B, k, _ in plan]
+    q_ready = torch.cuda.Event()
+    q_ready.record()
+    ss = ShardedSearch(idx, 0, max_batch=64, max_k=100, device=torch.device("cuda", 0))
+    for (B, k, masked), q, (s_o, r_o) in zip(plan, q_dev, outs):
+        ss.submit(q, k, s_out=s_o, r_out=r_o, mask_ptr=mask_d.data_ptr() if masked else 0, q_ready=q_ready)
+    ss.finalize_all()
+    torch.cuda.synchronize()
+    for (B, k, masked), q, (s_o, r_o) in zip(plan, qs, outs):
+        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k, mask_h if masked else None)
+        _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
+
+
 def test_large_k_massive_ties(native):
     """300 identical rows, k = 100: the 100 lowest duplicate rows, via the exact fallback."""
     dim, n = 128, 8000

@@ -20,9 +20,14 @@ for n in sizes:
     idx.add_synthetic(0, 0, n)
     idx.set_scan_timing(1)
     qs = torch.from_numpy(np.stack([synth.planted_queries(0, n, D, B, qseed=i)[0] for i in range(13)])).cuda()
+    q_ready = torch.cuda.Event()
+    q_ready.record()
     ss = ShardedSearch(idx, 0, max_batch=B, overlap=os.environ.get("HIPRAG_OVERLAP", "1") != "0")
     for i in range(3):
         ss.search(qs[i], K)
+    for i in range(3):  # pipelined warmup too (creates the index's pre stream outside the timed pass)
+        ss.submit(qs[i], K, q_ready=q_ready)
+    ss.finalize_all()
     torch.cuda.synchronize()
     idx.take_scan_times()
     cands = []
@@ -34,7 +39,7 @@ for n in sizes:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(3, 13):  # pipelined pass: the timed one
-        ss.submit(qs[i], K)
+        ss.submit(qs[i], K, q_ready=q_ready)
     ss.finalize_all()
     torch.cuda.synchronize()
     step = (time.perf_counter() - t0) / 10 * 1e3

@@ -409,20 +409,50 @@ static double storage_u(const hr_index* h) {
 // tail waits for this batch's FILTER by event; st_tail == st: one stream, the synchronous set.
 static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
                        const double* kth_dev_host /* mode 1: host array of kth, B */, int mode, int cap_out,
-                       Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail) {
+                       Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail,
+                       hipEvent_t q_ready = nullptr) {
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     const int Bp = pl.Bp;
     const bool piped = st_tail != st && mode == 0;
     if (!piped) st_tail = st;
     Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
+    static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
+    const int64_t n_tiles = (h->n + 31) / 32;
+    // SAMPLE size: n_tiles/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
+    static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
+    static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
+    const int64_t s_target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048, n_tiles / (sdiv_env > 0 ? sdiv_env : 128));
+    // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
+    // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
+    // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
+    // large enough (>= 16 sample sizes) for the narrow SAMPLE to finish inside the previous FILTER.
+    static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
+    const bool early = piped && q_ready && early_env && !(dbg & 5) && tail_cus(h) > 0 && n_tiles >= 16 * s_target;
+    hipStream_t sp = st;  // stream of query prep + SAMPLE
+    if (early) {
+        if (!h->pre) {
+            // highest priority: a stream of its own priority class gets its own hardware queue even
+            // when the (GPU_MAX_HW_QUEUES = 4) normal-priority queues are shared by many streams --
+            // sharing one with the scan stream would serialise the early SAMPLE behind the FILTER
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            static const int prio_env = getenv("HIPRAG_PRE_PRIO") ? atoi(getenv("HIPRAG_PRE_PRIO")) : 1;
+            HIP_TRY(hipStreamCreateWithPriority(&h->pre, hipStreamNonBlocking, prio_env ? hi : lo));
+        }
+        sp = h->pre;
+    }
     if (piped) {
         h->flip ^= 1;
         if (!sc.scanned) HIP_TRY(hipEventCreateWithFlags(&sc.scanned, hipEventDisableTiming));
         if (!sc.released) HIP_TRY(hipEventCreateWithFlags(&sc.released, hipEventDisableTiming));
+        if (early && !sc.sampled) HIP_TRY(hipEventCreateWithFlags(&sc.sampled, hipEventDisableTiming));
         // the set's previous batch must be through select/rescore before its buffers are rewritten
-        if (sc.armed) HIP_TRY(hipStreamWaitEvent(st, sc.released, 0));
+        // (skipped when it has already happened -- in the pipelined flow the host finalized that
+        // batch before submitting this one -- a stream wait costs a bubble on the stream)
+        if (sc.armed && hipEventQuery(sc.released) != hipSuccess) HIP_TRY(hipStreamWaitEvent(sp, sc.released, 0));
     }
+    if (early) HIP_TRY(hipStreamWaitEvent(sp, q_ready, 0));  // the caller's queries
     const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
@@ -439,15 +469,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(sc.overflow.ensure((size_t)Bp * 4));
     HIP_TRY(sc.dyn_q.ensure(256));
 
-    static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int MT = mfma_type(h->dtype);
     float* fl = (mode == 0 && !(dbg & 1)) ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
     if (MT == BF16)
-        hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad,
+        hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, sp, q_dev, B, Bp, h->dim, h->dpad,
                            h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
                            sc.mkeys.as<uint32_t>(), np, sc.cnt.as<uint32_t>(), fl, sc.dyn_q.as<uint32_t>());
     else
-        hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
+        hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, sp, q_dev, B, Bp, h->dim, h->dpad, h->S,
                            pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
                            sc.mkeys.as<uint32_t>(), np, sc.cnt.as<uint32_t>(), fl, sc.dyn_q.as<uint32_t>());
     HIP_TRY(hipGetLastError());
@@ -479,14 +508,13 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     }
     // HIPRAG_SCAN_DEBUG (timing experiments only; results are wrong with bits 1/4 set):
     // 1 = no candidate appends, 2 = no threshold refresh, 4 = no sample pass, 8 = refresh never publishes,
-    // 16 = publish with relaxed stores instead of atomicMax
+    // 16 = publish with relaxed stores instead of atomicMax, 32 = the SAMPLE pass publishes nothing
     if (!fl) {
         if (dbg & 1)
             for (auto& f : h->floor_host) f = INFINITY;
         HIP_TRY(hipMemcpyAsync(sc.floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
     }
 
-    const int64_t n_tiles = (h->n + 31) / 32;
     ScanArgs a{};
     a.rows = h->rows;
     a.xnorm = h->metric == L2 ? h->xnorm : nullptr;
@@ -524,23 +552,47 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
                 h->ev_free.pop_back();
             }
             ev.sampled = false;
+            ev.early = early;
         }
         if (groups && !(dbg & 4)) {
-            static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
-            static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
-            const int64_t target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048,
-                                                     n_tiles / (sdiv_env > 0 ? sdiv_env : 128));  // A/B: 128 beats 64 by 0.7 % at 10M
-            a.sample_stride = std::max<int64_t>(1, n_tiles / target);
+            a.sample_stride = std::max<int64_t>(1, n_tiles / s_target);
             a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
-            if (timed) HIP_TRY(hipEventRecord(ev.e[0], st));
-            if (int rc = launch_scan(h, sc, cus, pl, a, SCAN_SAMPLE, st)) return rc;
-            if (timed) HIP_TRY(hipEventRecord(ev.e[1], st));
+            if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
+            const int pub = a.publish;
+            a.publish = (dbg & 32) ? 0 : 1;
+            if (int rc = launch_scan(h, sc, early ? tail_cus(h) : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
+            a.publish = pub;
             ev.sampled = true;
+            if (early) {
+                if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
+                HIP_TRY(hipEventRecord(sc.sampled, sp));
+                HIP_TRY(hipStreamWaitEvent(st, sc.sampled, 0));
+            }
         }
         a.sample_stride = 1;
         a.n_units = n_tiles;
-        if (timed) HIP_TRY(hipEventRecord(ev.e[2], st));
+        // one event between SAMPLE and FILTER ends the one and starts the other (each record is a
+        // ~6 us bubble on the stream)
+        if (timed) HIP_TRY(hipEventRecord(ev.e[1], st));
+        // diagnostics: per-wave stamps of the 10th main FILTER launch, dumped to $HIPRAG_STAMPS
+        static const char* stamp_path = getenv("HIPRAG_STAMPS");
+        static int64_t stamp_launch = 0;
+        const bool stamp = stamp_path && groups && ++stamp_launch == 10;
+        if (stamp) {
+            HIP_TRY(h->stamp_buf.ensure((size_t)4 * 8 * 65536));
+            a.stamps = h->stamp_buf.as<unsigned long long>();
+        }
         if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
+        if (stamp) {
+            a.stamps = nullptr;
+            std::vector<unsigned long long> hs((size_t)4 * sc.last_W);
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMemcpy(hs.data(), h->stamp_buf.p, hs.size() * 8, hipMemcpyDeviceToHost));
+            if (FILE* f = fopen(stamp_path, "wb")) {
+                fwrite(hs.data(), 8, hs.size(), f);
+                fclose(f);
+            }
+        }
         if (timed) {
             HIP_TRY(hipEventRecord(ev.e[3], st));
             h->ev_pending.push_back(ev);
@@ -612,13 +664,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
 }
 
 static int shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
-                        Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail) {
+                        Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail,
+                        hipEvent_t q_ready = nullptr) {
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     for (int b0 = 0; b0 < B; b0 += pl.Bp) {
         const int bc = std::min(pl.Bp, B - b0);
         if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, kc, mask_dev, row_offset, nullptr, 0, 0,
-                                 cand_out + (int64_t)b0 * kc, bound_out + b0, st, st_tail))
+                                 cand_out + (int64_t)b0 * kc, bound_out + b0, st, st_tail, q_ready))
             return rc;
     }
     return HR_OK;
@@ -770,9 +823,10 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
     return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st, st);
 }
 
-extern "C" int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc,
-                                           const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
-                                           double* bound_out_dev, void* scan_stream, void* tail_stream) {
+extern "C" int hr_index_search_shard_async_ev(hr_index* h, const float* q_dev, int B, int k, int kc,
+                                              const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                              double* bound_out_dev, void* scan_stream, void* tail_stream,
+                                              void* q_ready_event) {
     if (!h || !q_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
     if (scan_stream == tail_stream) return set_err(HR_E_INVALID, "scan and tail streams must differ");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -780,7 +834,14 @@ extern "C" int hr_index_search_shard_async(hr_index* h, const float* q_dev, int 
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
     return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev,
-                        (hipStream_t)scan_stream, (hipStream_t)tail_stream);
+                        (hipStream_t)scan_stream, (hipStream_t)tail_stream, (hipEvent_t)q_ready_event);
+}
+
+extern "C" int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc,
+                                           const uint64_t* row_mask_dev, int64_t row_offset, void* cand_out_dev,
+                                           double* bound_out_dev, void* scan_stream, void* tail_stream) {
+    return hr_index_search_shard_async_ev(h, q_dev, B, k, kc, row_mask_dev, row_offset, cand_out_dev, bound_out_dev,
+                                          scan_stream, tail_stream, nullptr);
 }
 
 extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_dev, int cap,
@@ -1014,7 +1075,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
-                      &h->fb_out, &h->stage, &h->exh,
+                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();
@@ -1024,6 +1085,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     for (auto& ev : h->ev_pending)
         for (auto& x : ev.e) (void)hipEventDestroy(x);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->pre) (void)hipStreamDestroy(h->pre);
     delete h;
 }
 
@@ -1035,8 +1097,8 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
         h->ev_pending.pop_front();
         HIP_TRY(hipEventSynchronize(ev.e[3]));
         float a = 0.f, b = 0.f;
-        if (ev.sampled) HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.e[1]));
-        HIP_TRY(hipEventElapsedTime(&b, ev.e[2], ev.e[3]));
+        if (ev.sampled) HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.early ? ev.e[2] : ev.e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ev.e[1], ev.e[3]));
         if (sample_ms) sample_ms[k] = a;
         if (filter_ms) filter_ms[k] = b;
         h->last_sample_ms = a;

@@ -71,6 +71,7 @@ struct Scratch {
     int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
+    hipEvent_t sampled = nullptr;     // pre stream: this set's early query prep + SAMPLE are done
     bool armed = false;               // `released` has been recorded at least once
     void release_all() {
         for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
@@ -78,7 +79,8 @@ struct Scratch {
             b->release();
         if (scanned) (void)hipEventDestroy(scanned);
         if (released) (void)hipEventDestroy(released);
-        scanned = released = nullptr;
+        if (sampled) (void)hipEventDestroy(sampled);
+        scanned = released = sampled = nullptr;
     }
 };
 static constexpr int kSyncSet = 2;
@@ -93,11 +95,12 @@ struct hr_index {
     std::vector<uint32_t> live_host;
     unsigned long long* norm_bits = nullptr;  // device max stored norm² (as double bits)
     hipStream_t stream = nullptr;
+    hipStream_t pre = nullptr;  // early query prep + SAMPLE of pipelined batches (created on first use)
     // per-launch timing of the main (SAMPLE, FILTER) scan pair: events are recorded on the
     // search stream and harvested later, so batches can be pipelined (see hr_index_take_scan_times)
     struct ScanEvents {
-        hipEvent_t e[4];
-        bool sampled;
+        hipEvent_t e[4];  // SAMPLE start, FILTER start (= SAMPLE end unless early), early SAMPLE end, FILTER end
+        bool sampled, early;
     };
     std::vector<ScanEvents> ev_free;
     std::deque<ScanEvents> ev_pending;
@@ -106,6 +109,7 @@ struct hr_index {
     int64_t main_passes = 0;
     int n_cu = 256;
     std::mutex mu;
+    DevBuf stamp_buf;  // diagnostics (HIPRAG_STAMPS)
     // search workspace
     DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, fb_q, fb_out, stage, exh;
     DevBuf ivf_coarse, ivf_probe, ivf_units, ivf_uoff, ivf_out;  // IVF lists search (hr_ivf.hip)

@@ -130,6 +130,11 @@ static __global__ __attribute__((unused)) void k_gen_rows(uint64_t seed, int64_t
 // One wave per (padded) query.  q32: normalised fp32 queries [Bp][dpad] (exact rescoring
 // operand); qfrag: MFMA A-fragments [S][QB][64 lanes][8]; qerr[4b] = ||q - q̂||, [4b+1] = ||q̂||,
 // [4b+2] = |q|^2 (canonical fp64 of the processed query: the euclidean score's first term).
+// One wave per query.  The wave's whole query row is loaded in ONE batch of independent loads
+// (kPrepJ per lane: dim <= 2560) before any arithmetic: the kernel then costs one memory round
+// trip instead of one per unrolled group of the two passes (measured 17 -> ? us per launch at
+// B=64, D=1024).  Arithmetic order is unchanged (canonical: lane-strided fp64 sum + butterfly).
+static constexpr int kPrepJ = 40;  // 40 * 64 = 2560 = the widest query tile the scan's LDS holds
 template <int MT>
 __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int B, int Bp, int dim, int dpad, int S,
                                                 int QB, int metric, float* __restrict__ q32,
@@ -139,6 +144,11 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
+    const bool real = b < B;
+    auto src = [&](int d) -> float { return (real && d < dim) ? q[(int64_t)b * dim + d] : 0.0f; };
+    float v[kPrepJ];
+#pragma unroll
+    for (int j = 0; j < kPrepJ; ++j) v[j] = src(lane + 64 * j);
     // per-batch scratch of this query (replaces two memsets and an H2D copy per batch):
     // group maxima -> -inf, candidate count -> 0, floor -> -inf (+inf for padding rows);
     // floor_q == nullptr: the caller uploaded explicit floors (collect mode)
@@ -147,18 +157,22 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     if (lane == 0) {
         if (dyn_q && b == 0) *dyn_q = 0;
         if (cnt) cnt[b] = 0;
-        if (floor_q) floor_q[b] = b < B ? -__builtin_inff() : __builtin_inff();
+        if (floor_q) floor_q[b] = real ? -__builtin_inff() : __builtin_inff();
     }
-    auto src = [&](int d) -> float { return (b < B && d < dim) ? q[(int64_t)b * dim + d] : 0.0f; };
+    // elements j >= kPrepJ (dim > 2560: IVF lists only) are read in place, in the same order
     double inv = 1.0;
     bool scale = false;
     if (metric == COSINE) {
         double p = 0.0;
-#pragma unroll 8
-        for (int d = lane; d < dim; d += 64) {
-            double x = (double)src(d);
-            p = p + x * x;
-        }
+        auto acc = [&](int d, float xf) {
+            if (d < dim) {
+                const double x = (double)xf;
+                p = p + x * x;
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < kPrepJ; ++j) acc(lane + 64 * j, v[j]);
+        for (int d = lane + 64 * kPrepJ; d < dim; d += 64) acc(d, src(d));
         double n2 = wave_butterfly_sum(p);
         if (n2 > 0.0) {
             inv = 1.0 / __builtin_sqrt(n2);
@@ -167,20 +181,22 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     }
     double e1 = 0.0, nh = 0.0, qn = 0.0;
     const int qb = b >> 5;
-#pragma unroll 8
-    for (int d = lane; d < dpad; d += 64) {
-        float x = src(d);
-        float v = scale ? (float)((double)x * inv) : x;
-        q32[(int64_t)b * dpad + d] = v;
-        uint16_t h = quant_mt<MT>(v);
-        float dq = dequant_mt<MT>(h);
-        int s = d >> 4, sl = (b & 31) + 32 * ((d >> 3) & 1), j = d & 7;
-        qfrag[(((int64_t)s * QB + qb) * 64 + sl) * 8 + j] = h;
-        double e = (double)v - (double)dq;
+    auto put = [&](int d, float x) {
+        const float y = scale ? (float)((double)x * inv) : x;
+        q32[(int64_t)b * dpad + d] = y;
+        const uint16_t h = quant_mt<MT>(y);
+        const float dq = dequant_mt<MT>(h);
+        const int s = d >> 4, sl = (b & 31) + 32 * ((d >> 3) & 1), jj = d & 7;
+        qfrag[(((int64_t)s * QB + qb) * 64 + sl) * 8 + jj] = h;
+        const double e = (double)y - (double)dq;
         e1 += e * e;
         nh += (double)dq * (double)dq;
-        qn = qn + (double)v * (double)v;
-    }
+        qn = qn + (double)y * (double)y;
+    };
+#pragma unroll
+    for (int j = 0; j < kPrepJ; ++j)
+        if (lane + 64 * j < dpad) put(lane + 64 * j, v[j]);
+    for (int d = lane + 64 * kPrepJ; d < dpad; d += 64) put(d, src(d));
     e1 = wave_butterfly_sum(e1);
     nh = wave_butterfly_sum(nh);
     qn = wave_butterfly_sum(qn);
@@ -245,6 +261,8 @@ struct ScanArgs {
     uint32_t* dyn_q;
     // euclidean: approximate score 2 q̂.x - |x|^2 (fp32 |x|^2 per row); nullptr for cosine / ip
     const float* xnorm;
+    // diagnostics (HIPRAG_STAMPS): per-wave wall-clock stamps {entry, staged, end, tiles}, nullable
+    unsigned long long* stamps;
 };
 
 template <int MT>
@@ -344,6 +362,7 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const int64_t u1 = u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
     const int S = a.S;
+    const unsigned long long t_entry = a.stamps ? wall_clock64() : 0ull;
 
     // first loads of the corpus stream go out before the query staging, so their HBM latency
     // overlaps it
@@ -358,6 +377,7 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     // thread (a load->store loop pays one L2 round trip per 8 KiB)
     stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
     __syncthreads();
+    const unsigned long long t_staged = a.stamps ? wall_clock64() : 0ull;
 
     if (u0 >= u1 && FILTER) {
         if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = 0;
@@ -600,7 +620,13 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     }
 
     if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;
-    if (!FILTER) {
+    if (a.stamps && lane == 0) {
+        a.stamps[4 * w] = t_entry;
+        a.stamps[4 * w + 1] = t_staged;
+        a.stamps[4 * w + 2] = wall_clock64();
+        a.stamps[4 * w + 3] = (unsigned long long)done;
+    }
+    if (!FILTER && a.publish) {  // (publish == 0: timing experiments only)
         // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope
         // atomics from 8 XCDs), where same-address atomics serialise, so the workgroup's 8 waves
         // first reduce in LDS (the query tile is no longer needed): one atomic per address per

@@ -40,7 +40,7 @@ EXPORTS = [
     "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
-    "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records",
+    "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev",
 ]
 
 _lib = None
@@ -87,6 +87,7 @@ def load_library(path: str | None = None):
             "hr_index_load": [ctypes.c_char_p, i32, vp, pp],
             "hr_index_search_shard": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp],
             "hr_index_search_shard_async": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp, vp],
+            "hr_index_search_shard_async_ev": [vp, vp, i32, i32, i32, vp, i64, vp, vp, vp, vp, vp],
             "hr_index_add_device_at": [vp, vp, i64, vp, i64, vp],
             "hr_gen_rows_device": [u64, i64, i64, i32, vp, vp],
             "hr_topk_records": [vp, vp, i64, i32, i32, vp, vp],
@@ -244,15 +245,19 @@ class NativeIndex:
                                                ctypes.c_void_p(rows_ptr), ctypes.c_void_p(stream or None)))
 
     def search_shard(self, q_ptr: int, B: int, k: int, kc: int, row_offset: int, cand_ptr: int, bound_ptr: int,
-                     mask_ptr: int = 0, stream: int = 0, tail_stream: int | None = None) -> None:
+                     mask_ptr: int = 0, stream: int = 0, tail_stream: int | None = None,
+                     q_ready_event: int = 0) -> None:
         """Per-shard exact top-kc.  With tail_stream (!= stream) the scan runs on `stream` and
-        select/rescore on `tail_stream` (pipelined; outputs ready in tail_stream order)."""
+        select/rescore on `tail_stream` (pipelined; outputs ready in tail_stream order).
+        q_ready_event (raw hipEvent_t, pipelined only): the queries are ready once it completes,
+        which lets a large shard prep the queries and run its SAMPLE pass early (see hiprag.h)."""
         if tail_stream is not None:
-            _check(self.lib.hr_index_search_shard_async(self._h, ctypes.c_void_p(q_ptr), int(B), int(k), int(kc),
-                                                        ctypes.c_void_p(mask_ptr or None), int(row_offset),
-                                                        ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bound_ptr),
-                                                        ctypes.c_void_p(stream or None),
-                                                        ctypes.c_void_p(tail_stream or None)))
+            _check(self.lib.hr_index_search_shard_async_ev(self._h, ctypes.c_void_p(q_ptr), int(B), int(k), int(kc),
+                                                           ctypes.c_void_p(mask_ptr or None), int(row_offset),
+                                                           ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bound_ptr),
+                                                           ctypes.c_void_p(stream or None),
+                                                           ctypes.c_void_p(tail_stream or None),
+                                                           ctypes.c_void_p(q_ready_event or None)))
             return
         _check(self.lib.hr_index_search_shard(self._h, ctypes.c_void_p(q_ptr), int(B), int(k), int(kc),
                                               ctypes.c_void_p(mask_ptr or None), int(row_offset),

@@ -92,10 +92,12 @@ class ShardedSearch:
                                  s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream(),
                                  cand_rank_stride=cand_all.stride(0) * 8, bound_rank_stride=bound_all.stride(0) * 8)
 
-    def _shard_search(self, q, k, cand, bound, mask_ptr):
+    def _shard_search(self, q, k, cand, bound, mask_ptr, q_ready=None):
         tail = self.tail.cuda_stream if self.tail is not None else None
+        ev = q_ready.cuda_event if (q_ready is not None and tail is not None) else 0
         self.index.search_shard(q.data_ptr(), q.shape[0], k, self.kc, self.row_offset, cand.data_ptr(),
-                                bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream(), tail_stream=tail)
+                                bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream(), tail_stream=tail,
+                                q_ready_event=ev)
 
     def _shard_collect(self, q, kth, cap, cand, bound, mask_ptr):
         self.index.search_shard_collect(q.data_ptr(), q.shape[0], kth.data_ptr(), cap, self.row_offset,
@@ -116,9 +118,12 @@ class ShardedSearch:
                 self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
     # the search
-    def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
+    def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0, q_ready=None):
         """Enqueue one batch; returns a ticket for finalize().  q: (B, dim) float32 device tensor,
-        identical on every rank."""
+        identical on every rank.  q_ready: optional recorded torch.cuda.Event after which q (and
+        the mask) are ready; then a large shard preps the queries and runs its SAMPLE pass beside
+        the previous batch's FILTER scan instead of after it.  Without it the queries are taken to
+        be ready in the current stream's order."""
         torch = self.torch
         B = int(q.shape[0])
         if B > self.max_batch:
@@ -135,10 +140,12 @@ class ShardedSearch:
         L = _record_len(B, self.kc)
         rec = slot.rec[:L]
         cand, bound = _record_views(rec, B, self.kc)
-        self._shard_search(q, k, cand, bound, mask_ptr)
+        self._shard_search(q, k, cand, bound, mask_ptr, q_ready)
         if self.tail is not None:
-            # the caller's writes to s_out/r_out (allocation, earlier use) happen on its stream
-            self.tail.wait_stream(torch.cuda.current_stream(self.device))
+            # The caller's earlier writes to s_out/r_out (allocation, earlier use) were enqueued on its
+            # stream before this batch's FILTER scan, and the native search makes the tail stream wait
+            # for that scan (search_shard with tail_stream), so no torch wait_stream is needed here: its
+            # event record would cost a ~6 us bubble on the scan stream every batch.
             with torch.cuda.stream(self.tail):
                 self._exchange_and_merge(slot, rec, L, B, k, s_out, r_out)
         else:

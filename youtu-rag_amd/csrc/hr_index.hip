@@ -563,7 +563,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             if (int rc = launch_scan(h, sc, early ? tail_cus(h) : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
             a.publish = pub;
             ev.sampled = true;
-            if (early) {
+            if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE
                 if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
                 HIP_TRY(hipEventRecord(sc.sampled, sp));
                 HIP_TRY(hipStreamWaitEvent(st, sc.sampled, 0));

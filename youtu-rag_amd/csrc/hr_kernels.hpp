@@ -265,6 +265,7 @@ struct ScanArgs {
     unsigned long long* stamps;
 };
 
+
 template <int MT>
 __device__ inline f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c) {
     if constexpr (MT == BF16)

@@ -35,7 +35,7 @@ for n in sizes:
         ss.search(qs[i], K)
         cands.append(idx.last_candidates())
     idx.take_scan_times()
-    idx.set_scan_timing(4)
+    idx.set_scan_timing(8)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(3, 13):  # pipelined pass: the timed one

@@ -453,6 +453,23 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         if (sc.armed && hipEventQuery(sc.released) != hipSuccess) HIP_TRY(hipStreamWaitEvent(sp, sc.released, 0));
     }
     if (early) HIP_TRY(hipStreamWaitEvent(sp, q_ready, 0));  // the caller's queries
+    // Early mode on a small shard also runs each workspace's FILTER on a scan stream of its own:
+    // consecutive batches use different workspaces, so batch i+1's FILTER has no dependency on
+    // batch i's and its workgroups take the CUs batch i's FILTER frees during its tail (measured
+    // 0.482 -> 0.462 ms/step at 1.25M rows, 0.873 -> 0.835 at 2.5M, 1.625 -> 1.607 at 5M, no gain
+    // at 10M; A/B: HIPRAG_DUAL_SCAN=0 off, 2 at any size)
+    static const int dual_env = getenv("HIPRAG_DUAL_SCAN") ? atoi(getenv("HIPRAG_DUAL_SCAN")) : 1;
+    const bool dual = early && (dual_env == 2 || (dual_env == 1 && n_tiles <= 160 * 1024));
+    hipStream_t sf = st;  // stream of the FILTER scan
+    if (dual) {
+        if (!sc.scan) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            static const int prio_env = getenv("HIPRAG_SCAN_PRIO") ? atoi(getenv("HIPRAG_SCAN_PRIO")) : 1;
+            HIP_TRY(hipStreamCreateWithPriority(&sc.scan, hipStreamNonBlocking, prio_env ? hi : lo));
+        }
+        sf = sc.scan;
+    }
     const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
@@ -566,14 +583,22 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE
                 if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
                 HIP_TRY(hipEventRecord(sc.sampled, sp));
-                HIP_TRY(hipStreamWaitEvent(st, sc.sampled, 0));
+                HIP_TRY(hipStreamWaitEvent(sf, sc.sampled, 0));
             }
         }
         a.sample_stride = 1;
         a.n_units = n_tiles;
         // one event between SAMPLE and FILTER ends the one and starts the other (each record is a
         // ~6 us bubble on the stream)
-        if (timed) HIP_TRY(hipEventRecord(ev.e[1], st));
+        // dual-stream mode: a timed FILTER waits for the previous FILTER and the FILTER after it waits
+        // for the timed one, so the timed launch's events bracket that launch alone (not the tail of
+        // the launch before it, nor the head of the one after)
+        if (dual && (timed || h->isolate_next)) {
+            const Scratch& other = h->scr[h->flip];  // (flipped above: the previous batch's set)
+            if (other.armed && other.scanned) HIP_TRY(hipStreamWaitEvent(sf, other.scanned, 0));
+        }
+        h->isolate_next = dual && timed;
+        if (timed) HIP_TRY(hipEventRecord(ev.e[1], sf));
         // diagnostics: per-wave stamps of the 10th main FILTER launch, dumped to $HIPRAG_STAMPS
         static const char* stamp_path = getenv("HIPRAG_STAMPS");
         static int64_t stamp_launch = 0;
@@ -582,11 +607,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             HIP_TRY(h->stamp_buf.ensure((size_t)4 * 8 * 65536));
             a.stamps = h->stamp_buf.as<unsigned long long>();
         }
-        if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, st)) return rc;
+        if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, sf)) return rc;
         if (stamp) {
             a.stamps = nullptr;
             std::vector<unsigned long long> hs((size_t)4 * sc.last_W);
-            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipStreamSynchronize(sf));
             HIP_TRY(hipMemcpy(hs.data(), h->stamp_buf.p, hs.size() * 8, hipMemcpyDeviceToHost));
             if (FILE* f = fopen(stamp_path, "wb")) {
                 fwrite(hs.data(), 8, hs.size(), f);
@@ -594,7 +619,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             }
         }
         if (timed) {
-            HIP_TRY(hipEventRecord(ev.e[3], st));
+            HIP_TRY(hipEventRecord(ev.e[3], sf));
             h->ev_pending.push_back(ev);
             while (h->ev_pending.size() > 4096) {  // nobody is harvesting: recycle the oldest
                 h->ev_free.push_back(h->ev_pending.front());
@@ -603,7 +628,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         }
     }
     if (piped) {  // the tail stream picks the batch up once its FILTER is done
-        HIP_TRY(hipEventRecord(sc.scanned, st));
+        HIP_TRY(hipEventRecord(sc.scanned, sf));
         HIP_TRY(hipStreamWaitEvent(st_tail, sc.scanned, 0));
     }
     // select

@@ -72,6 +72,7 @@ struct Scratch {
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
     hipEvent_t sampled = nullptr;     // pre stream: this set's early query prep + SAMPLE are done
+    hipStream_t scan = nullptr;       // early mode: this set's FILTER stream (created on first use)
     bool armed = false;               // `released` has been recorded at least once
     void release_all() {
         for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
@@ -80,6 +81,8 @@ struct Scratch {
         if (scanned) (void)hipEventDestroy(scanned);
         if (released) (void)hipEventDestroy(released);
         if (sampled) (void)hipEventDestroy(sampled);
+        if (scan) (void)hipStreamDestroy(scan);
+        scan = nullptr;
         scanned = released = sampled = nullptr;
     }
 };
@@ -107,6 +110,7 @@ struct hr_index {
     float last_sample_ms = 0.f, last_filter_ms = 0.f;
     int time_every = 0;               // record events around every Nth main pass (0 = never)
     int64_t main_passes = 0;
+    bool isolate_next = false;        // dual-stream mode: the next FILTER waits for a timed one
     int n_cu = 256;
     std::mutex mu;
     DevBuf stamp_buf;  // diagnostics (HIPRAG_STAMPS)

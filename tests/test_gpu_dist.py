@@ -76,3 +76,58 @@ def test_two_ranks_on_one_gpu_match_single_index(tmp_path):
         np.testing.assert_array_equal(got["r"], r_ref)
         np.testing.assert_array_equal(got["s"], s_ref)
     assert (r_ref[5] >= 0).all() and len(set(r_ref[5].tolist())) == K
+
+
+# ---------------------------------------------------------------- early SAMPLE + dual FILTER streams
+NE, DIME, BE, KE, NB = 2_200_000, 64, 64, 10, 5  # 1.1M-row shards: large enough for the early mode
+
+
+def _worker_early(rank, world, port, path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hiprag import _native, synth
+    from hiprag.dist import ShardedSearch
+
+    torch.cuda.set_device(0)
+    lo, hi = NE * rank // world, NE * (rank + 1) // world
+    idx = _native.NativeIndex(DIME, "bf16", "cosine", device=0)
+    idx.reserve(hi - lo)
+    idx.add_synthetic(31, lo, hi - lo)  # the counter-based generator: global rows, any sharding
+    ss = ShardedSearch(idx, lo, max_batch=BE, device=torch.device("cuda", 0))
+    qs = torch.from_numpy(np.stack([synth.planted_queries(31, NE, DIME, BE, qseed=50 + i)[0] for i in range(NB)])).cuda()
+    q_ready = torch.cuda.Event()
+    q_ready.record()
+    s = torch.empty((NB, BE, KE), dtype=torch.float32, device="cuda")
+    r = torch.empty((NB, BE, KE), dtype=torch.int64, device="cuda")
+    for i in range(NB):  # pipelined: batch i+1's prep + SAMPLE beside batch i's FILTER, alternating workspaces
+        ss.submit(qs[i], KE, s_out=s[i], r_out=r[i], q_ready=q_ready)
+    ss.finalize_all()
+    torch.cuda.synchronize()
+    np.savez(f"{path}.{rank}.npz", s=s.cpu().numpy(), r=r.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_early_sample_pipelined_match_oracle(tmp_path):
+    """2 ranks x 1.1M-row shards with queries ready by event: the per-shard early SAMPLE on the pre
+    stream and the dual FILTER streams, then the exchange + merge; every batch identical to the
+    CPU oracle over the whole corpus."""
+    import torch.multiprocessing as mp
+
+    import oracle
+    from hiprag import synth
+    from oracle import ref_numpy as R
+
+    path = str(tmp_path / "res")
+    mp.start_processes(_worker_early, args=(2, _free_port(), path), nprocs=2, join=True, start_method="spawn")
+    stored = oracle.c_build_synthetic(31, 0, NE, DIME, "bf16", "cosine")
+    got = [np.load(f"{path}.{rank}.npz") for rank in range(2)]
+    for i in range(NB):
+        q, _ = synth.planted_queries(31, NE, DIME, BE, qseed=50 + i)
+        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), KE)
+        for g in got:
+            np.testing.assert_array_equal(g["r"][i], r_ref)
+            np.testing.assert_array_equal(g["s"][i], s_ref.astype(np.float32))

@@ -45,6 +45,7 @@ PRESETS = {
 _TORCH_DTYPES = {"float32": "float32", "fp32": "float32", "bfloat16": "bfloat16", "bf16": "bfloat16",
                  "float16": "float16", "fp16": "float16"}
 _K7_DTYPE = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
+_PIN = os.environ.get("HIPRAG_EMBED_PIN", "1") != "0"  # A/B switch for the pinned token staging
 
 
 class HashWordTokenizer:
@@ -168,7 +169,10 @@ class TorchRocmEmbedder(BaseEmbedder):
         torch = self.torch
         inputs = self.tokenizer(list(sentences), padding=True, truncation=True, return_tensors="pt",
                                 max_length=self.max_length, add_special_tokens=True)
-        inputs = {k: v.to(self.device, non_blocking=True) for k, v in inputs.items()}
+        # pinned staging: the H2D copy is then truly asynchronous, so the host tokenises batch i+1
+        # while the GPU runs batch i's forward (a pageable copy waits for the stream to drain)
+        pin = self.device.type == "cuda" and _PIN
+        inputs = {k: (v.pin_memory() if pin else v).to(self.device, non_blocking=True) for k, v in inputs.items()}
         with torch.inference_mode():
             hidden = self.model(**inputs)[0]
             if hidden.dtype != getattr(torch, self.dtype_name):

@@ -83,6 +83,9 @@ int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_t n, const 
  * rows of dimension dim, row-major, to device memory on `stream`. */
 int hr_gen_rows_device(uint64_t seed, int64_t row0, int64_t n, int dim, float* out_dev, void* stream);
 int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n);
+/* Host queries and outputs.  1 <= k <= HR_MAX_K: the scan path.  k > HR_MAX_K (Chroma's n_results
+ * has no cap, chroma_store.py:118-120): an exhaustive exact pass per query (same scores and order,
+ * one corpus pass + one n-row sort per query).  Slots past the live (allowed) rows: -inf / -1. */
 int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
                     int64_t* rows_out);
 int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const uint64_t* row_mask_dev,

@@ -221,6 +221,28 @@ def test_early_sample_pipelined_vs_oracle(native):
         _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
 
 
+@pytest.mark.parametrize("dtype,metric", [("bf16", "cosine"), ("f32", "cosine"), ("f16", "cosine"), ("bf16", "euclidean"), ("bf16", "ip")])
+def test_topk_beyond_max_k_exhaustive(native, dtype, metric):
+    """top_k > HR_MAX_K (Chroma has no n_results cap): the exhaustive exact path, identical to the
+    oracle, with and without a mask, including k beyond the number of allowed rows (-inf / -1).
+    (The synthetic rows are raw-scale: euclidean keeps them unnormalised, so not in f16.)"""
+    dim, n, B = 96, 3000, 5
+    m = "l2" if metric == "euclidean" else metric
+    idx = native.NativeIndex(dim, dtype, metric)
+    idx.add_synthetic(12, 0, n)
+    rng = np.random.default_rng(3)
+    raw = R.gen_rows(12, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, 3, rng), rng.standard_normal((B - 3, dim)).astype(np.float32)])
+    stored = oracle.c_build_synthetic(12, 0, n, dim, dtype, m)
+    qp = R.process_queries(q, m)
+    allowed = rng.random(n) < 0.1  # ~300 allowed rows: k = 500 runs past them
+    for k, mask in ((129, None), (500, None), (500, oracle.mask_from_bool(allowed))):
+        s, r = idx.search(q, k, mask)
+        s_ref, r_ref = oracle.c_search(stored, dtype, qp, k, mask, metric=m)
+        _check(s, r, s_ref, r_ref)
+    assert (r[:, -1] == -1).all()
+
+
 def test_large_k_massive_ties(native):
     """300 identical rows, k = 100: the 100 lowest duplicate rows, via the exact fallback."""
     dim, n = 128, 8000
@@ -307,8 +329,10 @@ def test_empty_small_and_ragged(native):
     idx.remove([0, 1, 2])
     s, r = idx.search(q, 5)
     assert (r == -1).all()
+    s, r = idx.search(q, native.HR_MAX_K + 1)  # no top-k cap (the exhaustive path beyond HR_MAX_K)
+    assert (r == -1).all() and np.isneginf(s).all()
     with pytest.raises(ValueError):
-        idx.search(q, native.HR_MAX_K + 1)
+        idx.search(q, 0)
     with pytest.raises(ValueError):
         idx.search(np.ones((1, 63), np.float32), 5)
 

@@ -109,6 +109,11 @@ def test_store_semantics(tmp_path, c1):
     hits = run(store.search(query_embedding=q.tolist(), top_k=5))
     assert all(c.document_id != "doc_3" for c, _ in hits)
     assert hits[0][0].id == "chunk_45" and abs(hits[0][1] - 1.0) < 1e-5
+    # top_k has no cap (Chroma n_results): beyond HR_MAX_K and beyond the live count
+    many = run(store.search(query_embedding=q.tolist(), top_k=300))
+    assert len(many) == 300 and [c.id for c, _ in many[:5]] == [c.id for c, _ in hits]
+    assert len(run(store.search(query_embedding=q.tolist(), top_k=5000))) == run(store.count())
+    assert run(store.search(query_embedding=q.tolist(), top_k=0)) == []
     run(store.clear())
     assert run(store.count()) == 0 and run(store.search([0.0] * 128)) == []
 

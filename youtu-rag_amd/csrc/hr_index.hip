@@ -804,12 +804,58 @@ extern "C" int hr_index_search_device(hr_index* h, const float* q_dev, int B, in
     return search_device_impl(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
 }
 
+// top-k beyond HR_MAX_K (Chroma's n_results has no cap, chroma_store.py:118-120): the exhaustive
+// exact pass per query -- canonical fp64 score of every live, allowed row + stable radix sort,
+// the same arithmetic and (score desc, row asc) order as the scan path -- written straight into
+// the caller's host arrays.  One corpus pass and one n-row sort per query: for the rare large-k
+// call, not the batched hot path.
+static int search_exact_all_host(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev,
+                                 float* scores_out, int64_t* rows_out, hipStream_t st) {
+    Scratch& sc = h->scr[kSyncSet];
+    const int QB = (B + 31) / 32, Bp = QB * 32;
+    HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
+    HIP_TRY(sc.qfrag.ensure((size_t)h->S * QB * 1024));
+    HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
+    if (mfma_type(h->dtype) == BF16)
+        hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
+                           QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(), nullptr, 1,
+                           nullptr, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
+                           QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(), nullptr, 1,
+                           nullptr, nullptr, nullptr);
+    HIP_TRY(hipGetLastError());
+    std::vector<double> qerr((size_t)Bp * 4);
+    HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
+    const int m = (int)std::min<int64_t>(k, h->n);
+    HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
+    HIP_TRY(h->fb_cand.ensure((size_t)m * sizeof(Cand)));
+    std::vector<Cand> c((size_t)m);
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int b = 0; b < B; ++b) {
+        if (int rc = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
+                                     h->metric, qerr[4 * (size_t)b + 2], h->live, (const uint32_t*)mask_dev, h->n, 0, m,
+                                     h->fb_cand.as<Cand>(), h->exh.p, h->exh.bytes, st))
+            return set_err(rc, "exhaustive exact pass failed");
+        HIP_TRY(hipMemcpyAsync(c.data(), h->fb_cand.p, (size_t)m * sizeof(Cand), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        h->n_exhaustive++;
+        for (int i = 0; i < k; ++i) {
+            const bool v = i < m && c[(size_t)i].row >= 0;
+            scores_out[(int64_t)b * k + i] = v ? (float)c[(size_t)i].score : -INFINITY;
+            rows_out[(int64_t)b * k + i] = v ? c[(size_t)i].row : -1;
+        }
+    }
+    return HR_OK;
+}
+
 extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* row_mask, float* scores_out,
                                int64_t* rows_out) {
     if (!h || !q || !scores_out || !rows_out) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
-    if (int rc = validate_search(h, B, k)) return rc;
+    if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
+    if (k <= 0) return set_err(HR_E_INVALID, "k must be positive");
     hipStream_t st = h->stream;
     if (h->n_live == 0) {  // empty index: reference returns [] (faiss_store.py:143-144)
         for (int64_t i = 0; i < (int64_t)B * k; ++i) {
@@ -822,13 +868,15 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     DevBuf& so = h->stage;
     const size_t words = (size_t)((h->n + 63) / 64);
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t off_r = up((size_t)B * k * 4), off_m = off_r + up((size_t)B * k * 8);
+    const size_t kk = (size_t)std::min(k, HR_MAX_K);  // (k > HR_MAX_K writes the host arrays directly)
+    const size_t off_r = up((size_t)B * kk * 4), off_m = off_r + up((size_t)B * kk * 8);
     HIP_TRY(so.ensure(off_m + (row_mask ? words * 8 : 0)));
     float* s_dev = (float*)so.p;
     int64_t* r_dev = (int64_t*)((uint8_t*)so.p + off_r);
     uint64_t* m_dev = row_mask ? (uint64_t*)((uint8_t*)so.p + off_m) : nullptr;
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     if (row_mask) HIP_TRY(hipMemcpyAsync(m_dev, row_mask, words * 8, hipMemcpyHostToDevice, st));
+    if (k > HR_MAX_K) return search_exact_all_host(h, h->q_in.as<float>(), B, k, m_dev, scores_out, rows_out, st);
     if (int rc = search_device_impl(h, h->q_in.as<float>(), B, k, m_dev, s_dev, r_dev, st)) return rc;
     HIP_TRY(hipMemcpyAsync(scores_out, s_dev, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(rows_out, r_dev, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));

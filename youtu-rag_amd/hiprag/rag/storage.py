@@ -262,9 +262,11 @@ class HipVectorStore(BaseVectorStore):
             return [[] for _ in range(len(q))]
         if q.shape[1] != self.dim:
             raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
-        k = min(int(top_k), _native.HR_MAX_K)
-        if top_k > _native.HR_MAX_K:
-            raise ValueError(f"top_k={top_k} exceeds the HIP path's maximum of {_native.HR_MAX_K}")
+        # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
+        # search takes its exhaustive exact path (same results, one corpus pass per query)
+        if int(top_k) <= 0:
+            return [[] for _ in range(len(q))]
+        k = min(int(top_k), self.count_sync())
         scores, rows = self._index.search(q, k, self._filter_bitmap(filters))
         out = []
         for b in range(len(q)):

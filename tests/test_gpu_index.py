@@ -221,6 +221,35 @@ def test_early_sample_pipelined_vs_oracle(native):
         _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
 
 
+@pytest.mark.parametrize("dtype,metric,k", [("bf16", "cosine", 10), ("bf16", "cosine", 100), ("f32", "cosine", 32),
+                                            ("f16", "cosine", 45), ("bf16", "ip", 45), ("bf16", "l2", 10)])
+def test_selective_filter_tile_list_vs_oracle(native, dtype, metric, k):
+    """Row masks that leave at most half the tiles (a few documents' contiguous chunks; 1 % of the
+    rows at random; a handful of rows; nothing): the scans visit only the listed tiles.  Identical
+    to the oracle, including k > 32 (row parts over the listed tiles) and deleted rows."""
+    dim, n, B = 128, 200_000, 24
+    idx = native.NativeIndex(dim, dtype, metric)
+    idx.add_synthetic(17, 0, n)
+    idx.remove(np.arange(5000, 5100))  # deleted rows inside an allowed range
+    rng = np.random.default_rng(k)
+    raw = R.gen_rows(17, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+    stored = oracle.c_build_synthetic(17, 0, n, dim, dtype, metric)
+    live = np.ones(n, bool)
+    live[5000:5100] = False
+    docs = np.zeros(n, bool)
+    for lo in (4900, 77_777, 150_001):
+        docs[lo:lo + 700] = True
+    few = np.zeros(n, bool)
+    few[rng.choice(n, 7, replace=False)] = True
+    for allowed in (docs, rng.random(n) < 0.01, few, np.zeros(n, bool)):
+        mask = oracle.mask_from_bool(allowed)
+        s, r = idx.search(q, k, mask)
+        s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, metric), k,
+                                       oracle.mask_from_bool(allowed & live), metric=metric)
+        _check(s, r, s_ref, r_ref)
+
+
 @pytest.mark.parametrize("dtype,metric", [("bf16", "cosine"), ("f32", "cosine"), ("f16", "cosine"), ("bf16", "euclidean"), ("bf16", "ip")])
 def test_topk_beyond_max_k_exhaustive(native, dtype, metric):
     """top_k > HR_MAX_K (Chroma has no n_results cap): the exhaustive exact path, identical to the

@@ -1,0 +1,53 @@
+"""Filtered search on one GPU: the host entry point (hr_index_search with a row mask, the
+HipVectorStore path of a where-clause) at 10M x 1024 bf16, B = 64, top-10, for masks of
+different selectivity.  With HIPRAG_TILE_LIST=0 every search scans all tiles (A/B).
+Usage: python tools/bench_filter.py [rows]"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "youtu-rag_amd"), REPO]
+import numpy as np  # noqa: E402
+
+from hiprag import _native, synth  # noqa: E402
+
+
+def mask_from_bool(allowed):
+    pad = (-len(allowed)) % 64
+    return np.packbits(np.concatenate([allowed, np.zeros(pad, bool)]), bitorder="little").view(np.uint64).copy()
+
+
+def main():
+    n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10_000_000
+    D, B, K = 1024, 64, 10
+    idx = _native.NativeIndex(D, "bf16", "cosine")
+    idx.reserve(n)
+    idx.add_synthetic(0, 0, n)
+    q, _ = synth.planted_queries(0, n, D, B, qseed=7)
+    rng = np.random.default_rng(0)
+    cases = {"none": None}
+    doc = np.zeros(n, bool)
+    doc[n // 3:n // 3 + 10_000] = True  # one document's chunks (contiguous rows)
+    cases["1 document (10k rows)"] = doc
+    docs = np.zeros(n, bool)
+    for lo in rng.choice(n - 2000, 50, replace=False):
+        docs[lo:lo + 2000] = True  # 50 documents of 2k chunks
+    cases["50 documents (100k rows)"] = docs
+    cases["1% random rows"] = rng.random(n) < 0.01
+    cases["10% random rows"] = rng.random(n) < 0.10
+    for name, allowed in cases.items():
+        m = None if allowed is None else mask_from_bool(allowed)
+        for _ in range(2):
+            idx.search(q, K, m)
+        t0 = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            idx.search(q, K, m)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        frac = 0.0 if allowed is None else float(np.mean(allowed))
+        print(f"{name:28s} allowed {frac:7.4f}  {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -419,16 +419,20 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
     static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int64_t n_tiles = (h->n + 31) / 32;
-    // SAMPLE size: n_tiles/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
+    // units the scans visit: every tile, or (selective filter) the listed tiles only
+    const bool use_tl = h->tl_n >= 0;
+    const int64_t n_vis = use_tl ? h->tl_n : n_tiles;
+    // SAMPLE size: n_vis/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
     static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
     static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
-    const int64_t s_target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048, n_tiles / (sdiv_env > 0 ? sdiv_env : 128));
+    const int64_t s_target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048, n_vis / (sdiv_env > 0 ? sdiv_env : 128));
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
     // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
     // large enough (>= 16 sample sizes) for the narrow SAMPLE to finish inside the previous FILTER.
     static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
-    const bool early = piped && q_ready && early_env && !(dbg & 5) && tail_cus(h) > 0 && n_tiles >= 16 * s_target;
+    const bool early = piped && q_ready && early_env && !use_tl && !(dbg & 5) && tail_cus(h) > 0 &&
+                       n_tiles >= 16 * s_target;
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -555,7 +559,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
-    if (n_tiles > 0) {
+    a.tile_list = use_tl ? h->tl.as<uint32_t>() : nullptr;
+    if (n_vis > 0) {
         hr_index::ScanEvents ev{};
         // time the main pass only, not fallbacks, and only every time_every-th one: each event
         // record costs a ~6 us bubble between kernels on the stream
@@ -572,8 +577,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             ev.early = early;
         }
         if (groups && !(dbg & 4)) {
-            a.sample_stride = std::max<int64_t>(1, n_tiles / s_target);
-            a.n_units = (n_tiles + a.sample_stride - 1) / a.sample_stride;
+            a.sample_stride = std::max<int64_t>(1, n_vis / s_target);
+            a.n_units = (n_vis + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
             const int pub = a.publish;
             a.publish = (dbg & 32) ? 0 : 1;
@@ -587,7 +592,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             }
         }
         a.sample_stride = 1;
-        a.n_units = n_tiles;
+        a.n_units = n_vis;
         // one event between SAMPLE and FILTER ends the one and starts the other (each record is a
         // ~6 us bubble on the stream)
         // dual-stream mode: a timed FILTER waits for the previous FILTER and the FILTER after it waits
@@ -639,7 +644,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         HIP_TRY(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, sort_cap * 8 + 16));
         sel_attr[h->device & 63] = true;
     }
-    const bool priv = a.private_bufs && n_tiles > 0;
+    const bool priv = a.private_bufs && n_vis > 0;
     hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st_tail, sc.cnt.as<uint32_t>(), sc.buf.as<float2>(),
                        kCap, priv ? sc.pcnt.as<uint32_t>() : nullptr, priv ? sc.pbuf.as<float2>() : nullptr,
                        (int)sc.last_W, kCapW, Bp, sc.mkeys.as<uint32_t>(), np, sc.floor_q.as<float>(), a.use_groups, B, kc_sel,
@@ -877,6 +882,28 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     if (row_mask) HIP_TRY(hipMemcpyAsync(m_dev, row_mask, words * 8, hipMemcpyHostToDevice, st));
     if (k > HR_MAX_K) return search_exact_all_host(h, h->q_in.as<float>(), B, k, m_dev, scores_out, rows_out, st);
+    // Selective filter (kb_file_search's index_type / source where-clauses, kb_search_toolkit.py:530-535):
+    // when at most half the tiles hold a live, allowed row, the scans visit only those tiles -- a
+    // filter that keeps one document's chunks reads that document's tiles, not the whole corpus
+    struct TileListScope {
+        hr_index* h;
+        ~TileListScope() { h->tl_n = -1; }
+    } tl_scope{h};
+    if (row_mask) {
+        const int64_t n_tiles = (h->n + 31) / 32;
+        const uint32_t* mw = (const uint32_t*)row_mask;  // u64 words, little-endian = u32 per tile
+        std::vector<uint32_t>& tl = h->tl_host;
+        tl.clear();
+        for (int64_t t = 0; t < n_tiles; ++t)
+            if (h->live_host[(size_t)t] & mw[t]) tl.push_back((uint32_t)t);
+        static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
+        if (tl_env && (int64_t)tl.size() * 2 <= n_tiles) {
+            HIP_TRY(h->tl.ensure(std::max<size_t>(4, tl.size() * 4)));
+            if (!tl.empty())
+                HIP_TRY(hipMemcpyAsync(h->tl.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st));
+            h->tl_n = (int64_t)tl.size();
+        }
+    }
     if (int rc = search_device_impl(h, h->q_in.as<float>(), B, k, m_dev, s_dev, r_dev, st)) return rc;
     HIP_TRY(hipMemcpyAsync(scores_out, s_dev, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(rows_out, r_dev, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
@@ -1148,7 +1175,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
-                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf,
+                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();

@@ -114,6 +114,11 @@ struct hr_index {
     int n_cu = 256;
     std::mutex mu;
     DevBuf stamp_buf;  // diagnostics (HIPRAG_STAMPS)
+    // tile list of the current selective-filter search (hr_index_search with a row mask that
+    // leaves at most half the tiles): sorted tiles holding a live, allowed row; tl_n < 0 = none
+    DevBuf tl;
+    int64_t tl_n = -1;
+    std::vector<uint32_t> tl_host;
     // search workspace
     DevBuf q_in, cand, bound, kth, fail, fb_cand, fb_bound, fb_q, fb_out, stage, exh;
     DevBuf ivf_coarse, ivf_probe, ivf_units, ivf_uoff, ivf_out;  // IVF lists search (hr_ivf.hip)

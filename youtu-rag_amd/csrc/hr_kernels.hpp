@@ -232,6 +232,9 @@ struct ScanArgs {
     int S;
     int64_t n_units;         // tiles (FILTER) or sample tiles (SAMPLE)
     int64_t sample_stride;   // SAMPLE: tile = unit * stride
+    // optional sorted list of the tiles to visit (a selective row filter: only tiles holding at
+    // least one live, allowed row); unit u then stands for tile_list[u * stride].  nullptr: all tiles
+    const uint32_t* tile_list;
     uint32_t* mkeys;         // [np parts][QB*32 queries][32 groups] group-max keys (a wave access spans 2 lines)
     int np;                  // row parts: group (p, g) = rows of tile part p with row % 32 == g (k > 32)
     int64_t part_tiles;      // tiles per part (part of tile t = t / part_tiles)
@@ -363,13 +366,18 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const int64_t u1 = u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
     const int S = a.S;
+    // tile of unit u (wave-uniform: a scalar load when a tile list is given)
+    auto tile_at = [&](int64_t u) -> int64_t {
+        const int64_t i = u * stride;
+        return a.tile_list ? (int64_t)a.tile_list[i] : i;
+    };
     const unsigned long long t_entry = a.stamps ? wall_clock64() : 0ull;
 
     // first loads of the corpus stream go out before the query staging, so their HBM latency
     // overlaps it
     XFrag<MT, DT> ring[P];
     if (u0 < u1) {
-        const int64_t c0 = (u0 * stride) * S;
+        const int64_t c0 = tile_at(u0) * S;
 #pragma unroll
         for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
     }
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     // With np > 1 parts (top-k beyond 32) the groups are (part, row % 32): 32*np disjoint row sets,
     // so min over all of them bounds the (32*np)-th best score; gkq points at this wave's current
     // part and the other parts sit at scalar offsets (p - part) * pstride.
-    int64_t part = (u0 * stride) / a.part_tiles;
+    int64_t part = (u0 < u1 ? tile_at(u0) : 0) / a.part_tiles;
     int64_t part_end = (part + 1) * a.part_tiles;
     uint32_t* gkq[QB];
 #pragma unroll
@@ -513,8 +521,8 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
             issued = true;
         }
         if (dyn && u + 1 == u_end) pend = grab_resolve(graw);  // this unit's last k-steps prefetch its first unit
-        const int64_t t = u * stride;
-        const int64_t tn = (u + 1 < u_end) ? (u + 1) * stride : (pend >= 0 ? pend * stride : t);
+        const int64_t t = tile_at(u);
+        const int64_t tn = (u + 1 < u_end) ? tile_at(u + 1) : (pend >= 0 ? tile_at(pend) : t);
         if (t >= part_end) {  // wave-uniform; never taken with one part
             if (MODE != SCAN_COLLECT && a.use_groups) flush();
             const int64_t np_ = t / a.part_tiles;

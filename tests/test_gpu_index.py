@@ -185,19 +185,21 @@ def test_dynamic_tail_and_pipelined_workspaces_vs_oracle(native):
     _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(qs[0], "cosine"), k, mask))
 
 
-def test_early_sample_pipelined_vs_oracle(native):
+@pytest.mark.parametrize("metric", ["cosine", "l2"])
+def test_early_sample_pipelined_vs_oracle(native, metric):
     """Queries ready by event on a shard large enough (>= 16 sample sizes) for the early SAMPLE:
-    query prep + SAMPLE run on the index's pre stream beside the previous batch's FILTER.  Batches
-    of different shapes (B = 64 / 20 -> 2 / 1 query blocks, k = 10 / 100 -> 1 / 5 row parts, with
-    and without a device row mask) alternate over the two workspaces: all identical to the oracle."""
+    query prep + SAMPLE run on the index's pre stream beside the previous batch's FILTER, and each
+    workspace's FILTER on its own stream.  Batches of different shapes (B = 64 / 20 -> 2 / 1 query
+    blocks, k = 10 / 100 -> 1 / 5 row parts, with and without a device row mask) alternate over the
+    two workspaces: all identical to the oracle (cosine and euclidean)."""
     torch = pytest.importorskip("torch")
     from hiprag.dist import ShardedSearch
 
     dim, n = 64, 1_100_000
-    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx = native.NativeIndex(dim, "bf16", metric)
     idx.add_synthetic(23, 0, n)
     raw = R.gen_rows(23, 0, n, dim)
-    stored = oracle.c_build_synthetic(23, 0, n, dim, "bf16", "cosine")
+    stored = oracle.c_build_synthetic(23, 0, n, dim, "bf16", metric)
     rng = np.random.default_rng(8)
     allowed = rng.random(n) < 0.6
     mask_h = oracle.mask_from_bool(allowed)
@@ -217,7 +219,8 @@ def test_early_sample_pipelined_vs_oracle(native):
     ss.finalize_all()
     torch.cuda.synchronize()
     for (B, k, masked), q, (s_o, r_o) in zip(plan, qs, outs):
-        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k, mask_h if masked else None)
+        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, metric), k, mask_h if masked else None,
+                                       metric=metric)
         _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
 
 

@@ -180,6 +180,9 @@ int hr_device_count(int* n_out);
 int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out);
 /* Diagnostics: candidates appended by the most recent FILTER scan (sum, max per query). */
 int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query);
+/* Diagnostics: cumulative counters since creation -- out[0] main scan passes, out[1] queries that
+ * failed the exactness guard (collect fallback), out[2] queries answered by the exhaustive pass. */
+int hr_index_stats(hr_index* h, int64_t out[3]);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

@@ -36,6 +36,8 @@ def main():
     cases["50 documents (100k rows)"] = docs
     cases["1% random rows"] = rng.random(n) < 0.01
     cases["10% random rows"] = rng.random(n) < 0.10
+    cases["30% random rows"] = rng.random(n) < 0.30
+    stats = idx.stats()
     for name, allowed in cases.items():
         m = None if allowed is None else mask_from_bool(allowed)
         for _ in range(2):
@@ -45,8 +47,13 @@ def main():
         for _ in range(reps):
             idx.search(q, K, m)
         ms = (time.perf_counter() - t0) / reps * 1e3
-        frac = 0.0 if allowed is None else float(np.mean(allowed))
-        print(f"{name:28s} allowed {frac:7.4f}  {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS", flush=True)
+        frac = 1.0 if allowed is None else float(np.mean(allowed))
+        tot, mx = idx.last_candidates()
+        st0 = stats
+        stats = idx.stats()
+        fails = stats["guard_failures"] - st0["guard_failures"]
+        print(f"{name:28s} allowed {frac:7.4f}  {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS  "
+              f"candidates/query {tot / B:8.0f} (max {mx})  guard failures {fails} / {12 * B}", flush=True)
 
 
 if __name__ == "__main__":

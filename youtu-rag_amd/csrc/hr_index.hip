@@ -758,6 +758,7 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     for (int b = 0; b < B; ++b)
         if (fail[(size_t)b]) failed.push_back(b);
     if (failed.empty()) return HR_OK;
+    h->n_guard_fail += (int64_t)failed.size();
     // exact fallback: ONE collect re-scan of all failing queries (every row with approx >= kth - E,
     // rescored exactly), merged, then scattered back to the failing rows of the outputs
     const int nf = (int)failed.size(), kc2 = kFallbackCap;
@@ -1237,6 +1238,15 @@ extern "C" int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filte
 
 
 // diagnostics: candidates appended by the last FILTER scan (sum and max over queries)
+extern "C" int hr_index_stats(hr_index* h, int64_t out[3]) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    out[0] = h->main_passes;
+    out[1] = h->n_guard_fail;
+    out[2] = h->n_exhaustive;
+    return HR_OK;
+}
+
 extern "C" int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);

@@ -126,6 +126,7 @@ struct hr_index {
     int flip = 0;                     // next ping-pong set of the pipelined path
     const Scratch* last_scr = nullptr;  // set of the most recent FILTER launch (diagnostics)
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
+    int64_t n_guard_fail = 0;         // queries that failed the exactness guard (collect fallback)
     std::vector<float> floor_host;
 };
 

@@ -40,7 +40,7 @@ EXPORTS = [
     "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
-    "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev",
+    "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
 ]
 
 _lib = None
@@ -102,6 +102,7 @@ def load_library(path: str | None = None):
             "hr_device_count": [vp],
             "hr_index_debug_approx": [vp, vp, i32, vp, vp],
             "hr_index_last_candidates": [vp, vp, vp],
+            "hr_index_stats": [vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -284,6 +285,12 @@ class NativeIndex:
         t, m = ctypes.c_int64(0), ctypes.c_int64(0)
         _check(self.lib.hr_index_last_candidates(self._h, ctypes.byref(t), ctypes.byref(m)))
         return t.value, m.value
+
+    def stats(self) -> dict:
+        """Cumulative diagnostics: main scan passes, guard failures (collect fallback), exhaustive passes."""
+        out = (ctypes.c_int64 * 3)()
+        _check(self.lib.hr_index_stats(self._h, out))
+        return {"main_passes": out[0], "guard_failures": out[1], "exhaustive": out[2]}
 
     def set_scan_timing(self, every: int) -> None:
         """Record HIP events around every `every`-th main-pass scan (0 = off, the default)."""

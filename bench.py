@@ -41,8 +41,8 @@ MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (no sparsity), MI355X_MICROARCH.md
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=40)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--rows", type=int, default=10_000_000)
     p.add_argument("--dim", type=int, default=1024)
     p.add_argument("--batch", type=int, default=64)

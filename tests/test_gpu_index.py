@@ -648,3 +648,53 @@ def test_fuzz_vs_oracle(native, case):
     stored = R.process_rows(x, metric, dtype)
     s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, metric), k, mask, metric=metric)
     _check(s, r, s_ref, r_ref)
+
+
+def _fuzz_filter_cases(n_cases=20, seed=77):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_cases):
+        dim = int(rng.choice([17, 64, 130, 384, 1024]))
+        dtype = str(rng.choice(["f32", "bf16", "f16"]))
+        metric = str(rng.choice(["cosine", "ip", "l2"]))
+        B = int(rng.choice([1, 9, 64, 70]))
+        k = int(rng.choice([1, 10, 33, 100, 128, 129, 300]))
+        n = int(rng.integers(2000, 40000))
+        kind = str(rng.choice(["sparse", "docs", "half", "none"]))
+        out.append((i, dim, dtype, metric, B, k, n, kind))
+    return out
+
+
+@pytest.mark.parametrize("case", _fuzz_filter_cases(), ids=lambda c: "-".join(map(str, c)))
+def test_fuzz_filters_and_large_k_vs_oracle(native, case):
+    """Random combinations over the filter paths -- sparse random masks and document ranges
+    (tile lists), dense masks (full scan) -- and k across the scan / exhaustive boundary
+    (k > HR_MAX_K), with deleted rows: ids and bits equal to the oracle."""
+    i, dim, dtype, metric, B, k, n, kind = case
+    rng = np.random.default_rng(1000 + i)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    if metric != "cosine":
+        x *= (0.5 + rng.random((n, 1))).astype(np.float32)
+    idx = native.NativeIndex(dim, dtype, metric)
+    idx.add(x)
+    dead = rng.choice(n, n // 50, replace=False)
+    idx.remove(dead)
+    live = np.ones(n, bool)
+    live[dead] = False
+    allowed = np.ones(n, bool)
+    if kind == "sparse":
+        allowed = rng.random(n) < 0.005
+    elif kind == "docs":
+        allowed = np.zeros(n, bool)
+        for lo in rng.integers(0, n, 3):
+            allowed[lo:lo + int(rng.integers(1, 400))] = True
+    elif kind == "half":
+        allowed = rng.random(n) < 0.5
+    mask = None if kind == "none" else oracle.mask_from_bool(allowed)
+    j = rng.integers(0, n, B)
+    q = (x[j] + 0.1 * rng.standard_normal((B, dim))).astype(np.float32)
+    s, r = idx.search(q, k, mask)
+    stored = R.process_rows(x, metric, dtype)
+    s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, metric), k,
+                                   oracle.mask_from_bool(allowed & live), metric=metric)
+    _check(s, r, s_ref, r_ref)

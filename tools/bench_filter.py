@@ -37,6 +37,7 @@ def main():
     cases["1% random rows"] = rng.random(n) < 0.01
     cases["10% random rows"] = rng.random(n) < 0.10
     cases["30% random rows"] = rng.random(n) < 0.30
+    cases["all rows (mask of ones)"] = np.ones(n, bool)
     stats = idx.stats()
     for name, allowed in cases.items():
         m = None if allowed is None else mask_from_bool(allowed)

@@ -890,15 +890,25 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
         hr_index* h;
         ~TileListScope() { h->tl_n = -1; }
     } tl_scope{h};
-    if (row_mask) {
+    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
+    if (row_mask && tl_env) {
         const int64_t n_tiles = (h->n + 31) / 32;
         const uint32_t* mw = (const uint32_t*)row_mask;  // u64 words, little-endian = u32 per tile
+        const uint32_t* lw = h->live_host.data();
+        // a dense mask (most tiles hold an allowed row) keeps the full scan: decided on every 64th
+        // tile first, so a dense mask costs ~n_tiles/64 host checks, not a full list build
+        int64_t probe = 0, hit = 0;
+        for (int64_t t = 0; t < n_tiles; t += 64, ++probe) hit += (lw[t] & mw[t]) != 0;
         std::vector<uint32_t>& tl = h->tl_host;
         tl.clear();
-        for (int64_t t = 0; t < n_tiles; ++t)
-            if (h->live_host[(size_t)t] & mw[t]) tl.push_back((uint32_t)t);
-        static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
-        if (tl_env && (int64_t)tl.size() * 2 <= n_tiles) {
+        bool use = false;
+        if (hit * 10 <= probe * 7) {  // not dense: build the list, giving up past half the tiles
+            const int64_t limit = n_tiles / 2;
+            for (int64_t t = 0; t < n_tiles && (int64_t)tl.size() <= limit; ++t)
+                if (lw[t] & mw[t]) tl.push_back((uint32_t)t);
+            use = (int64_t)tl.size() <= limit;
+        }
+        if (use) {
             HIP_TRY(h->tl.ensure(std::max<size_t>(4, tl.size() * 4)));
             if (!tl.empty())
                 HIP_TRY(hipMemcpyAsync(h->tl.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st));

@@ -201,11 +201,14 @@ def test_early_sample_pipelined_vs_oracle(native, metric):
     raw = R.gen_rows(23, 0, n, dim)
     stored = oracle.c_build_synthetic(23, 0, n, dim, "bf16", metric)
     rng = np.random.default_rng(8)
-    allowed = rng.random(n) < 0.6
-    mask_h = oracle.mask_from_bool(allowed)
-    mask_d = torch.from_numpy(mask_h.view(np.int64)).cuda()
-    plan = [(64, 10, False), (64, 10, True), (20, 10, False), (64, 100, False), (64, 10, False), (20, 100, True),
-            (64, 10, False), (64, 10, False)]
+    dense = rng.random(n) < 0.6
+    docs = np.zeros(n, bool)  # a few documents' chunks: the device mask builds a tile list
+    for lo in (1000, 500_000, 1_050_000):
+        docs[lo:lo + 3000] = True
+    masks_h = {"dense": oracle.mask_from_bool(dense), "docs": oracle.mask_from_bool(docs)}
+    masks_d = {kk: torch.from_numpy(v.view(np.int64)).cuda() for kk, v in masks_h.items()}
+    plan = [(64, 10, None), (64, 10, "dense"), (20, 10, None), (64, 100, "docs"), (64, 10, "docs"), (20, 100, "dense"),
+            (64, 10, None), (64, 10, "docs"), (64, 10, None)]
     qs = [np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
           for B, _, _ in plan]
     q_dev = [torch.from_numpy(q).cuda() for q in qs]
@@ -214,14 +217,22 @@ def test_early_sample_pipelined_vs_oracle(native, metric):
     q_ready = torch.cuda.Event()
     q_ready.record()
     ss = ShardedSearch(idx, 0, max_batch=64, max_k=100, device=torch.device("cuda", 0))
-    for (B, k, masked), q, (s_o, r_o) in zip(plan, q_dev, outs):
-        ss.submit(q, k, s_out=s_o, r_out=r_o, mask_ptr=mask_d.data_ptr() if masked else 0, q_ready=q_ready)
+    for (B, k, mk), q, (s_o, r_o) in zip(plan, q_dev, outs):
+        ss.submit(q, k, s_out=s_o, r_out=r_o, mask_ptr=masks_d[mk].data_ptr() if mk else 0, q_ready=q_ready)
     ss.finalize_all()
     torch.cuda.synchronize()
-    for (B, k, masked), q, (s_o, r_o) in zip(plan, qs, outs):
-        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, metric), k, mask_h if masked else None,
+    for (B, k, mk), q, (s_o, r_o) in zip(plan, qs, outs):
+        s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, metric), k, masks_h[mk] if mk else None,
                                        metric=metric)
         _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
+    # the synchronous device entry point with the sparse device mask (tile list on the scan stream)
+    s_d = torch.empty((64, 10), dtype=torch.float32, device="cuda")
+    r_d = torch.empty((64, 10), dtype=torch.int64, device="cuda")
+    idx.search_device(q_dev[0].data_ptr(), 64, 10, s_d.data_ptr(), r_d.data_ptr(), mask_ptr=masks_d["docs"].data_ptr(),
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(qs[0], metric), 10, masks_h["docs"], metric=metric)
+    _check(s_d.cpu().numpy(), r_d.cpu().numpy(), s_ref, r_ref)
 
 
 @pytest.mark.parametrize("dtype,metric,k", [("bf16", "cosine", 10), ("bf16", "cosine", 100), ("f32", "cosine", 32),

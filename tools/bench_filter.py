@@ -57,5 +57,44 @@ def main():
               f"candidates/query {tot / B:8.0f} (max {mx})  guard failures {fails} / {12 * B}", flush=True)
 
 
+def pipelined(n=10_000_000):
+    """The same masks through the pipelined device path (ShardedSearch, device mask: the tile list
+    is built on the GPU), 20 batches in flight two deep."""
+    import torch
+
+    from hiprag.dist import ShardedSearch
+
+    D, B, K, nb = 1024, 64, 10, 20
+    idx = _native.NativeIndex(D, "bf16", "cosine")
+    idx.reserve(n)
+    idx.add_synthetic(0, 0, n)
+    qs = torch.from_numpy(np.stack([synth.planted_queries(0, n, D, B, qseed=100 + i)[0] for i in range(nb)])).cuda()
+    ready = torch.cuda.Event()
+    ready.record()
+    ss = ShardedSearch(idx, 0, max_batch=B)
+    rng = np.random.default_rng(1)
+    doc = np.zeros(n, bool)
+    doc[n // 3:n // 3 + 10_000] = True
+    for name, allowed in (("none", None), ("1 document (10k rows)", doc), ("1% random rows", rng.random(n) < 0.01)):
+        mp = 0
+        if allowed is not None:
+            md = torch.from_numpy(mask_from_bool(allowed).view(np.int64)).cuda()
+            mp = md.data_ptr()
+        for i in range(3):
+            ss.submit(qs[i], K, mask_ptr=mp, q_ready=ready)
+        ss.finalize_all()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nb):
+            ss.submit(qs[i], K, mask_ptr=mp, q_ready=ready)
+        ss.finalize_all()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / nb * 1e3
+        print(f"pipelined {name:28s} {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS", flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("PIPELINED") == "1":
+        pipelined(int(float(sys.argv[1])) if len(sys.argv) > 1 else 10_000_000)
+        sys.exit(0)
     main()

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "../../include/hiprag.h"
 #include "hr_common.hpp"
@@ -64,7 +66,35 @@ __global__ void k_take(const uint64_t* __restrict__ keys, const uint32_t* __rest
 
 }  // namespace
 
+namespace {
+// tile t holds at least one live, allowed row
+struct TileAllowed {
+    const uint32_t* live;
+    const uint32_t* mask;
+    __device__ bool operator()(uint32_t t) const { return (live[t] & mask[t]) != 0u; }
+};
+}  // namespace
+
 namespace hr {
+
+// Sorted list of the tiles holding a live, allowed row of a DEVICE row mask (rocPRIM select over
+// tile indices; the count lands in device memory).  The host-mask path builds the same list on the
+// host (hr_index_search); this one serves device masks (pipelined / distributed search).
+size_t tile_list_scratch_bytes(int64_t n_tiles) {
+    size_t tmp = 0;
+    if (rocprim::select(nullptr, tmp, rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (uint32_t*)nullptr,
+                        (size_t)n_tiles, TileAllowed{nullptr, nullptr}) != hipSuccess)
+        tmp = 0;
+    return tmp;
+}
+
+int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles, uint32_t* list, uint32_t* count,
+                    void* scratch, size_t scratch_bytes, hipStream_t st) {
+    return rocprim::select(scratch, scratch_bytes, rocprim::counting_iterator<uint32_t>(0), list, count,
+                           (size_t)n_tiles, TileAllowed{live, mask}, st) == hipSuccess
+               ? HR_OK
+               : HR_E_HIP;
+}
 
 // scratch layout: keys_in, keys_out (8n each), vals_in, vals_out (4n each), radix-sort temp
 size_t exhaustive_scratch_bytes(int64_t n) {

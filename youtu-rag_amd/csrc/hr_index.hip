@@ -419,20 +419,19 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
     static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int64_t n_tiles = (h->n + 31) / 32;
-    // units the scans visit: every tile, or (selective filter) the listed tiles only
-    const bool use_tl = h->tl_n >= 0;
-    const int64_t n_vis = use_tl ? h->tl_n : n_tiles;
-    // SAMPLE size: n_vis/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
+    // SAMPLE size for n units: n/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
     static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
     static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
-    const int64_t s_target = std::max<int64_t>(smin_env > 0 ? smin_env : 2048, n_vis / (sdiv_env > 0 ? sdiv_env : 128));
+    auto sample_target = [&](int64_t n) {
+        return std::max<int64_t>(smin_env > 0 ? smin_env : 2048, n / (sdiv_env > 0 ? sdiv_env : 128));
+    };
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
     // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
     // large enough (>= 16 sample sizes) for the narrow SAMPLE to finish inside the previous FILTER.
     static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
-    const bool early = piped && q_ready && early_env && !use_tl && !(dbg & 5) && tail_cus(h) > 0 &&
-                       n_tiles >= 16 * s_target;
+    const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && tail_cus(h) > 0 &&
+                       n_tiles >= 16 * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -457,6 +456,33 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         if (sc.armed && hipEventQuery(sc.released) != hipSuccess) HIP_TRY(hipStreamWaitEvent(sp, sc.released, 0));
     }
     if (early) HIP_TRY(hipStreamWaitEvent(sp, q_ready, 0));  // the caller's queries
+    // Units the scans visit: every tile, or (selective filter) only the tiles holding a live, allowed
+    // row -- from the host-mask path (hr_index_search built h->tl), or built here for a device mask
+    // (rocPRIM select on the prep stream; the count is read back, so a masked batch costs one host
+    // wait for the prep stream).  A dense mask (more than half the tiles) keeps the full scan.
+    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
+    const uint32_t* tl_ptr = nullptr;
+    int64_t n_vis = n_tiles;
+    if (h->tl_n >= 0) {
+        tl_ptr = h->tl.as<uint32_t>();
+        n_vis = h->tl_n;
+    } else if (h->tl_n == -1 && mask_dev && tl_env && n_tiles > 0) {  // (-2: the host already chose the full scan)
+        HIP_TRY(sc.tl.ensure((size_t)n_tiles * 4 + 64));
+        HIP_TRY(sc.tl_tmp.ensure(std::max<size_t>(64, tile_list_scratch_bytes(n_tiles))));
+        uint32_t* list = sc.tl.as<uint32_t>();
+        uint32_t* cnt_dev = list + n_tiles;
+        if (int rc = build_tile_list(h->live, (const uint32_t*)mask_dev, n_tiles, list, cnt_dev, sc.tl_tmp.p,
+                                     sc.tl_tmp.bytes, sp))
+            return set_err(rc, "tile list build failed");
+        uint32_t cnt_h = 0;
+        HIP_TRY(hipMemcpyAsync(&cnt_h, cnt_dev, 4, hipMemcpyDeviceToHost, sp));
+        HIP_TRY(hipStreamSynchronize(sp));
+        if ((int64_t)cnt_h * 2 <= n_tiles) {
+            tl_ptr = list;
+            n_vis = cnt_h;
+        }
+    }
+    const int64_t s_target = sample_target(n_vis);
     // Early mode on a small shard also runs each workspace's FILTER on a scan stream of its own:
     // consecutive batches use different workspaces, so batch i+1's FILTER has no dependency on
     // batch i's and its workgroups take the CUs batch i's FILTER frees during its tail (measured
@@ -559,7 +585,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
-    a.tile_list = use_tl ? h->tl.as<uint32_t>() : nullptr;
+    a.tile_list = tl_ptr;
     if (n_vis > 0) {
         hr_index::ScanEvents ev{};
         // time the main pass only, not fallbacks, and only every time_every-th one: each event
@@ -908,6 +934,7 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
                 if (lw[t] & mw[t]) tl.push_back((uint32_t)t);
             use = (int64_t)tl.size() <= limit;
         }
+        h->tl_n = -2;  // evaluated on the host: full scan unless the list is used below
         if (use) {
             HIP_TRY(h->tl.ensure(std::max<size_t>(4, tl.size() * 4)));
             if (!tl.empty())

@@ -57,6 +57,9 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
                     const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
                     size_t scratch_bytes, hipStream_t st);
+size_t tile_list_scratch_bytes(int64_t n_tiles);
+int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles, uint32_t* list, uint32_t* count,
+                    void* scratch, size_t scratch_bytes, hipStream_t st);
 }  // namespace hr
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
@@ -67,7 +70,8 @@ static constexpr int kScanThreads = 512;
 // (hr_index_search_shard_async: batch i's select/rescore on the tail stream overlaps batch
 // i+1's scan on the scan stream); a third serves the synchronous and collect paths.
 struct Scratch {
-    DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q;
+    DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q,
+        tl, tl_tmp;  // device-mask tile list (+ its count after the list) and its rocPRIM scratch
     int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
@@ -76,7 +80,7 @@ struct Scratch {
     bool armed = false;               // `released` has been recorded at least once
     void release_all() {
         for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
-                          &overflow, &pbuf, &pcnt, &dyn_q})
+                          &overflow, &pbuf, &pcnt, &dyn_q, &tl, &tl_tmp})
             b->release();
         if (scanned) (void)hipEventDestroy(scanned);
         if (released) (void)hipEventDestroy(released);
@@ -115,7 +119,8 @@ struct hr_index {
     std::mutex mu;
     DevBuf stamp_buf;  // diagnostics (HIPRAG_STAMPS)
     // tile list of the current selective-filter search (hr_index_search with a row mask that
-    // leaves at most half the tiles): sorted tiles holding a live, allowed row; tl_n < 0 = none
+    // leaves at most half the tiles): sorted tiles holding a live, allowed row; tl_n = -1: none
+    // (a device mask builds its own), -2: the host evaluated the mask and chose the full scan
     DevBuf tl;
     int64_t tl_n = -1;
     std::vector<uint32_t> tl_host;

@@ -187,7 +187,7 @@ def test_dynamic_tail_and_pipelined_workspaces_vs_oracle(native):
 
 @pytest.mark.parametrize("metric", ["cosine", "l2"])
 def test_early_sample_pipelined_vs_oracle(native, metric):
-    """Queries ready by event on a shard large enough (>= 16 sample sizes) for the early SAMPLE:
+    """Queries ready by event on a shard large enough (>= 8 sample sizes) for the early SAMPLE:
     query prep + SAMPLE run on the index's pre stream beside the previous batch's FILTER, and each
     workspace's FILTER on its own stream.  Batches of different shapes (B = 64 / 20 -> 2 / 1 query
     blocks, k = 10 / 100 -> 1 / 5 row parts, with and without a device row mask) alternate over the

@@ -428,10 +428,12 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
     // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
-    // large enough (>= 16 sample sizes) for the narrow SAMPLE to finish inside the previous FILTER.
+    // large enough (>= 8 sample sizes, 524k rows) for the narrow SAMPLE to finish inside the previous
+    // FILTER (A/B at 16: 1M x 768 0.355 vs 0.325 ms/step; at 4, 300k-row shards lose 10 %).
     static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
+    static const int early_min = getenv("HIPRAG_EARLY_MIN") ? atoi(getenv("HIPRAG_EARLY_MIN")) : 8;  // A/B
     const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && tail_cus(h) > 0 &&
-                       n_tiles >= 16 * sample_target(n_tiles);
+                       n_tiles >= early_min * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {

@@ -164,6 +164,11 @@ int hr_topk_records(const void* in_dev, const int64_t* seg_off_records_dev, int6
  * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */
 int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,
                       float* out_dev, void* stream);
+/* K8: out = LayerNorm(x + r) * gamma + beta over rows x H (H <= 4096), dtype of x, r, gamma, beta and
+ * out (HR_F32 / HR_BF16 / HR_F16); the encoder layers' residual add + LayerNorm fused
+ * (BertSelfOutput / BertOutput, modeling_bert.py; XLM-R the same).  Ordered on `stream`. */
+int hr_add_layernorm(const void* x_dev, const void* r_dev, const void* gamma_dev, const void* beta_dev, void* out_dev,
+                     int64_t rows, int H, float eps, int dtype, void* stream);
 
 /* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
  * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */

@@ -100,3 +100,37 @@ def test_ingest_split_embed_add_query(tmp_path):
     # persisted once at the end of the bulk ingest; a fresh store serves the same rows
     store2 = HipVectorStore(cfg)
     assert asyncio.run(store2.count()) == n
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("H", [100, 768, 1024, 4096])
+def test_k8_add_layernorm_matches_torch(dt, H):
+    """K8 (hr_add_layernorm) vs PyTorch's add + F.layer_norm: fp32 within 1e-5; bf16 / f16 within one
+    unit in the last place of the dtype, and bit-identical for nearly every element (the statistics
+    are fp32 sums in another order than torch's Welford)."""
+    g = torch.Generator(device="cpu").manual_seed(H)
+    x = (torch.randn((37, H), generator=g) * 3).to(DEV, TD[dt])
+    r = torch.randn((37, H), generator=g).to(DEV, TD[dt])
+    w = (1 + 0.1 * torch.randn(H, generator=g)).to(DEV, TD[dt])
+    b = (0.1 * torch.randn(H, generator=g)).to(DEV, TD[dt])
+    out = _native.add_layernorm(x, r, w, b, 1e-12)
+    ref = torch.nn.functional.layer_norm(x + r, (H,), w, b, 1e-12)
+    torch.cuda.synchronize()
+    if dt == "f32":
+        torch.testing.assert_close(out, ref, rtol=0, atol=1e-5)
+    else:
+        ulp = 2.0 ** (-7 if dt == "bf16" else -10)
+        diff = (out.float() - ref.float()).abs()
+        assert bool((diff <= ulp * ref.float().abs().clamp_min(1.0)).all())
+        assert float((out == ref).float().mean()) > 0.99
+
+
+@pytest.mark.parametrize("dtype,atol", [("float32", 1e-5), ("bfloat16", 2e-2)])
+def test_fused_layernorm_embedder_matches_unfused(dtype, atol):
+    """The embedder with K8 in every encoder layer vs the same seeded model with PyTorch's add +
+    LayerNorm: fp32 to 1e-5; bf16 to the accumulated rounding of 12 layers."""
+    texts = [f"passage {i}: " + " ".join(f"w{(i * 5 + j) % 89}" for j in range(3 + 9 * i)) for i in range(6)]
+    fused = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=4, fused_layernorm=True)
+    plain = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=4, fused_layernorm=False)
+    assert fused.fused_layers == 24 and plain.fused_layers == 0
+    torch.testing.assert_close(fused.encode_passages(texts), plain.encode_passages(texts), rtol=0, atol=atol)

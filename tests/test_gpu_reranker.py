@@ -91,3 +91,17 @@ def test_reranker_scores_order_and_retriever():
     got = asyncio.run(ret.batch_retrieve([query], top_k=5))[0]
     want = asyncio.run(rr.rerank(query, results[:10], top_k=5))
     assert [r.chunk.id for r in got] == [r.chunk.id for r in want]
+
+
+def test_fused_layernorm_reranker_matches_unfused():
+    """Cross-encoder scores with K8 in every XLM-R encoder layer vs PyTorch's add + LayerNorm (fp32)."""
+    from hiprag.rag.rerankers import TorchRocmReranker
+
+    words = [f"w{i}" for i in range(200)]
+    rng = np.random.default_rng(3)
+    texts = [" ".join(rng.choice(words, rng.integers(1, 60))) for _ in range(40)]
+    a = TorchRocmReranker(preset="tiny", dtype="float32", batch_size=16, max_length=64, seed=2, fused_layernorm=True)
+    b = TorchRocmReranker(preset="tiny", dtype="float32", batch_size=16, max_length=64, seed=2, fused_layernorm=False)
+    assert a.fused_layers > 0 and b.fused_layers == 0
+    np.testing.assert_allclose(a.score_pairs(["w1 w2 w9"], [texts])[0].cpu().numpy(),
+                               b.score_pairs(["w1 w2 w9"], [texts])[0].cpu().numpy(), rtol=0, atol=1e-5)

@@ -41,6 +41,7 @@ EXPORTS = [
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
+    "hr_add_layernorm",
 ]
 
 _lib = None
@@ -103,6 +104,7 @@ def load_library(path: str | None = None):
             "hr_index_debug_approx": [vp, vp, i32, vp, vp],
             "hr_index_last_candidates": [vp, vp, vp],
             "hr_index_stats": [vp, vp],
+            "hr_add_layernorm": [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, i32, vp],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -360,3 +362,24 @@ def pool_normalize(hidden_ptr: int, dtype: str, mask_ptr: int, B: int, T: int, H
     _check(load_library().hr_pool_normalize(ctypes.c_void_p(hidden_ptr), DTYPES[dtype], ctypes.c_void_p(mask_ptr),
                                             int(B), int(T), int(H), int(n_instr), ctypes.c_void_p(out_ptr),
                                             ctypes.c_void_p(stream or None)))
+
+
+def add_layernorm(x, r, weight, bias, eps: float):
+    """K8: LayerNorm(x + r) with affine weight/bias over the last dim, one fused HIP kernel (torch
+    tensors on one device, same dtype, contiguous; runs on the current stream)."""
+    import torch
+
+    names = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16"}
+    if x.dtype not in names or r.dtype != x.dtype or weight.dtype != x.dtype or bias.dtype != x.dtype:
+        raise ValueError("add_layernorm: x, r, weight and bias must share one of f32 / bf16 / f16")
+    if x.shape != r.shape or weight.shape != (x.shape[-1],) or bias.shape != (x.shape[-1],):
+        raise ValueError("add_layernorm: shape mismatch")
+    x, r = x.contiguous(), r.contiguous()
+    out = torch.empty_like(x)
+    H = x.shape[-1]
+    _check(load_library().hr_add_layernorm(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(r.data_ptr()),
+                                           ctypes.c_void_p(weight.data_ptr()), ctypes.c_void_p(bias.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), x.numel() // H, H, float(eps),
+                                           DTYPES[names[x.dtype]],
+                                           ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)))
+    return out

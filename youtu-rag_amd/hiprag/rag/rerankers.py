@@ -32,7 +32,7 @@ import numpy as np
 
 from .. import _native
 from .base import BaseReranker, RetrievalResult
-from .rocm_embedder import PRESETS, HashWordTokenizer
+from .rocm_embedder import PRESETS, HashWordTokenizer, fuse_encoder_layers
 
 logger = logging.getLogger(__name__)
 
@@ -82,10 +82,13 @@ class TorchRocmReranker(BaseReranker):
 
     def __init__(self, model_name_or_path: str | None = None, *, model=None, tokenizer=None,
                  preset: str = "bge-reranker-base", batch_size: int = 256, max_length: int = 512, gpu_id: int = 0,
-                 device=None, dtype: str = "bfloat16", seed: int = 0, cache_size: int = 1 << 20, **_ignored):
+                 device=None, dtype: str = "bfloat16", seed: int = 0, cache_size: int = 1 << 20,
+                 fused_layernorm: bool | None = None, **_ignored):
         import torch
 
         self.torch = torch
+        if fused_layernorm is None:
+            fused_layernorm = os.environ.get("HIPRAG_FUSED_LN", "1") != "0"
         self.device = torch.device(device) if device is not None else torch.device("cuda", gpu_id)
         if dtype not in _TORCH_DTYPES:
             raise ValueError(f"dtype must be one of {sorted(_TORCH_DTYPES)}")
@@ -103,6 +106,8 @@ class TorchRocmReranker(BaseReranker):
         self.tokenizer = tokenizer if tokenizer is not None else HashWordTokenizer(
             getattr(getattr(model, "config", None), "vocab_size", 30522))
         self.model = model.to(self.device, self.tdt).eval()
+        # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
+        self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0
         max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
         self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
         self.batch_size = int(batch_size)

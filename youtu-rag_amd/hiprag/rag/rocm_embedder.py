@@ -94,6 +94,28 @@ class HashWordTokenizer:
         return {"input_ids": input_ids, "attention_mask": mask}
 
 
+def _fused_output_forward(self, hidden_states, input_tensor):
+    """BertSelfOutput / BertOutput (and the XLM-R twins) with the residual add + LayerNorm as one
+    HIP kernel (K8); dropout is the identity in eval mode."""
+    ln = self.LayerNorm
+    return _native.add_layernorm(self.dense(hidden_states), input_tensor, ln.weight, ln.bias, ln.eps)
+
+
+def fuse_encoder_layers(model) -> int:
+    """Route every encoder layer's dense -> dropout -> LayerNorm(x + residual) block of a BERT /
+    XLM-R model (modeling_bert.py BertSelfOutput / BertOutput) through K8.  Eval-mode models only.
+    Returns the number of blocks patched."""
+    import types
+
+    n = 0
+    for m in model.modules():
+        if type(m).__name__.endswith(("SelfOutput", "Output")) and hasattr(m, "dense") and hasattr(m, "LayerNorm") \
+                and getattr(m.LayerNorm, "elementwise_affine", True):
+            m.forward = types.MethodType(_fused_output_forward, m)
+            n += 1
+    return n
+
+
 def build_random_bert(preset: str = "bge-large", seed: int = 0, **overrides):
     """Seeded random-init BertModel of a named shape (no weights exist offline)."""
     import torch
@@ -115,10 +137,12 @@ class TorchRocmEmbedder(BaseEmbedder):
     def __init__(self, model_name_or_path: str | None = None, *, model=None, tokenizer=None, preset: str = "bge-large",
                  batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
-                 trust_remote_code: bool = False, **_ignored):
+                 trust_remote_code: bool = False, fused_layernorm: bool | None = None, **_ignored):
         import torch
 
         self.torch = torch
+        if fused_layernorm is None:
+            fused_layernorm = os.environ.get("HIPRAG_FUSED_LN", "1") != "0"
         self.device = torch.device(device) if device is not None else torch.device("cuda", gpu_id)
         if dtype not in _TORCH_DTYPES:
             raise ValueError(f"dtype must be one of {sorted(_TORCH_DTYPES)}")
@@ -140,6 +164,8 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.tokenizer = tokenizer if tokenizer is not None else HashWordTokenizer(
             getattr(getattr(model, "config", None), "vocab_size", 30522))
         self.model = model.to(self.device, tdt).eval()
+        # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
+        self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0
         max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
         self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
         self.batch_size = int(batch_size)

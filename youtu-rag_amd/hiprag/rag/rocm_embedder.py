@@ -210,10 +210,19 @@ class TorchRocmEmbedder(BaseEmbedder):
     def _encode_all(self, texts: list[str], prefix: str, instruction: str):
         torch = self.torch
         texts = [f"{prefix}{t}" for t in texts]
-        parts = [self.encode(texts[i:i + self.batch_size], instruction) for i in range(0, len(texts), self.batch_size)]
-        if not parts:
-            return torch.empty((0, self.dim or 0), dtype=torch.float32, device=self.device)
-        return parts[0] if len(parts) == 1 else torch.cat(parts)
+        if len(texts) <= self.batch_size:  # one batch: the caller's order (padding is the same either way)
+            if not texts:
+                return torch.empty((0, self.dim or 0), dtype=torch.float32, device=self.device)
+            return self.encode(texts, instruction)
+        # several batches: length-sorted (character count as the token-count proxy), so each batch
+        # pads to about its own length instead of the longest text of a random mix; rows are
+        # independent through the encoder, so only the order of the output rows changes back
+        order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
+        parts = [self.encode([texts[j] for j in order[i:i + self.batch_size]], instruction)
+                 for i in range(0, len(texts), self.batch_size)]
+        out = torch.empty((len(texts), parts[0].shape[1]), dtype=torch.float32, device=self.device)
+        out[torch.as_tensor(order, device=self.device)] = torch.cat(parts)
+        return out
 
     def encode_queries(self, queries):
         queries = queries if isinstance(queries, list) else [queries]

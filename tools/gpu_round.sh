@@ -11,4 +11,5 @@ echo "bench rc=$rb"; tail -1 gpurun_out/bench_full.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rs=$?
 echo "smoke rc=$rs"; tail -1 gpurun_out/smoke.log
 [ $rs -ne 0 ] && exit $rs
+[ "${NO_PROFILE:-0}" = 1 ] && exit 0
 bash tools/profile.sh ${1:-r01}

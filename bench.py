@@ -164,7 +164,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic: counter-based corpus generator (hiprag.synth), planted queries q = x_j/|x_j| + 0.05·eps",
-        "config": {"workload": f"{N // 1_000_000}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, row-sharded",
+        "config": {"workload": f"{N / 1e6:g}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, row-sharded",
                    "rows": N, "dim": D, "batch": B, "k": K, "parallelism": f"rowshard{G}"},
         "roofline": {"bound": "hbm", "kernel": "k_scan (FILTER pass)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -180,8 +180,16 @@ def main():
     # tools/summarize_profile.py): FETCH_SIZE x 2 (gfx950 correction) x 1024, per FILTER launch
     import glob
 
-    suffix = f"_{N // 1_000_000}Mx{D}_b{B}_summary.json" if G == 1 else f"_{N // 1_000_000}Mx{D}_b{B}_g{G}_summary.json"
-    summaries = sorted(glob.glob(os.path.join(REPO, "profiles", "r*" + suffix)))
+    # the FILTER launch's workload is the rank's shard, so a profile of that shard size on one GPU
+    # (tools/profile.sh <tag> --rows n) serves every G that cuts the corpus into such shards
+    suffixes = [f"_{N / 1e6:g}Mx{D}_b{B}_summary.json" if G == 1 else f"_{N / 1e6:g}Mx{D}_b{B}_g{G}_summary.json"]
+    if D == 1024:
+        suffixes.append(f"_shard{n_max_local / 1e6:g}M_b{B}_summary.json")
+    summaries = []
+    for suffix in suffixes:
+        summaries = sorted(glob.glob(os.path.join(REPO, "profiles", "r*" + suffix)))
+        if summaries:
+            break
     if summaries and args.dtype == "bf16" and K == 10:
         with open(summaries[-1]) as f:
             prof = json.load(f)

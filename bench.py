@@ -201,6 +201,8 @@ def main():
             result["roofline"]["traffic_unit"] = "GB per launch (HBM read, PMC)"
             result["roofline"]["traffic_source"] = os.path.relpath(summaries[-1], REPO)
             result["roofline"]["profiled_avg_launch_ms"] = round(prof["k_scan_filter_ms_avg"], 4)
+            if prof.get("k_scan_filter_busy_ms_per_launch"):  # overlapping launches (dual FILTER streams)
+                result["roofline"]["profiled_busy_ms_per_launch"] = round(prof["k_scan_filter_busy_ms_per_launch"], 4)
 
     # recall@10 against the oracle's exact answer over the full corpus (rank 0)
     if rank == 0 and not args.no_cpu:

@@ -25,12 +25,33 @@ def main(src, tag, alg_bytes=None):
     dur = {}
     for r in kt:
         dur.setdefault(r["Kernel_Name"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-    scans = sorted(dur.get("k_scan", []))
-    cut = (scans[0] + scans[-1]) / 2 if scans else 0
-    filt = [d for d in dur.get("k_scan", []) if d > cut]
-    samp = [d for d in dur.get("k_scan", []) if d <= cut]
+    # SAMPLE and FILTER are both k_scan: the FILTER runs on n_cu - 32 workgroups, the SAMPLE on 32,
+    # so the larger grid is the FILTER (older traces without grid columns: split by duration)
+    scan_rows = [r for r in kt if r["Kernel_Name"] == "k_scan"]
+    if scan_rows and "Grid_Size_X" in scan_rows[0]:
+        gmax = max(int(r["Grid_Size_X"]) for r in scan_rows)
+        filt_rows = [r for r in scan_rows if int(r["Grid_Size_X"]) == gmax]
+        samp_rows = [r for r in scan_rows if int(r["Grid_Size_X"]) != gmax]
+    else:
+        d = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), i) for i, r in enumerate(scan_rows))
+        cut = (d[0][0] + d[-1][0]) / 2 if d else 0
+        filt_rows = [r for r in scan_rows if int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > cut]
+        samp_rows = [r for r in scan_rows if int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) <= cut]
+    ms = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # noqa: E731
+    filt, samp = [ms(r) for r in filt_rows], [ms(r) for r in samp_rows]
+    # time during which at least one FILTER launch runs, per launch: with the dual FILTER streams
+    # consecutive launches overlap, so this (not the per-launch duration) is the HBM time per launch
+    busy, end = 0, None
+    for s, e in sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in filt_rows):
+        if end is None or s > end:
+            busy += e - s
+            end = e
+        elif e > end:
+            busy += e - end
+            end = e
     out = {"tag": tag, "kernels_ms_avg": {k: statistics.mean(v) for k, v in dur.items()},
            "k_scan_filter_ms_avg": statistics.mean(filt) if filt else None, "k_scan_filter_launches": len(filt),
+           "k_scan_filter_busy_ms_per_launch": busy / 1e6 / len(filt) if filt else None,
            "k_scan_sample_ms_avg": statistics.mean(samp) if samp else None}
     p = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
     if os.path.exists(p):  # MFMA pipe busy fraction of the FILTER launches
@@ -66,6 +87,8 @@ def main(src, tag, alg_bytes=None):
             out["traffic_over_algorithmic"] = out["k_scan_filter_hbm_read_bytes"] / alg_bytes
         if out["k_scan_filter_ms_avg"]:
             out["achieved_GBps_profiled"] = alg_bytes / (out["k_scan_filter_ms_avg"] * 1e-3) / 1e9
+        if out["k_scan_filter_busy_ms_per_launch"]:
+            out["achieved_GBps_profiled_busy"] = alg_bytes / (out["k_scan_filter_busy_ms_per_launch"] * 1e-3) / 1e9
     with open(f"profiles/{tag}_summary.json", "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))

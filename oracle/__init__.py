@@ -48,6 +48,8 @@ def lib():
         L.hro_search.argtypes = [vp, i32, i64, i32, vp, i32, i32, vp, i64, vp, vp, i32, i32]
         L.hro_search_synthetic.argtypes = [u64, i64, i64, i32, i32, i32, vp, i32, i32, vp, vp, i32]
         L.hro_search_synthetic.restype = i32
+        L.hro_search_synthetic_masked.argtypes = [u64, i64, i64, i32, i32, i32, vp, i32, i32, vp, vp, vp, i32]
+        L.hro_search_synthetic_masked.restype = i32
         L.hro_score_pairs.argtypes = [vp, i32, i32, vp, vp, vp, i64, vp, i32]
         L.hro_norm2.argtypes = [vp, i32]
         L.hro_norm2.restype = ctypes.c_double
@@ -111,13 +113,22 @@ def c_search(stored: np.ndarray, dtype: str, q: np.ndarray, k: int, mask: np.nda
 
 
 def c_search_synthetic(seed: int, row0: int, n: int, dim: int, dtype: str, metric: str, q: np.ndarray, k: int,
-                       nthreads: int | None = None):
+                       nthreads: int | None = None, mask: np.ndarray | None = None):
+    """Exact top-k over the synthetic rows [row0, row0 + n), generated on the fly; ``mask`` (optional
+    uint64 bitmap, bit r = row row0 + r) restricts the search to the allowed rows."""
     q = np.ascontiguousarray(q, np.float32)
     B = q.shape[0]
     s = np.empty((B, k), np.float64)
     r = np.empty((B, k), np.int64)
-    rc = lib().hro_search_synthetic(seed, row0, n, dim, DTYPES[dtype], METRICS[metric], _p(q), B, k, _p(s), _p(r),
-                                    nthreads or default_threads())
+    if mask is not None:
+        m = np.ascontiguousarray(mask, np.uint64)
+        if len(m) * 64 < n:
+            raise ValueError("mask shorter than the row range")
+        rc = lib().hro_search_synthetic_masked(seed, row0, n, dim, DTYPES[dtype], METRICS[metric], _p(q), B, k, _p(m),
+                                               _p(s), _p(r), nthreads or default_threads())
+    else:
+        rc = lib().hro_search_synthetic(seed, row0, n, dim, DTYPES[dtype], METRICS[metric], _p(q), B, k, _p(s),
+                                        _p(r), nthreads or default_threads())
     if rc != 0:
         raise ValueError("dim too large for the synthetic oracle")
     return s, r

@@ -364,6 +364,17 @@ int hro_search_synthetic(uint64_t seed, int64_t row0, int64_t n, int dim, int dt
     return 0;
 }
 
+/* The same restricted to the rows whose bit is set in mask (bit r of word r>>6, r relative to row0):
+ * a where-clause bitmap AND the live rows, i.e. a filtered search over a store with tombstones. */
+int hro_search_synthetic_masked(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, int metric,
+                                const float* q, int B, int k, const uint64_t* mask, double* scores_out,
+                                int64_t* rows_out, int nthreads) {
+    if (dim > 4096) return -1;
+    synth_ctx c = {seed, row0, dim, dtype, metric};
+    search_generic(synth_src, &c, n, dim, q, B, k, mask, row0, scores_out, rows_out, nthreads, metric);
+    return 0;
+}
+
 /* Exact canonical scores of explicit (query, row) pairs against stored rows. */
 void hro_score_pairs(const void* stored, int dtype, int dim, const float* q, const int32_t* qidx, const int64_t* rows,
                      int64_t npairs, double* out, int metric) {

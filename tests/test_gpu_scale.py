@@ -1,0 +1,265 @@
+"""GPU parity at the BASELINE.json sizes (configs[1..4]), through the C ABI.
+
+* C3: 10M x 1024 bf16, B = 64 (two batches: planted + isotropic queries), k = 10 and 100, against
+  the oracle's exact search over all 10M rows (generated on the fly by the same counter-based
+  generator).  Isotropic queries are the worst case for exact-id parity (SURVEY §7 hard part 1:
+  top-k gaps shrink with N), so this is where the exactness guard and its collect / exhaustive
+  fallbacks must hold; the guard counters (hr_index_stats) are printed.  Also: the pipelined
+  two-stream path the bench times, and tombstones + a where-clause bitmap at 10M.
+* C2: 1M x 768, f32 and bf16 stores, B = 64, k = 10.
+* C5: one 6.25M-row f16 IVF shard (50M / 8), nlist 8192, nprobe 32, k = 100, against the IVF
+  restatement (FAISS IndexIVFFlat's algorithm, oracle/ref_numpy.ivf_search) evaluated on the rows
+  of the probed lists only.
+Bar: ids identical (score desc, row asc), scores equal to the oracle's fp64 canonical scores cast
+to fp32 (so within the north_star's 1e-5).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import ref_numpy as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from hiprag import _native
+
+    _native.load_library()
+    assert _native.device_count() >= 1, "no HIP device visible"
+    return _native
+
+
+def _check(s_gpu, r_gpu, s_ref, r_ref):
+    np.testing.assert_array_equal(r_gpu, r_ref)
+    valid = r_ref >= 0
+    np.testing.assert_array_equal(s_gpu[valid], s_ref[valid].astype(np.float32))
+    assert np.all(np.isneginf(s_gpu[~valid]))
+
+
+def _queries(seed, n, dim, B, qseed):
+    from hiprag import synth
+
+    planted, _ = synth.planted_queries(seed, n, dim, B, qseed=qseed)
+    iso = np.random.default_rng(qseed + 1).standard_normal((B, dim)).astype(np.float32)
+    return planted, iso
+
+
+# ---------------------------------------------------------------- C3: 10M x 1024 bf16
+N3, D3, SEED3 = 10_000_000, 1024, 0
+
+
+@pytest.fixture(scope="module")
+def c3(native):
+    idx = native.NativeIndex(D3, "bf16", "cosine")
+    idx.reserve(N3)
+    idx.add_synthetic(SEED3, 0, N3)
+    planted, iso = _queries(SEED3, N3, D3, 64, qseed=4242)
+    q = np.concatenate([planted, iso])
+    # one oracle pass over the 10M rows for all 128 queries at k = 100; top-10 is its prefix
+    s_ref, r_ref = oracle.c_search_synthetic(SEED3, 0, N3, D3, "bf16", "cosine", R.process_queries(q, "cosine"), 100)
+    yield idx, q, s_ref, r_ref
+    idx.close()
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_c3_10M_bf16_vs_oracle(c3, k):
+    idx, q, s_ref, r_ref = c3
+    before = idx.stats()
+    s, r = idx.search(q, k)  # 128 queries: two 64-query corpus passes
+    after = idx.stats()
+    print(f"\nC3 10Mx1024 bf16 k={k}: stats {after}, this search: "
+          f"guard failures {after['guard_failures'] - before['guard_failures']}, "
+          f"exhaustive {after['exhaustive'] - before['exhaustive']}")
+    _check(s[:64], r[:64], s_ref[:64, :k], r_ref[:64, :k])    # planted
+    _check(s[64:], r[64:], s_ref[64:, :k], r_ref[64:, :k])    # isotropic
+
+
+def test_c3_pipelined_path_vs_oracle(c3):
+    """The bench's path (ShardedSearch: scan + tail streams, early SAMPLE, two workspaces) on the
+    same 10M rows: planted and isotropic batches alternate, each identical to the oracle."""
+    import torch
+
+    from hiprag.dist import ShardedSearch
+
+    idx, q, s_ref, r_ref = c3
+    k = 10
+    qd = torch.from_numpy(q).cuda().view(2, 64, D3)
+    ready = torch.cuda.Event()
+    ready.record()
+    ss = ShardedSearch(idx, 0, max_batch=64, device=torch.device("cuda", 0))
+    s_out = torch.empty((4, 64, k), dtype=torch.float32, device="cuda")
+    r_out = torch.empty((4, 64, k), dtype=torch.int64, device="cuda")
+    for i in range(4):
+        ss.submit(qd[i % 2], k, s_out=s_out[i], r_out=r_out[i], q_ready=ready)
+    ss.finalize_all()
+    torch.cuda.synchronize()
+    for i in range(4):
+        h = i % 2
+        _check(s_out[i].cpu().numpy(), r_out[i].cpu().numpy(), s_ref[64 * h:64 * (h + 1), :k],
+               r_ref[64 * h:64 * (h + 1), :k])
+
+
+def test_c3_tombstones_and_filter_vs_oracle(c3):
+    """Deleted rows (tombstones) and a where-clause bitmap at 10M: a dense random filter (full scan
+    with the mask fused into the scan) and a few documents' contiguous row ranges (tile list)."""
+    idx, q, _, _ = c3
+    rng = np.random.default_rng(77)
+    dead = np.unique(rng.integers(0, N3, 20_000))
+    idx.remove(dead)
+    live = np.ones(N3, bool)
+    live[dead] = False
+    dense = rng.random(N3) < 0.5
+    docs = np.zeros(N3, bool)
+    for lo in (123_456, 5_000_000, 9_990_000):
+        docs[lo:lo + 10_000] = True
+    qp = q[:64]
+    qn = R.process_queries(qp, "cosine")
+    try:
+        for allowed in (None, dense, docs):
+            m = live if allowed is None else (live & allowed)
+            k = 10
+            s, r = idx.search(qp, k, None if allowed is None else oracle.mask_from_bool(allowed))
+            s_ref, r_ref = oracle.c_search_synthetic(SEED3, 0, N3, D3, "bf16", "cosine", qn, k,
+                                                     mask=oracle.mask_from_bool(m))
+            _check(s, r, s_ref, r_ref)
+    finally:
+        print(f"\nC3 filtered: stats {idx.stats()}")
+
+
+# ---------------------------------------------------------------- C2: 1M x 768, f32 and bf16
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_c2_1M_768_vs_oracle(native, dtype):
+    n, dim, seed = 1_000_000, 768, 11
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    try:
+        idx.add_synthetic(seed, 0, n)
+        planted, iso = _queries(seed, n, dim, 64, qseed=99)
+        q = np.concatenate([planted, iso])
+        s, r = idx.search(q, 10)
+        s_ref, r_ref = oracle.c_search_synthetic(seed, 0, n, dim, dtype, "cosine", R.process_queries(q, "cosine"), 10)
+        print(f"\nC2 1Mx768 {dtype}: stats {idx.stats()}")
+        _check(s, r, s_ref, r_ref)
+    finally:
+        idx.close()
+
+
+# ---------------------------------------------------------------- C5: one 6.25M f16 IVF shard
+def test_c5_ivf_6p25M_shard_vs_oracle(native):
+    """nlist 8192, nprobe 32, k = 100 over the 6.25M rows one of 8 GPUs holds of the 50M corpus.
+    The oracle restates IndexIVFFlat: exact coarse scores of every centroid (canonical fp64 over the
+    index's fp32 centroids), the nprobe best lists (score desc, list asc), then the exact top-k of
+    the rows of those lists (score desc, id asc) -- evaluated here on those rows only."""
+    import torch
+
+    from hiprag import synth
+    from hiprag.ivf import IvfIndex
+
+    n, dim, nlist, nprobe, k, seed, row0 = 6_250_000, 1024, 8192, 32, 100, 5, 12_500_000
+    ivf = IvfIndex(dim, nlist, dtype="f16")
+    try:
+        sample = torch.empty((nlist * 16, dim), dtype=torch.float32, device="cuda")
+        native.gen_rows_device(seed, row0, nlist * 16, dim, sample.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream)
+        ivf.train(sample, iters=4, seed=0)
+        del sample
+        ivf.build_synthetic(seed, row0, n)
+        rng = np.random.default_rng(7)
+        x = synth.corpus_rows(seed, row0 + rng.choice(n, 8, replace=False), dim)
+        eps = rng.standard_normal(x.shape).astype(np.float32)
+        planted = x / np.linalg.norm(x, axis=1, keepdims=True) + 0.05 * eps / np.linalg.norm(eps, axis=1, keepdims=True)
+        iso = rng.standard_normal((8, dim)).astype(np.float32)
+        q = np.concatenate([planted, iso]).astype(np.float32)
+        B = len(q)
+        qd = torch.from_numpy(q).cuda()
+        cand = torch.empty((B, k, 2), dtype=torch.float64, device="cuda")
+        bound = torch.empty(B, dtype=torch.float64, device="cuda")
+        probes = torch.empty((B, nprobe, 2), dtype=torch.float64, device="cuda")
+        ivf.search_candidates(qd, k, nprobe, cand, bound, probes=probes)
+        torch.cuda.synchronize()
+        got_probe = probes.view(torch.int64)[..., 1].cpu().numpy()
+        got_ids = cand.view(torch.int64)[..., 1].cpu().numpy()
+        got_s = cand[..., 0].cpu().numpy()
+        # coarse stage: canonical fp64 scores of every centroid
+        qn = R.process_queries(q, "cosine")
+        cent = ivf.centroids[:, :dim].cpu().numpy()
+        lists = np.arange(nlist)
+        members = ivf.list_members()
+        for b in range(B):
+            coarse = R.canon_sum(qn[b].astype(np.float64)[None, :] * cent.astype(np.float64))
+            p_ref = lists[np.lexsort((lists, -coarse))][:nprobe]
+            np.testing.assert_array_equal(got_probe[b], p_ref)
+            ids = np.sort(np.concatenate([members[l] for l in p_ref]))
+            stored = R.process_rows(synth.corpus_rows(seed, ids, dim), "cosine", "f16")
+            s_ref, r_ref = oracle.c_search(stored, "f16", qn[b:b + 1], k)
+            ok = r_ref[0] >= 0
+            np.testing.assert_array_equal(got_ids[b][ok], ids[r_ref[0][ok]])
+            assert np.all(got_ids[b][~ok] == -1)
+            np.testing.assert_array_equal(got_s[b][ok], s_ref[0][ok])
+        assert torch.all(torch.isneginf(bound))
+    finally:
+        ivf.close()
+
+
+# ---------------------------------------------------------------- C4: 100k-chunk ingest -> query
+def test_c4_100k_chunk_ingest_then_retrieve(tmp_path):
+    """BASELINE configs[3]: split -> in-process embed -> hr_index_add_device for 100k chunks, then
+    queries through the reference retriever API.  Stored rows are bit-equal to the oracle's bf16
+    quantisation of the vectors the embedder produced; retrieval ids are identical to the oracle's
+    exact search over them; re-ingesting a document replaces its chunks (processors.py:364-418)."""
+    import asyncio
+    import time
+
+    import torch
+
+    from hiprag.rag import BatchedVectorRetriever, ChunkingConfig, Document, HipVectorStore, RetrieverConfig, \
+        VectorStoreConfig
+    from hiprag.rag.ingest import GpuIngestor
+    from hiprag.rag.rocm_embedder import TorchRocmEmbedder
+
+    emb = TorchRocmEmbedder(preset="tiny", batch_size=512, max_length=64, seed=2)
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb100k", persist_directory=str(tmp_path),
+                            index_params={"dtype": "bf16", "persist": True})
+    store = HipVectorStore(cfg)
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20))
+    seen = []
+    inner = emb.embed_texts_device
+    emb.embed_texts_device = lambda texts: seen.append(inner(texts)) or seen[-1]
+    rng = np.random.default_rng(3)
+    words = np.array([f"t{i}" for i in range(5000)])
+    n_docs, sents = 2000, 260  # ~54 chunks of <= 200 chars per document
+    docs = [Document(id=f"d{d}", content=". ".join(" ".join(rng.choice(words, 6)) for _ in range(sents)),
+                     metadata={"source": f"s{d % 17}"}) for d in range(n_docs)]
+    t0 = time.time()
+    n = asyncio.run(ing.ingest(docs))
+    print(f"\nC4 ingest: {n} chunks in {time.time() - t0:.1f}s")
+    assert n >= 100_000 and asyncio.run(store.count()) == n
+    vecs = torch.cat(seen).cpu().numpy()
+    assert len(vecs) == n
+    stored = store._index.get_rows(np.arange(n))
+    expect = R.process_rows(vecs, "cosine", "bf16")
+    np.testing.assert_array_equal(stored, R.dequantize(expect, "bf16"))
+    ids = [r["id"] for r in store._records]
+    queries = [" ".join(rng.choice(words, 5)) for _ in range(16)]
+    retr = BatchedVectorRetriever(store, emb, RetrieverConfig(top_k=10, similarity_threshold=0.0))
+    got = asyncio.run(retr.batch_retrieve(queries, top_k=10))
+    qv = R.process_queries(emb.encode_queries(queries).cpu().numpy(), "cosine")
+    s_ref, r_ref = oracle.c_search(expect, "bf16", qv, 10)
+    assert [[x.chunk.id for x in res] for res in got] == [[ids[j] for j in rr] for rr in r_ref]
+    for res, sr in zip(got, s_ref):
+        np.testing.assert_array_equal(np.float32([x.score for x in res]), sr.astype(np.float32))
+    # re-ingest one document: its old chunks are tombstoned, the new ones appended
+    new = Document(id="d5", content="completely different text about t1 t2 t3. " * 20, metadata={"source": "new"})
+    old_rows = [store._id_to_row[i] for i in ids if i.startswith("d5_chunk_")]
+    n_new = asyncio.run(ing.chunk_and_store(new))
+    assert asyncio.run(store.count()) == n - len(old_rows) + n_new
+    allowed = np.ones(n, bool)
+    allowed[old_rows] = False
+    vec_new = seen[-1].cpu().numpy()
+    all_stored = np.concatenate([expect, R.process_rows(vec_new, "cosine", "bf16")])
+    allowed = np.concatenate([allowed, np.ones(len(vec_new), bool)])
+    got2 = asyncio.run(retr.batch_retrieve(queries[:4], top_k=10))
+    s2, r2 = oracle.c_search(all_stored, "bf16", qv[:4], 10, oracle.mask_from_bool(allowed))
+    ids2 = [r["id"] if r is not None else None for r in store._records]
+    assert [[x.chunk.id for x in res] for res in got2] == [[ids2[j] for j in rr] for rr in r2]

@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU search time the cpu_baseline accumulates")
+    p.add_argument("--cpu-ref-rows", type=int, default=1_000_000, help="row sample of the reference-path CPU baseline")
+    p.add_argument("--cpu-embed-preset", default="bge-large")
     p.add_argument("--recall-queries", type=int, default=4)
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
     return p.parse_args()
@@ -61,6 +63,119 @@ def log(*a):
 
 
 TIME_EVERY = 8
+
+
+def cpu_reference_baseline(args, qbatches, N, D, K, B):
+    """The reference's CPU search path timed on the host cores, on a bounded row sample.
+
+    (b) ``value``: FAISSVectorStore.search over its fp32 store (faiss_store.py:98, :148-154:
+        normalize_L2(query) + IndexFlatIP.search = one sgemm of the query batch against the rows +
+        a top-k selection), restated with numpy's BLAS sgemm + argpartition over 128k-row blocks,
+        a whole 64-query batch per call -- the CPU's best case;
+    (a) ``per_query_loop``: VectorRetriever.batch_retrieve's sequential loop (base_retriever.py:
+        96-98): one sgemv + selection per query, as the reference issues them;
+    ``embed``: the embedding server's encode (deploying-locally.mdx:81-116: tokenise, transformer
+        forward, instruction-masked mean-pool, L2 normalise) of one query per call on the same
+        cores, for the north_star's "CPU embed+search" figure (random-init bge-large, no weights
+        offline).
+    Rows: the synthetic corpus (the same generator), normalised, bf16-quantised like the GPU store,
+    held as fp32 as the reference store holds them.  Scaled by N / sample rows."""
+    import oracle
+    from oracle import ref_numpy as R
+
+    threads = oracle.default_threads()
+    try:
+        from threadpoolctl import threadpool_info
+
+        blas = [{"api": p.get("internal_api"), "threads": p.get("num_threads")} for p in threadpool_info()
+                if p.get("user_api") == "blas"]
+    except Exception:  # noqa: BLE001
+        blas = []
+    S = min(args.cpu_ref_rows, N)
+    x = R.dequantize(oracle.c_build_synthetic(args.seed, 0, S, D, args.dtype, "cosine", threads), args.dtype)
+    blk = 1 << 17
+
+    def search(qn, k):
+        best_s = np.full((len(qn), k), -np.inf, np.float32)
+        best_r = np.full((len(qn), k), -1, np.int64)
+        for r0 in range(0, S, blk):
+            sc = qn @ x[r0:r0 + blk].T                                   # IndexFlatIP: sgemm / sgemv
+            kk = min(k, sc.shape[1])
+            idx = np.argpartition(-sc, kk - 1, axis=1)[:, :kk]
+            all_s = np.concatenate([best_s, np.take_along_axis(sc, idx, 1)], 1)
+            all_r = np.concatenate([best_r, idx + r0], 1)
+            o = np.argsort(-all_s, axis=1, kind="stable")[:, :k]
+            best_s, best_r = np.take_along_axis(all_s, o, 1), np.take_along_axis(all_r, o, 1)
+        return best_s, best_r
+
+    def normalize(q):  # faiss.normalize_L2
+        q = np.asarray(q, np.float32)
+        return q / np.linalg.norm(q, axis=1, keepdims=True)
+
+    search(normalize(qbatches[0][:2]), K)  # warm the BLAS threads
+    dt, nb = 0.0, 0
+    while nb < len(qbatches) and (dt < args.cpu_seconds or nb == 0):
+        t1 = time.perf_counter()
+        search(normalize(qbatches[nb]), K)
+        dt += time.perf_counter() - t1
+        nb += 1
+    qps_b = nb * B / (dt * (N / S))
+    # (a) one query per call
+    nq, ta = 0, 0.0
+    flat = np.concatenate(qbatches[:2])
+    while nq < len(flat) and (ta < args.cpu_seconds / 3 or nq == 0):
+        t1 = time.perf_counter()
+        search(normalize(flat[nq:nq + 1]), K)
+        ta += time.perf_counter() - t1
+        nq += 1
+    qps_a = nq / (ta * (N / S))
+    out = {"value": round(qps_b, 3), "unit": "queries/s", "cores": threads, "kind": "port",
+           "path": "FAISSVectorStore.search semantics (faiss_store.py:148-154: normalize_L2 + IndexFlatIP = sgemm + "
+                   "top-k) over the fp32 store, numpy BLAS",
+           "sample": f"{nb} batches x {B} queries over {S} of the {N} rows ({dt:.2f}s), scaled by {N / S:.1f}x",
+           "blas": blas,
+           "per_query_loop": {"value": round(qps_a, 3), "unit": "queries/s",
+                              "path": "VectorRetriever.batch_retrieve's per-query loop (base_retriever.py:96-98): "
+                                      "one sgemv + top-k per query",
+                              "sample": f"{nq} queries over {S} rows ({ta:.2f}s), scaled by {N / S:.1f}x"}}
+    del x
+    # CPU query embedding (the server's encode on the host cores, one query per call)
+    try:
+        import torch
+
+        from hiprag.rag.rocm_embedder import DEFAULT_QUERY_INSTRUCTION, HashWordTokenizer, build_random_bert
+
+        torch.set_num_threads(threads)
+        model = build_random_bert(args.cpu_embed_preset, seed=0).eval()
+        tok = HashWordTokenizer()
+        instr = f"Instruction: {DEFAULT_QUERY_INSTRUCTION} \nQuery:"
+        n_instr = len(tok(instr, add_special_tokens=True)["input_ids"])
+        queries = [f"what does document {i} say about topic {i % 7} and its retrieval setup" for i in range(6)]
+
+        def encode(q):
+            inp = tok([instr + q], padding=True, truncation=True, max_length=512, return_tensors="pt")
+            with torch.inference_mode():
+                h = model(**inp)[0]
+                m = inp["attention_mask"].clone()
+                m[:, :n_instr] = 0
+                v = (h * m[..., None]).sum(1) / m.sum(1, keepdim=True)
+                return torch.nn.functional.normalize(v, dim=-1)
+
+        encode(queries[0])
+        te, ne = 0.0, 0
+        for q in queries[1:]:
+            t1 = time.perf_counter()
+            encode(q)
+            te += time.perf_counter() - t1
+            ne += 1
+        ms = 1000.0 * te / ne
+        out["embed"] = {"ms_per_query": round(ms, 2), "model": f"{args.cpu_embed_preset} (random init), fp32",
+                        "queries": ne}
+        out["embed_plus_search_per_query_qps"] = round(1.0 / (ms / 1000.0 + 1.0 / qps_a), 4)
+        out["embed_plus_search_batched_qps"] = round(1.0 / (ms / 1000.0 + 1.0 / qps_b), 4)
+    except Exception as e:  # noqa: BLE001
+        out["embed"] = {"error": repr(e)}
+    return out
 
 
 def main():
@@ -227,8 +342,14 @@ def main():
             result["recall_at_10"] = None
             result["recall_error"] = repr(e)
 
-    # CPU baseline: the oracle's exact search on a bounded sample, rank 0, N=1 only
+    # CPU baselines, rank 0, N=1 only: the reference's search path on the host cores (cpu_baseline),
+    # the reference's per-query loop and the CPU query embedding beside it, and the exact fp64 oracle
+    # (the checker, cpu_oracle) -- each on a bounded sample, scaled to the full corpus
     if rank == 0 and G == 1 and not args.no_cpu:
+        try:
+            result["cpu_baseline"] = cpu_reference_baseline(args, qs[args.warmup:], N, D, K, B)
+        except Exception as e:  # report, never hide
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
         try:
             import oracle
             from oracle import ref_numpy as R
@@ -236,23 +357,19 @@ def main():
             S = min(args.cpu_sample_rows, N)
             threads = oracle.default_threads()
             stored = oracle.c_build_synthetic(args.seed, 0, S, D, args.dtype, "cosine", threads)
-            # successive timed batches until >= cpu_seconds of CPU search have accumulated
             dt, nb = 0.0, 0
-            while nb < args.steps and (dt < args.cpu_seconds or nb == 0):
+            while nb < args.steps and (dt < args.cpu_seconds / 2 or nb == 0):
                 qn = R.process_queries(qs[args.warmup + nb], "cosine")
                 t1 = time.perf_counter()
                 oracle.c_search(stored, args.dtype, qn, K, nthreads=threads)
                 dt += time.perf_counter() - t1
                 nb += 1
-            cpu_qps = nb * B / (dt * (N / S))
-            result["cpu_baseline"] = {"value": round(cpu_qps, 4), "unit": "queries/s", "cores": threads,
-                                      "kind": "port",
-                                      "sample": f"oracle exact fp64 search (hr_oracle.c, OpenMP) of {nb} batches x {B} "
-                                                f"queries over {S} of the {N} rows ({dt:.2f}s), scaled by {N / S:.1f}x "
-                                                f"to the full corpus"}
+            result["cpu_oracle"] = {"value": round(nb * B / (dt * (N / S)), 4), "unit": "queries/s", "cores": threads,
+                                    "sample": f"exact fp64 checker (hr_oracle.c, OpenMP) of {nb} batches x {B} queries "
+                                              f"over {S} of the {N} rows ({dt:.2f}s), scaled by {N / S:.1f}x"}
             del stored
         except Exception as e:
-            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+            result["cpu_oracle"] = {"value": None, "error": repr(e)}
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -91,6 +91,8 @@ int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* r
 int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const uint64_t* row_mask_dev,
                            float* scores_out_dev, int64_t* rows_out_dev, void* stream);
 int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out);
+/* Shape of a handle (e.g. one returned by hr_index_load): dim, storage dtype, metric, devices. */
+int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* metric_out, int* n_dev_out);
 int hr_index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out);
 int hr_index_save(hr_index* h, const char* path);
 int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr_index** out);

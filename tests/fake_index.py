@@ -50,3 +50,19 @@ class OracleIndex:
 
     def close(self):
         pass
+
+    # persistence (the C ABI writes <path>.tmp then renames; the fake does the same)
+    def save(self, path):
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, rows=self.rows, live=self.live, dim=self.dim, dtype=self.dtype, metric=self.metric)
+        import os
+
+        os.replace(tmp, path)
+
+    @classmethod
+    def load(cls, path, dim=None, dtype=None, metric=None):
+        with np.load(path, allow_pickle=False) as z:
+            idx = cls(int(z["dim"]), str(z["dtype"]), str(z["metric"]))
+            idx.rows, idx.live = z["rows"].copy(), z["live"].copy()
+        return idx

@@ -1,0 +1,197 @@
+"""CPU: host logic of HipVectorStore that round 1 left O(N) -- incremental crash-safe persistence,
+the predicate-cached where-clause compiler, the search micro-batcher, raw-embedding fidelity.
+The device index is the oracle-backed tests/fake_index.OracleIndex (host-logic tests only)."""
+import asyncio
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fake_index import OracleIndex
+from hiprag.rag import Chunk, HipVectorStore, RetrieverConfig, VectorRetriever, VectorStoreConfig
+from hiprag.rag import filters as F
+from hiprag.rag import persist as P
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def make_store(tmp_path, dtype="f32", **params):
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
+                            index_params={"dtype": dtype, "persist": True, "fsync": False, **params})
+    return HipVectorStore(cfg, index_factory=lambda dim: OracleIndex(dim, dtype),
+                          index_loader=lambda path, dim, dt, metric: OracleIndex.load(path))
+
+
+def chunks(doc, n, dim=16, seed=0, start=0):
+    rng = np.random.default_rng(seed)
+    return [Chunk(id=f"{doc}_chunk_{i}", document_id=doc, content=f"{doc} {i}", chunk_index=i,
+                  metadata={"source": f"src_{doc}", "index_type": "index_content"},
+                  embedding=rng.standard_normal(dim).astype(np.float32).tolist()) for i in range(start, start + n)]
+
+
+def files(tmp_path):
+    return {f: os.path.getsize(os.path.join(tmp_path, f)) for f in os.listdir(tmp_path)}
+
+
+def test_journal_writes_o_chunk_bytes_and_replays(tmp_path):
+    s = make_store(tmp_path)
+    run(s.add_chunks(chunks("d0", 200)))          # first write: generation-1 snapshot
+    f1 = files(tmp_path)
+    assert "kb.manifest.json" in f1 and "kb.g1.hri" in f1
+    run(s.add_chunks(chunks("d1", 10, seed=1)))   # later writes: journal only
+    run(s.add_chunks(chunks("d2", 10, seed=2)))
+    run(s.delete_by_document_id("d0"))
+    f2 = files(tmp_path)
+    assert f2["kb.g1.hri"] == f1["kb.g1.hri"]     # snapshot untouched
+    # two adds of 10 rows x 16 dims + records + one delete of 200 rows: a few KB, not a rewrite
+    assert f2["kb.g1.journal"] < 20_000
+    q = np.random.default_rng(9).standard_normal((3, 16)).astype(np.float32)
+    want = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q, 5)]
+    s2 = make_store(tmp_path)                      # reload = snapshot + journal replay
+    assert run(s2.count()) == run(s.count()) == 20
+    assert [[(c.id, sc) for c, sc in r] for r in s2.search_batch(q, 5)] == want
+    assert run(s2.get_by_id("d0_chunk_3")) is None and run(s2.get_by_id("d1_chunk_3")) is not None
+
+
+def test_torn_journal_tail_is_dropped(tmp_path):
+    s = make_store(tmp_path)
+    run(s.add_chunks(chunks("d0", 5)))
+    run(s.add_chunks(chunks("d1", 5, seed=1)))
+    run(s.add_chunks(chunks("d2", 5, seed=2)))
+    j = os.path.join(tmp_path, "kb.g1.journal")
+    data = open(j, "rb").read()
+    with open(j, "wb") as f:  # a crash in the middle of the last append
+        f.write(data[:-7])
+    s2 = make_store(tmp_path)
+    assert run(s2.count()) == 10 and run(s2.get_by_id("d2_chunk_0")) is None
+    assert os.path.getsize(j) < len(data) - 7  # truncated to the last complete entry
+    run(s2.add_chunks(chunks("d3", 2, seed=3)))  # and appends continue from there
+    assert run(make_store(tmp_path).count()) == 12
+
+
+def test_flush_compacts_and_a_crash_mid_flush_keeps_the_old_generation(tmp_path):
+    s = make_store(tmp_path)
+    run(s.add_chunks(chunks("d0", 20)))
+    run(s.add_chunks(chunks("d1", 20, seed=1)))
+    s.flush()
+    f = files(tmp_path)
+    assert "kb.g2.hri" in f and "kb.g1.hri" not in f and "kb.g1.journal" not in f
+    assert json.load(open(os.path.join(tmp_path, "kb.manifest.json")))["gen"] == 2
+    # a crash after the next generation's data files but before its manifest: the old one is served
+    s._index.save(os.path.join(tmp_path, "kb.g3.hri"))
+    assert run(make_store(tmp_path).count()) == 40
+
+
+def test_row_count_mismatch_refuses_and_header_wins(tmp_path):
+    s = make_store(tmp_path, dtype="bf16")
+    run(s.add_chunks(chunks("d0", 8)))
+    # the files' dtype / metric win over the config's
+    s2 = make_store(tmp_path, dtype="f32")
+    assert s2.dtype == "bf16"
+    rows = os.path.join(tmp_path, "kb.g1.rows.jsonl")
+    lines = open(rows).read().splitlines()
+    with open(rows, "w") as f:
+        f.write("\n".join(lines[:-1]) + "\n")  # one record lost
+    with pytest.raises(RuntimeError):
+        make_store(tmp_path)
+
+
+def test_deferred_block_writes_one_snapshot(tmp_path):
+    s = make_store(tmp_path)
+    run(s.add_chunks(chunks("d0", 4)))
+    with s.deferred_save():
+        for d in range(1, 6):
+            run(s.delete_by_document_id(f"d{d - 1}"))
+            run(s.add_chunks(chunks(f"d{d}", 4, seed=d)))
+    f = files(tmp_path)
+    assert "kb.g2.hri" in f and not any(k.endswith(".journal") for k in f)
+    assert run(make_store(tmp_path).count()) == 4
+
+
+def test_keep_embeddings_returns_the_raw_fp32_vector(tmp_path):
+    s = make_store(tmp_path, dtype="bf16", keep_embeddings=True, include_embeddings=True)
+    cs = chunks("d0", 6)
+    run(s.add_chunks(cs))
+    got = run(s.get_by_id("d0_chunk_2"))
+    assert got.embedding == cs[2].embedding  # chroma_store.py:233-244: the stored fp32 values
+    hit = run(s.search(query_embedding=cs[4].embedding, top_k=1))[0][0]
+    assert hit.id == "d0_chunk_4" and hit.embedding == cs[4].embedding
+    s.flush()
+    s2 = make_store(tmp_path, dtype="bf16", keep_embeddings=True)
+    assert run(s2.get_by_id("d0_chunk_5")).embedding == cs[5].embedding
+
+
+def test_concurrent_retrieves_coalesce_into_one_launch(tmp_path):
+    """64 concurrent VectorRetriever.retrieve calls (the reference's one-query-per-call pattern,
+    base_retriever.py:58-63) give the results of 64 sequential calls with one index search."""
+    s = make_store(tmp_path)
+    run(s.add_chunks(chunks("d0", 500, dim=16)))
+    rng = np.random.default_rng(4)
+    table = {f"q{i}": rng.standard_normal(16).astype(np.float32) for i in range(64)}
+
+    class Emb:
+        async def embed_query(self, q):
+            return table[q].tolist()
+
+    ret = VectorRetriever(s, Emb(), RetrieverConfig(top_k=5, similarity_threshold=0.0))
+    seq = [run(ret.retrieve(q, top_k=3 + i % 5)) for i, q in enumerate(table)]
+    before, launches = s._index.searches, s._batcher.launches
+
+    async def concurrent():
+        return await asyncio.gather(*[ret.retrieve(q, top_k=3 + i % 5) for i, q in enumerate(table)])
+
+    par = run(concurrent())
+    assert s._index.searches - before == 1 and s._batcher.launches - launches == 1
+    assert [[(r.chunk.id, r.score, r.rank) for r in x] for x in par] == [[(r.chunk.id, r.score, r.rank) for r in x]
+                                                                         for x in seq]
+
+    # different filters go to different launches; results still per-call exact
+    async def mixed():
+        return await asyncio.gather(*[s.search(query_embedding=table[q].tolist(), top_k=4,
+                                               filters={"chunk_index": {"$lt": 250}} if i % 2 else None)
+                                      for i, q in enumerate(table)])
+
+    before = s._index.searches
+    res = run(mixed())
+    assert s._index.searches - before == 2
+    for i, r in enumerate(res):
+        if i % 2:
+            assert all(c.chunk_index < 250 for c, _ in r)
+
+
+def test_filter_cache_extends_over_appended_rows():
+    cols = F.MetadataColumns()
+    rng = np.random.default_rng(1)
+    metas = []
+
+    def brute(w):
+        def ok(m):
+            return all((m.get(k) == v and not isinstance(m.get(k), bool)) if not isinstance(v, dict)
+                       else (k in m and m[k] > v["$gt"]) for k, v in w.items())
+        return np.array([ok(m) for m in metas], bool)
+
+    wheres = [{"src": "a"}, {"src": "b", "n": {"$gt": 3}}, {"n": {"$gt": 5}}]
+    for step in range(5):
+        new = [{"src": ["a", "b", "c"][rng.integers(3)], "n": int(rng.integers(10))} if rng.random() < 0.9
+               else {"other": 1} for _ in range(int(rng.integers(1, 200)))]
+        metas.extend(new)
+        cols.append(new)
+        for w in wheres:  # cached after the first step, then extended
+            np.testing.assert_array_equal(F.evaluate(w, cols), brute(w))
+            words = F.evaluate_words(w, cols)
+            assert len(words) == (len(metas) + 63) // 64
+
+
+def test_journal_format_roundtrip(tmp_path):
+    j = P.Journal(str(tmp_path / "x.journal"), fsync=False)
+    v = np.arange(12, dtype=np.float32).reshape(3, 4)
+    j.append_add([{"id": "a"}, None, {"id": "c"}], v)
+    j.append_delete([5, 7])
+    j.close()
+    ops = list(P.Journal.replay(str(tmp_path / "x.journal")))
+    assert ops[0][0] == "add" and ops[0][1] == [{"id": "a"}, None, {"id": "c"}]
+    np.testing.assert_array_equal(ops[0][2], v)
+    assert ops[1][0] == "del" and ops[1][1].tolist() == [5, 7]

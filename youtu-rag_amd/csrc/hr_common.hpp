@@ -96,6 +96,14 @@ __device__ __host__ inline int tile_rot(int64_t t) { return (int)((uint32_t)((ui
 __device__ __host__ inline int row_slot(int64_t r) { return (int)((r + tile_rot(r >> 5)) & 31); }
 __device__ __host__ inline int slot_row(int64_t t, int slot) { return (slot - tile_rot(t)) & 31; }  // row % 32
 
+// Multi-device handles stripe rows over G shards by 32-row tile: handle row H lives in shard
+// (H/32) % G at local row ((H/32)/G)*32 + H%32.  Every shard's rows stay an append-only
+// contiguous range (the tiles of one shard fill in order), and the global row of shard s's local
+// row L is stripe_row(L, G, s) -- G = 1 is the identity.
+__device__ __host__ inline int64_t stripe_row(int64_t L, int G, int s) {
+    return G == 1 ? L : ((((L >> 5) * G) + s) << 5) | (L & 31);
+}
+
 // element (row r, column d) of the tiled corpus, as float
 template <int DT>
 __device__ inline float load_elem(const uint8_t* base, int S, int64_t r, int d) {

@@ -55,11 +55,11 @@ __global__ __launch_bounds__(256) void k_exact_all(const uint8_t* __restrict__ r
 }
 
 __global__ void k_take(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n, int m,
-                       int64_t row_offset, hr::Cand* __restrict__ out) {
+                       int64_t row_offset, int sG, int ss, hr::Cand* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     if (i < n && keys[i] != 0)
-        out[i] = hr::Cand{hr::key2d(keys[i]), (int64_t)vals[i] + row_offset};
+        out[i] = hr::Cand{hr::key2d(keys[i]), hr::stripe_row((int64_t)vals[i], sG, ss) + row_offset};
     else
         out[i] = hr::Cand{-__builtin_inf(), -1};
 }
@@ -106,11 +106,12 @@ size_t exhaustive_scratch_bytes(int64_t n) {
     return up(8 * (size_t)n) * 2 + up(4 * (size_t)n) * 2 + up(tmp);
 }
 
-// exact top-m (score desc, row asc) of query qv over rows [0, n) into out[0..m); empty slots -inf / -1
+// exact top-m (score desc, row asc) of query qv over rows [0, n) into out[0..m); empty slots -inf / -1;
+// returned rows are stripe_row(local row, sG, ss) + row_offset
 int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
                     const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
-                    size_t scratch_bytes, hipStream_t st) {
+                    size_t scratch_bytes, hipStream_t st, int sG, int ss) {
     if (n <= 0 || m <= 0) return HR_E_INVALID;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     uint8_t* p = (uint8_t*)scratch;
@@ -132,7 +133,7 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
     if (rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (size_t)n, 0, 64, st) != hipSuccess)
         return HR_E_HIP;
     hipLaunchKernelGGL(k_take, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, k_out, v_out, n, m, row_offset,
-                       out);
+                       sG, ss, out);
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 

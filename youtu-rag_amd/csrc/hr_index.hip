@@ -17,7 +17,11 @@ extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const 
     if (dim <= 0 || dim > 4096) return set_err(HR_E_INVALID, "dim must be in [1, 4096]");
     if (dtype < F32 || dtype > F16) return set_err(HR_E_INVALID, "dtype must be HR_F32, HR_BF16 or HR_F16");
     if (metric != COSINE && metric != IP && metric != L2) return set_err(HR_E_INVALID, "unknown metric");
-    if (n_dev != 1) return set_err(HR_E_UNSUPPORTED, "one device per handle (shard across processes for multi-GPU)");
+    if (n_dev < 1 || n_dev > 64) return set_err(HR_E_INVALID, "n_dev must be in [1, 64]");
+    if (n_dev > 1) {
+        if (!dev_ids) return set_err(HR_E_INVALID, "dev_ids required when n_dev > 1");
+        return group_create(dim, dtype, metric, n_dev, dev_ids, out);
+    }
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     int dev = dev_ids ? dev_ids[0] : 0;
@@ -44,7 +48,7 @@ extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const 
     return HR_OK;
 }
 
-static int grow(hr_index* h, int64_t need_rows) {
+int index_grow(hr_index* h, int64_t need_rows) {
     if (need_rows <= h->cap) return HR_OK;
     int64_t new_cap = std::max<int64_t>({need_rows, h->cap + h->cap / 2, 1024});
     new_cap = (new_cap + 31) / 32 * 32;
@@ -83,8 +87,9 @@ static int grow(hr_index* h, int64_t need_rows) {
 extern "C" int hr_index_reserve(hr_index* h, int64_t capacity_rows) {
     if (!h || capacity_rows < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return group_reserve(h, capacity_rows);
     if (int rc = set_device(h)) return rc;
-    return grow(h, capacity_rows);
+    return index_grow(h, capacity_rows);
 }
 
 static int mark_live(hr_index* h, int64_t r0, int64_t n) {
@@ -109,7 +114,7 @@ static int finish_add(hr_index* h) {
 }
 
 // euclidean: fp32 |x|^2 of stored rows [r0, r0 + n) for the approximate scan score
-static int update_row_norms(hr_index* h, int64_t r0, int64_t n) {
+int index_update_row_norms(hr_index* h, int64_t r0, int64_t n) {
     if (h->metric != L2 || n <= 0) return HR_OK;
     return dispatch_dt(h->dtype, [&](auto dt) -> int {
         hipLaunchKernelGGL((k_row_norms<decltype(dt)::value>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream,
@@ -122,11 +127,12 @@ static int update_row_norms(hr_index* h, int64_t r0, int64_t n) {
 // SRC: where the fp32 rows come from (host memory staged through h->stage, the generator, or device memory).
 enum { ADD_HOST = 0, ADD_SYNTH = 1, ADD_DEVICE = 2 };
 
+// ADD_SYNTH: local row L gets generator row gen_base + stripe_row(L) (hr_common.hpp)
 template <int SRC>
-static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t grow0, int64_t n, int64_t* first) {
+static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t gen_base, int64_t n, int64_t* first) {
     constexpr bool SYNTH = SRC == ADD_SYNTH;
     if (int rc = set_device(h)) return rc;
-    if (int rc = grow(h, h->n + n)) return rc;
+    if (int rc = index_grow(h, h->n + n)) return rc;
     const int64_t r0 = h->n;
     const int64_t chunk = SYNTH ? (int64_t)1 << 22 : std::max<int64_t>(1, ((int64_t)64 << 20) / (4 * h->dim));
     for (int64_t off = 0; off < n; off += chunk) {
@@ -143,28 +149,39 @@ static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t grow0
         const dim3 grid((unsigned)((m + 3) / 4));
         int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
             hipLaunchKernelGGL((k_store<decltype(dt)::value, SYNTH>), grid, dim3(256), 0, h->stream, src, seed,
-                               grow0 + off, m, h->dim, h->S, h->metric, r0 + off, h->rows, h->norm_bits);
+                               gen_base, m, h->dim, h->S, h->metric, r0 + off, h->rows, h->norm_bits, nullptr,
+                               h->stripe_G, h->stripe_s);
             HIP_TRY(hipGetLastError());
             return HR_OK;
         });
         if (rc) return rc;
     }
     h->n = r0 + n;
-    if (int rc = update_row_norms(h, r0, n)) return rc;
+    if (int rc = index_update_row_norms(h, r0, n)) return rc;
     if (int rc = mark_live(h, r0, n)) return rc;
     if (int rc = finish_add(h)) return rc;
     if (first) *first = r0;
     return HR_OK;
 }
 
+int index_add_host(hr_index* h, const float* rows, int64_t n, int64_t* first) {
+    return add_impl<ADD_HOST>(h, rows, 0, 0, n, first);
+}
+int index_add_synthetic(hr_index* h, uint64_t seed, int64_t gen_base, int64_t n) {
+    return add_impl<ADD_SYNTH>(h, nullptr, seed, gen_base, n, nullptr);
+}
+
+static int64_t max_rows(const hr_index* h) { return (((int64_t)1 << 32) - 64) * h->G; }
+
 extern "C" int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* first_row_out) {
     if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
         return HR_OK;
     }
+    if (h->G > 1) return group_add_host(h, rows, n, first_row_out);
     return add_impl<ADD_HOST>(h, rows, 0, 0, n, first_row_out);
 }
 
@@ -172,22 +189,24 @@ extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global
                                       int64_t* first_row_out) {
     if (!h || n < 0 || global_row0 < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
         return HR_OK;
     }
-    return add_impl<ADD_SYNTH>(h, nullptr, seed, global_row0, n, first_row_out);
+    if (h->G > 1) return group_add_synthetic(h, seed, global_row0, n, first_row_out);
+    return add_impl<ADD_SYNTH>(h, nullptr, seed, global_row0 - h->n, n, first_row_out);
 }
 
 extern "C" int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_t n, const int64_t* dest_dev,
                                       int64_t n_rows_after, void* stream) {
     if (!h || n < 0 || (n > 0 && (!rows_dev || !dest_dev))) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "explicit row placement (IVF lists) needs a single-device index");
     if (n_rows_after < h->n || n_rows_after > ((int64_t)1 << 32) - 64)
         return set_err(HR_E_INVALID, "n_rows_after must be >= the current size and < 2^32");
     if (int rc = set_device(h)) return rc;
-    if (int rc = grow(h, n_rows_after)) return rc;
+    if (int rc = index_grow(h, n_rows_after)) return rc;
     hipEvent_t ev;  // order after the producer of rows_dev / dest_dev on the caller's stream
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(ev, (hipStream_t)stream));
@@ -232,11 +251,12 @@ extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n
                                    void* stream) {
     if (!h || n < 0 || (n > 0 && !rows_dev)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->n + n > ((int64_t)1 << 32) - 64) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
+    if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
         return HR_OK;
     }
+    if (h->G > 1) return group_add_device(h, rows_dev, n, first_row_out, (hipStream_t)stream);
     if (int rc = set_device(h)) return rc;
     // the rows are produced on the caller's stream (e.g. the embedder's pooling kernel): order the store after it.
     // add_impl synchronises h->stream before returning, so the caller may reuse rows_dev afterwards.
@@ -252,11 +272,18 @@ extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n
 extern "C" int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n) {
     if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return group_remove(h, rows, n);
+    return index_remove_local(h, rows, n);
+}
+
+int index_remove_local(hr_index* h, const int64_t* rows, int64_t n) {
     if (int rc = set_device(h)) return rc;
+    // validate every row before touching anything: a failed call leaves host and device bits as they were
+    for (int64_t i = 0; i < n; ++i)
+        if (rows[i] < 0 || rows[i] >= h->n) return set_err(HR_E_INVALID, "row out of range");
     int64_t lo = INT64_MAX, hi = -1;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t r = rows[i];
-        if (r < 0 || r >= h->n) return set_err(HR_E_INVALID, "row out of range");
         uint32_t& w = h->live_host[(size_t)(r >> 5)];
         const uint32_t bit = 1u << (r & 31);
         if (w & bit) {
@@ -278,7 +305,21 @@ extern "C" int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     if (n_out) *n_out = h->n;
-    if (n_live_out) *n_live_out = h->n_live;
+    int64_t live = h->n_live;
+    if (h->G > 1) {
+        live = 0;
+        for (hr_index* s : h->shards) live += s->n_live;
+    }
+    if (n_live_out) *n_live_out = live;
+    return HR_OK;
+}
+
+extern "C" int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* metric_out, int* n_dev_out) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    if (dim_out) *dim_out = h->dim;
+    if (dtype_out) *dtype_out = h->dtype;
+    if (metric_out) *metric_out = h->metric;
+    if (n_dev_out) *n_dev_out = h->G;
     return HR_OK;
 }
 
@@ -685,7 +726,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         hipLaunchKernelGGL((k_rescore<decltype(dt)::value>), dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st_tail, h->rows,
                            h->S, h->dpad, sc.q32.as<float>(), sc.sel_rows.as<uint32_t>(), sc.sel_cnt.as<int>(), B,
                            kc_sel, row_offset, sc.bound_approx.as<float>(), sc.qerr.as<double>(), max_norm,
-                           acc_gamma(h), storage_u(h), h->metric, sc.overflow.as<int>(), cand_out, bound_out);
+                           acc_gamma(h), storage_u(h), h->metric, sc.overflow.as<int>(), cand_out, bound_out,
+                           h->stripe_G, h->stripe_s);
         HIP_TRY(hipGetLastError());
         return HR_OK;
     });
@@ -711,7 +753,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
                 HIP_TRY(hipMemcpy(&qn2, sc.qerr.as<double>() + 4 * (size_t)b + 2, 8, hipMemcpyDeviceToHost));
             if (int rc2 = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
                                           h->metric, qn2, h->live, (const uint32_t*)mask_dev, h->n, row_offset, cap_out,
-                                          cand_out + (int64_t)b * cap_out, h->exh.p, h->exh.bytes, st))
+                                          cand_out + (int64_t)b * cap_out, h->exh.p, h->exh.bytes, st, h->stripe_G,
+                                          h->stripe_s))
                 return set_err(rc2, "exhaustive exact pass failed");
             h->n_exhaustive++;
         }
@@ -741,9 +784,8 @@ static int validate_search(hr_index* h, int B, int k) {
     return HR_OK;
 }
 
-static int launch_merge(int device, const Cand* cand, const double* bounds, int G, int B, int kc, int k, float* s_out,
-                        int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st, int64_t cstride = 0,
-                        int64_t bstride = 0) {
+int launch_merge(int device, const Cand* cand, const double* bounds, int G, int B, int kc, int k, float* s_out,
+                 int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st, int64_t cstride, int64_t bstride) {
     if (!cstride) cstride = (int64_t)B * kc * (int64_t)sizeof(Cand);
     if (!bstride) bstride = (int64_t)B * 8;
     int p2 = 1;
@@ -761,7 +803,6 @@ static int launch_merge(int device, const Cand* cand, const double* bounds, int 
     return HR_OK;
 }
 
-static constexpr int kFallbackCap = 1024;
 
 // full single-shard search on device-resident queries, with the exact fallback
 static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
@@ -789,7 +830,7 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     h->n_guard_fail += (int64_t)failed.size();
     // exact fallback: ONE collect re-scan of all failing queries (every row with approx >= kth - E,
     // rescored exactly), merged, then scattered back to the failing rows of the outputs
-    const int nf = (int)failed.size(), kc2 = kFallbackCap;
+    const int nf = (int)failed.size(), kc2 = kFallbackCapMax;
     HIP_TRY(h->fb_q.ensure((size_t)nf * h->dim * 4));
     HIP_TRY(h->fb_cand.ensure((size_t)nf * kc2 * sizeof(Cand)));
     HIP_TRY(h->fb_bound.ensure((size_t)nf * 8));
@@ -835,16 +876,17 @@ extern "C" int hr_index_search_device(hr_index* h, const float* q_dev, int B, in
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
+    if (h->G > 1) return group_search_device(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
     return search_device_impl(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
 }
 
 // top-k beyond HR_MAX_K (Chroma's n_results has no cap, chroma_store.py:118-120): the exhaustive
 // exact pass per query -- canonical fp64 score of every live, allowed row + stable radix sort,
-// the same arithmetic and (score desc, row asc) order as the scan path -- written straight into
-// the caller's host arrays.  One corpus pass and one n-row sort per query: for the rare large-k
-// call, not the batched hot path.
-static int search_exact_all_host(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev,
-                                 float* scores_out, int64_t* rows_out, hipStream_t st) {
+// the same arithmetic and (score desc, row asc) order as the scan path -- into host records
+// out_host[B][m] (global rows; -inf / -1 padding).  One corpus pass and one n-row sort per query:
+// for the rare large-k call, not the batched hot path.
+int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, Cand* out_host,
+                    hipStream_t st) {
     Scratch& sc = h->scr[kSyncSet];
     const int QB = (B + 31) / 32, Bp = QB * 32;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
@@ -861,24 +903,54 @@ static int search_exact_all_host(hr_index* h, const float* q_dev, int B, int k, 
     HIP_TRY(hipGetLastError());
     std::vector<double> qerr((size_t)Bp * 4);
     HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
-    const int m = (int)std::min<int64_t>(k, h->n);
-    HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
-    HIP_TRY(h->fb_cand.ensure((size_t)m * sizeof(Cand)));
-    std::vector<Cand> c((size_t)m);
     HIP_TRY(hipStreamSynchronize(st));
+    const int mm = (int)std::min<int64_t>(m, h->n);
+    for (int b = 0; b < B; ++b)
+        for (int i = 0; i < m; ++i) out_host[(int64_t)b * m + i] = Cand{-INFINITY, -1};
+    if (mm <= 0) return HR_OK;
+    HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
+    HIP_TRY(h->fb_cand.ensure((size_t)mm * sizeof(Cand)));
     for (int b = 0; b < B; ++b) {
         if (int rc = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
-                                     h->metric, qerr[4 * (size_t)b + 2], h->live, (const uint32_t*)mask_dev, h->n, 0, m,
-                                     h->fb_cand.as<Cand>(), h->exh.p, h->exh.bytes, st))
+                                     h->metric, qerr[4 * (size_t)b + 2], h->live, (const uint32_t*)mask_dev, h->n, 0, mm,
+                                     h->fb_cand.as<Cand>(), h->exh.p, h->exh.bytes, st, h->stripe_G, h->stripe_s))
             return set_err(rc, "exhaustive exact pass failed");
-        HIP_TRY(hipMemcpyAsync(c.data(), h->fb_cand.p, (size_t)m * sizeof(Cand), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(out_host + (int64_t)b * m, h->fb_cand.p, (size_t)mm * sizeof(Cand), hipMemcpyDeviceToHost,
+                               st));
         HIP_TRY(hipStreamSynchronize(st));
         h->n_exhaustive++;
-        for (int i = 0; i < k; ++i) {
-            const bool v = i < m && c[(size_t)i].row >= 0;
-            scores_out[(int64_t)b * k + i] = v ? (float)c[(size_t)i].score : -INFINITY;
-            rows_out[(int64_t)b * k + i] = v ? c[(size_t)i].row : -1;
-        }
+    }
+    return HR_OK;
+}
+
+// Selective filter (kb_file_search's index_type / source where-clauses, kb_search_toolkit.py:530-535):
+// when at most half the tiles hold a live, allowed row, the scans visit only those tiles -- a
+// filter that keeps one document's chunks reads that document's tiles, not the whole corpus.
+// mask_words: the host mask as one u32 per tile of this index.  Sets h->tl / h->tl_n (reset by the caller).
+int index_host_tile_list(hr_index* h, const uint32_t* mw, hipStream_t st) {
+    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
+    h->tl_n = -1;
+    if (!mw || !tl_env) return HR_OK;
+    const int64_t n_tiles = (h->n + 31) / 32;
+    const uint32_t* lw = h->live_host.data();
+    // a dense mask (most tiles hold an allowed row) keeps the full scan: decided on every 64th
+    // tile first, so a dense mask costs ~n_tiles/64 host checks, not a full list build
+    int64_t probe = 0, hit = 0;
+    for (int64_t t = 0; t < n_tiles; t += 64, ++probe) hit += (lw[t] & mw[t]) != 0;
+    std::vector<uint32_t>& tl = h->tl_host;
+    tl.clear();
+    bool use = false;
+    if (hit * 10 <= probe * 7) {  // not dense: build the list, giving up past half the tiles
+        const int64_t limit = n_tiles / 2;
+        for (int64_t t = 0; t < n_tiles && (int64_t)tl.size() <= limit; ++t)
+            if (lw[t] & mw[t]) tl.push_back((uint32_t)t);
+        use = (int64_t)tl.size() <= limit;
+    }
+    h->tl_n = -2;  // evaluated on the host: full scan unless the list is used below
+    if (use) {
+        HIP_TRY(h->tl.ensure(std::max<size_t>(4, tl.size() * 4)));
+        if (!tl.empty()) HIP_TRY(hipMemcpyAsync(h->tl.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st));
+        h->tl_n = (int64_t)tl.size();
     }
     return HR_OK;
 }
@@ -890,6 +962,7 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     if (int rc = set_device(h)) return rc;
     if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
     if (k <= 0) return set_err(HR_E_INVALID, "k must be positive");
+    if (h->G > 1) return group_search_host(h, q, B, k, row_mask, scores_out, rows_out);
     hipStream_t st = h->stream;
     if (h->n_live == 0) {  // empty index: reference returns [] (faiss_store.py:143-144)
         for (int64_t i = 0; i < (int64_t)B * k; ++i) {
@@ -910,44 +983,43 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     uint64_t* m_dev = row_mask ? (uint64_t*)((uint8_t*)so.p + off_m) : nullptr;
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
     if (row_mask) HIP_TRY(hipMemcpyAsync(m_dev, row_mask, words * 8, hipMemcpyHostToDevice, st));
-    if (k > HR_MAX_K) return search_exact_all_host(h, h->q_in.as<float>(), B, k, m_dev, scores_out, rows_out, st);
-    // Selective filter (kb_file_search's index_type / source where-clauses, kb_search_toolkit.py:530-535):
-    // when at most half the tiles hold a live, allowed row, the scans visit only those tiles -- a
-    // filter that keeps one document's chunks reads that document's tiles, not the whole corpus
+    if (k > HR_MAX_K) {
+        std::vector<Cand> c((size_t)B * k);
+        if (int rc = index_exact_all(h, h->q_in.as<float>(), B, k, m_dev, c.data(), st)) return rc;
+        for (size_t i = 0; i < c.size(); ++i) {
+            scores_out[i] = c[i].row >= 0 ? (float)c[i].score : -INFINITY;
+            rows_out[i] = c[i].row;
+        }
+        return HR_OK;
+    }
     struct TileListScope {
         hr_index* h;
         ~TileListScope() { h->tl_n = -1; }
     } tl_scope{h};
-    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
-    if (row_mask && tl_env) {
-        const int64_t n_tiles = (h->n + 31) / 32;
-        const uint32_t* mw = (const uint32_t*)row_mask;  // u64 words, little-endian = u32 per tile
-        const uint32_t* lw = h->live_host.data();
-        // a dense mask (most tiles hold an allowed row) keeps the full scan: decided on every 64th
-        // tile first, so a dense mask costs ~n_tiles/64 host checks, not a full list build
-        int64_t probe = 0, hit = 0;
-        for (int64_t t = 0; t < n_tiles; t += 64, ++probe) hit += (lw[t] & mw[t]) != 0;
-        std::vector<uint32_t>& tl = h->tl_host;
-        tl.clear();
-        bool use = false;
-        if (hit * 10 <= probe * 7) {  // not dense: build the list, giving up past half the tiles
-            const int64_t limit = n_tiles / 2;
-            for (int64_t t = 0; t < n_tiles && (int64_t)tl.size() <= limit; ++t)
-                if (lw[t] & mw[t]) tl.push_back((uint32_t)t);
-            use = (int64_t)tl.size() <= limit;
-        }
-        h->tl_n = -2;  // evaluated on the host: full scan unless the list is used below
-        if (use) {
-            HIP_TRY(h->tl.ensure(std::max<size_t>(4, tl.size() * 4)));
-            if (!tl.empty())
-                HIP_TRY(hipMemcpyAsync(h->tl.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st));
-            h->tl_n = (int64_t)tl.size();
-        }
-    }
+    if (int rc = index_host_tile_list(h, (const uint32_t*)row_mask, st)) return rc;
     if (int rc = search_device_impl(h, h->q_in.as<float>(), B, k, m_dev, s_dev, r_dev, st)) return rc;
     HIP_TRY(hipMemcpyAsync(scores_out, s_dev, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(rows_out, r_dev, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    return HR_OK;
+}
+
+// one shard's exact candidates (group handles, hr_group.hip)
+int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
+                       double* bound_out, hipStream_t st) {
+    return shard_search(h, q_dev, B, kc, mask_dev, 0, cand_out, bound_out, st, st);
+}
+
+int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,
+                        const uint64_t* mask_dev, Cand* cand_out, double* bound_out, hipStream_t st) {
+    Plan pl;
+    if (int rc = make_plan(h, B, &pl)) return rc;
+    for (int b0 = 0; b0 < B; b0 += pl.Bp) {  // one collect scan per chunk of queries
+        const int bc = std::min(pl.Bp, B - b0);
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, mask_dev, 0, kth_host + b0, 1, cap,
+                                 cand_out + (int64_t)b0 * cap, bound_out + b0, st, st))
+            return rc;
+    }
     return HR_OK;
 }
 
@@ -956,6 +1028,7 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
                                      double* bound_out_dev, void* stream) {
     if (!h || !q_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
     if (int rc = set_device(h)) return rc;
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
@@ -970,6 +1043,7 @@ extern "C" int hr_index_search_shard_async_ev(hr_index* h, const float* q_dev, i
     if (!h || !q_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
     if (scan_stream == tail_stream) return set_err(HR_E_INVALID, "scan and tail streams must differ");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
     if (int rc = set_device(h)) return rc;
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
@@ -990,6 +1064,7 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
     if (!h || !q_dev || !kth_dev || !cand_out_dev || !bound_out_dev) return set_err(HR_E_INVALID, "null argument");
     if (B <= 0 || cap <= 0 || cap > 2048) return set_err(HR_E_INVALID, "B > 0 and cap in [1, 2048] required");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
     if (int rc = set_device(h)) return rc;
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
     std::vector<double> kth((size_t)B);
@@ -1038,6 +1113,7 @@ extern "C" int hr_merge_candidates_strided(int device, const void* cand_dev, con
 extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out) {
     if (!h || !q || !approx_out || !e_out || B <= 0 || B > 64) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "diagnostics need a single-device index");
     if (int rc = set_device(h)) return rc;
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
@@ -1095,6 +1171,11 @@ extern "C" int hr_index_get_rows(hr_index* h, const int64_t* rows, int64_t n, fl
     if (n == 0) return HR_OK;
     for (int64_t i = 0; i < n; ++i)
         if (rows[i] < 0 || rows[i] >= h->n) return set_err(HR_E_INVALID, "row out of range");
+    if (h->G > 1) return group_get_rows(h, rows, n, out);
+    return index_get_rows(h, rows, n, out);
+}
+
+int index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out) {
     if (int rc = set_device(h)) return rc;
     HIP_TRY(h->stage.ensure((size_t)n * 8 + (size_t)n * h->dim * 4));
     int64_t* idx = (int64_t*)h->stage.p;
@@ -1113,19 +1194,16 @@ extern "C" int hr_index_get_rows(hr_index* h, const int64_t* rows, int64_t n, fl
 }
 
 // ---------------------------------------------------------------- persistence
-struct FileHeader {
-    char magic[8];
-    int32_t version, dim, dtype, metric;
-    int64_t n, n_live;
-    double max_norm2;
-};
 
 extern "C" int hr_index_save(hr_index* h, const char* path) {
     if (!h || !path) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return group_save(h, path);
     if (int rc = set_device(h)) return rc;
-    FILE* f = std::fopen(path, "wb");
-    if (!f) return set_err(HR_E_IO, std::string("cannot open ") + path);
+    // crash-safe: write <path>.tmp, fsync it, then rename over <path> (a crash leaves the old file)
+    const std::string tmp_path = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp_path.c_str(), "wb");
+    if (!f) return set_err(HR_E_IO, std::string("cannot open ") + tmp_path);
     FileHeader hd{};
     std::memcpy(hd.magic, "HIPRAG02", 8);  // 02: slot-swizzled tiles
     hd.version = 1;
@@ -1145,12 +1223,16 @@ extern "C" int hr_index_save(hr_index* h, const char* path) {
         tmp.resize((size_t)m * tb);
         if (hipMemcpy(tmp.data(), h->rows + (size_t)t * tb, (size_t)m * tb, hipMemcpyDeviceToHost) != hipSuccess) {
             std::fclose(f);
+            std::remove(tmp_path.c_str());
             return set_err(HR_E_HIP, "save: device copy failed");
         }
         ok = std::fwrite(tmp.data(), 1, tmp.size(), f) == tmp.size();
     }
     if (ok && tiles > 0) ok = std::fwrite(h->live_host.data(), 4, (size_t)tiles, f) == (size_t)tiles;
-    std::fclose(f);
+    ok = ok && std::fflush(f) == 0 && fsync(fileno(f)) == 0;
+    ok = (std::fclose(f) == 0) && ok;
+    if (ok) ok = std::rename(tmp_path.c_str(), path) == 0;
+    if (!ok) std::remove(tmp_path.c_str());
     return ok ? HR_OK : set_err(HR_E_IO, std::string("write failed: ") + path);
 }
 
@@ -1168,7 +1250,17 @@ extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr
         std::fclose(f);
         return rc;
     }
-    int rc = grow(h, hd.n);  // h is not yet visible to any other thread
+    if (h->G > 1) {  // the file holds the canonical single-index layout: re-stripe it over the shards
+        int rc = group_load_into(h, f, hd.n, hd.n_live, hd.max_norm2);
+        std::fclose(f);
+        if (rc != HR_OK) {
+            hr_index_destroy(h);
+            return rc;
+        }
+        *out = h;
+        return HR_OK;
+    }
+    int rc = index_grow(h, hd.n);  // h is not yet visible to any other thread
     const int64_t tiles = (hd.n + 31) / 32;
     const size_t tb = tile_bytes(h);
     std::vector<uint8_t> tmp;
@@ -1193,20 +1285,31 @@ extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr
     h->n = hd.n;
     h->n_live = hd.n_live;
     h->max_norm2 = hd.max_norm2;
-    if (int rc2 = update_row_norms(h, 0, h->n)) {
+    if (int rc2 = index_finish_load(h)) {
         hr_index_destroy(h);
         return rc2;
     }
-    (void)hipStreamSynchronize(h->stream);
-    unsigned long long bits;
-    std::memcpy(&bits, &hd.max_norm2, 8);
-    (void)hipMemcpy(h->norm_bits, &bits, 8, hipMemcpyHostToDevice);
     *out = h;
+    return HR_OK;
+}
+
+// after rows / live bits / n / max_norm2 were installed: row norms (euclidean) and the device max norm
+int index_finish_load(hr_index* h) {
+    if (int rc = set_device(h)) return rc;
+    if (int rc = index_update_row_norms(h, 0, h->n)) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    unsigned long long bits;
+    std::memcpy(&bits, &h->max_norm2, 8);
+    HIP_TRY(hipMemcpy(h->norm_bits, &bits, 8, hipMemcpyHostToDevice));
     return HR_OK;
 }
 
 extern "C" void hr_index_destroy(hr_index* h) {
     if (!h) return;
+    if (h->G > 1) {
+        group_destroy(h);
+        return;
+    }
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rows) (void)hipFree(h->rows);
@@ -1215,7 +1318,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
-                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl,
+                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl, &h->s_mask,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();
@@ -1254,24 +1357,30 @@ extern "C" int hr_index_set_scan_timing(hr_index* h, int every) {
     if (!h || every < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
     h->time_every = every;
-    h->main_passes = 0;
+    if (h->G == 1) h->main_passes = 0;
+    for (hr_index* s : h->shards) {  // group: every shard times its own launches (harvested from shard 0)
+        s->time_every = every;
+        s->main_passes = 0;
+    }
     return HR_OK;
 }
 
 extern "C" int hr_index_take_scan_times(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n_out) {
     if (!h || cap < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (int rc = set_device(h)) return rc;
-    return harvest(h, sample_ms, filter_ms, cap, n_out);
+    hr_index* t = h->G > 1 ? h->shards[0] : h;
+    if (int rc = set_device(t)) return rc;
+    return harvest(t, sample_ms, filter_ms, cap, n_out);
 }
 
 extern "C" int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (int rc = set_device(h)) return rc;
-    if (int rc = harvest(h, nullptr, nullptr, 1 << 30, nullptr)) return rc;
-    if (sample_ms) *sample_ms = h->last_sample_ms;
-    if (filter_ms) *filter_ms = h->last_filter_ms;
+    hr_index* t = h->G > 1 ? h->shards[0] : h;
+    if (int rc = set_device(t)) return rc;
+    if (int rc = harvest(t, nullptr, nullptr, 1 << 30, nullptr)) return rc;
+    if (sample_ms) *sample_ms = t->last_sample_ms;
+    if (filter_ms) *filter_ms = t->last_filter_ms;
     return HR_OK;
 }
 
@@ -1283,12 +1392,14 @@ extern "C" int hr_index_stats(hr_index* h, int64_t out[3]) {
     out[0] = h->main_passes;
     out[1] = h->n_guard_fail;
     out[2] = h->n_exhaustive;
+    if (h->G > 1) group_stats(h, out);
     return HR_OK;
 }
 
 extern "C" int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "diagnostics need a single-device index");
     if (int rc = set_device(h)) return rc;
     // private per-wave counts of the last FILTER scan: pcnt[W][Bp]
     const Scratch* sc = h->last_scr;

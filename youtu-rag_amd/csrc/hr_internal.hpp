@@ -2,6 +2,7 @@
 // (hr_index.hip: index handles and the exact search; hr_ivf.hip: the IVF lists search).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -56,7 +57,7 @@ size_t exhaustive_scratch_bytes(int64_t n);
 int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float* qv, int metric, double qn2,
                     const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
-                    size_t scratch_bytes, hipStream_t st);
+                    size_t scratch_bytes, hipStream_t st, int sG = 1, int ss = 0);
 size_t tile_list_scratch_bytes(int64_t n_tiles);
 int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles, uint32_t* list, uint32_t* count,
                     void* scratch, size_t scratch_bytes, hipStream_t st);
@@ -133,6 +134,64 @@ struct hr_index {
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
     int64_t n_guard_fail = 0;         // queries that failed the exactness guard (collect fallback)
     std::vector<float> floor_host;
+    // ---- multi-device handles (hr_index_create with n_dev > 1, hr_group.hip)
+    // A group handle owns G shard handles (one per dev_ids entry, repeats allowed) and stripes its
+    // rows over them by 32-row tile (stripe_row, hr_common.hpp); it holds no rows itself.  Its
+    // device / stream are the primary's (dev_ids[0]): the shards' candidates are copied there
+    // (hipMemcpyPeerAsync, xGMI) and merged by k_merge.  A shard knows its place in the stripe.
+    int G = 1;                        // > 1: group handle
+    std::vector<hr_index*> shards;
+    int stripe_G = 1, stripe_s = 0;   // shard of a group: global row of local row L = stripe_row(L, G, s)
+    DevBuf g_cand, g_bound, g_kth, g_fail, g_out, g_q;  // group: gathered candidates / merge outputs (primary)
+    DevBuf s_mask;                    // shard of a group: this shard's words of the caller's row mask
+    std::vector<hipEvent_t> g_ev;     // group: one per shard (shard stream -> primary stream)
+    hipEvent_t g_ev_q = nullptr;      // group: queries ready on the primary stream
+};
+
+// group-handle entry points (hr_group.hip); each public hr_index_* call forwards here when h->G > 1
+int group_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);
+void group_destroy(hr_index* g);
+int group_reserve(hr_index* g, int64_t rows);
+int group_add_host(hr_index* g, const float* rows, int64_t n, int64_t* first);
+int group_add_synthetic(hr_index* g, uint64_t seed, int64_t global_row0, int64_t n, int64_t* first);
+int group_add_device(hr_index* g, const float* rows_dev, int64_t n, int64_t* first, hipStream_t st);
+int group_remove(hr_index* g, const int64_t* rows, int64_t n);
+int group_search_host(hr_index* g, const float* q, int B, int k, const uint64_t* mask, float* s_out, int64_t* r_out);
+int group_search_device(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
+                        int64_t* r_out, hipStream_t st);
+int group_get_rows(hr_index* g, const int64_t* rows, int64_t n, float* out);
+int group_save(hr_index* g, const char* path);
+int group_load_into(hr_index* g, FILE* f, int64_t n, int64_t n_live, double max_norm2);
+void group_stats(hr_index* g, int64_t out[3]);
+
+// single-shard internals shared with hr_group.hip (hr_index.hip)
+int index_grow(hr_index* h, int64_t need_rows);
+int index_add_host(hr_index* h, const float* rows, int64_t n, int64_t* first);
+int index_add_synthetic(hr_index* h, uint64_t seed, int64_t gen_base, int64_t n);
+int index_remove_local(hr_index* h, const int64_t* rows, int64_t n);
+int index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out);
+int index_update_row_norms(hr_index* h, int64_t r0, int64_t n);
+int index_finish_load(hr_index* h);
+// one batch of queries (device, on this shard's device) through the exact search of one shard:
+// candidates (global rows) + bounds into cand_out / bound_out on `st`
+int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
+                       double* bound_out, hipStream_t st);
+int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,
+                        const uint64_t* mask_dev, Cand* cand_out, double* bound_out, hipStream_t st);
+int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, Cand* out_host,
+                    hipStream_t st);
+int index_host_tile_list(hr_index* h, const uint32_t* mask_words, hipStream_t st);
+int launch_merge(int device, const Cand* cand, const double* bounds, int G, int B, int kc, int k, float* s_out,
+                 int64_t* r_out, double* kth_out, int32_t* fail_out, hipStream_t st, int64_t cstride = 0,
+                 int64_t bstride = 0);
+static constexpr int kFallbackCapMax = 1024;
+inline int fallback_cap(int G) { return std::max(64, std::min(kFallbackCapMax, 8192 / std::max(1, G))); }
+
+struct FileHeader {
+    char magic[8];
+    int32_t version, dim, dtype, metric;
+    int64_t n, n_live;
+    double max_norm2;
 };
 
 inline size_t tile_bytes(const hr_index* h) { return (size_t)h->S * (h->dtype == F32 ? 2048 : 1024); }

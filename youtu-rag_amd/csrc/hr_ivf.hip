@@ -434,6 +434,7 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
                              void* probes_out_dev, void* stream) {
     if (!h || !centroids_dev || !list_tiles_dev || !ids_dev || !q_dev || !cand_out_dev || !bound_out_dev)
         return set_err(HR_E_INVALID, "null argument");
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "IVF lists need a single-device index");
     if (B <= 0 || nlist <= 0 || nprobe <= 0 || nprobe > nlist || nprobe > kTopkMax || k <= 0 || k > kTopkMax ||
         max_list_tiles < 0)
         return set_err(HR_E_INVALID, "bad sizes (need 1 <= nprobe <= min(nlist, 1024), 1 <= k <= 1024)");

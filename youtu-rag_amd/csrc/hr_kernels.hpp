@@ -26,17 +26,20 @@ namespace hr {
 // One wave per row.  Phase 1: canonical fp64 norm² (lane-strided + butterfly, exactly the
 // oracle's order).  Phase 2: lane c owns 8-element chunks, scales (cosine), quantises
 // and writes its 16-byte (32-byte for fp32) slot of the tiled layout.
+// SYNTH: local row L = lrow0 + r gets generator row gen_base + stripe_row(L, sG, ss) (the handle row
+// of a striped shard; for a single-device index gen_base + L).
 template <int DT, bool SYNTH>
-__global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uint64_t seed, int64_t grow0, int64_t n,
+__global__ __launch_bounds__(256) void k_store(const float* __restrict__ in, uint64_t seed, int64_t gen_base, int64_t n,
                                                int dim, int S, int metric, int64_t lrow0, uint8_t* __restrict__ rows,
                                                unsigned long long* max_norm2_bits,
-                                               const int64_t* __restrict__ dest = nullptr) {
+                                               const int64_t* __restrict__ dest = nullptr, int sG = 1, int ss = 0) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n) return;
+    const int64_t grow = SYNTH ? gen_base + stripe_row(lrow0 + r, sG, ss) : 0;
     auto src = [&](int d) -> float {
         if (d >= dim) return 0.0f;
-        return SYNTH ? gen_elem(seed, grow0 + r, dim, d) : in[r * dim + d];
+        return SYNTH ? gen_elem(seed, grow, dim, d) : in[r * dim + d];
     };
     double inv = 1.0;
     bool scale = false;
@@ -842,7 +845,8 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
                                                  const float* __restrict__ bound_approx,
                                                  const double* __restrict__ qerr, double max_norm, double gamma,
                                                  double u_x, int metric, const int* __restrict__ overflow,
-                                                 Cand* __restrict__ out, double* __restrict__ bound_out) {
+                                                 Cand* __restrict__ out, double* __restrict__ bound_out, int sG = 1,
+                                                 int ss = 0) {
     const int lane = threadIdx.x & 63;
     const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= (int64_t)B * kc) return;
@@ -875,7 +879,7 @@ __global__ __launch_bounds__(256) void k_rescore(const uint8_t* __restrict__ row
         x2 = wave_butterfly_sum(x2);
         p = euclid_score(qn2, p, x2);
     }
-    if (lane == 0) out[wid] = Cand{p, r + row_offset};
+    if (lane == 0) out[wid] = Cand{p, stripe_row(r, sG, ss) + row_offset};
 }
 
 // ---------------------------------------------------------------- K4/C1: merge shards

@@ -41,7 +41,7 @@ EXPORTS = [
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
-    "hr_add_layernorm",
+    "hr_add_layernorm", "hr_index_info",
 ]
 
 _lib = None
@@ -83,6 +83,7 @@ def load_library(path: str | None = None):
             "hr_index_search": [vp, vp, i32, i32, vp, vp, vp],
             "hr_index_search_device": [vp, vp, i32, i32, vp, vp, vp, vp],
             "hr_index_size": [vp, vp, vp],
+            "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
             "hr_index_save": [vp, ctypes.c_char_p],
             "hr_index_load": [ctypes.c_char_p, i32, vp, pp],
@@ -144,9 +145,13 @@ def device_count() -> int:
 class NativeIndex:
     """One device shard of the vector index (an hr_index handle)."""
 
-    def __init__(self, dim: int, dtype: str = "bf16", metric: str = "cosine", device: int = 0, _handle=None):
+    def __init__(self, dim: int, dtype: str = "bf16", metric: str = "cosine", device: int = 0,
+                 devices: list[int] | None = None, _handle=None):
+        """One index handle.  ``devices`` (GPU ids, repeats allowed) shards its rows over several
+        GPUs inside the handle (hr_index_create with n_dev > 1); default: the single ``device``."""
         self.lib = load_library()
-        self.dim, self.dtype, self.metric, self.device = int(dim), dtype, metric, int(device)
+        self.devices = [int(d) for d in devices] if devices else [int(device)]
+        self.dim, self.dtype, self.metric, self.device = int(dim), dtype, metric, self.devices[0]
         if _handle is not None:
             self._h = _handle
             return
@@ -155,8 +160,9 @@ class NativeIndex:
         if metric not in METRICS:
             raise ValueError(f"unknown metric {metric!r}")
         h = ctypes.c_void_p()
-        dev = (ctypes.c_int * 1)(self.device)
-        _check(self.lib.hr_index_create(self.dim, DTYPES[dtype], METRICS[metric], 1, dev, ctypes.byref(h)))
+        dev = (ctypes.c_int * len(self.devices))(*self.devices)
+        _check(self.lib.hr_index_create(self.dim, DTYPES[dtype], METRICS[metric], len(self.devices), dev,
+                                        ctypes.byref(h)))
         self._h = h
 
     # -- lifecycle
@@ -317,12 +323,23 @@ class NativeIndex:
 
     @classmethod
     def load(cls, path: str, device: int = 0, dim: int | None = None, dtype: str | None = None,
-             metric: str | None = None) -> "NativeIndex":
+             metric: str | None = None, devices: list[int] | None = None) -> "NativeIndex":
         L = load_library()
         h = ctypes.c_void_p()
-        dev = (ctypes.c_int * 1)(int(device))
-        _check(L.hr_index_load(os.fsencode(path), 1, dev, ctypes.byref(h)))
-        return cls(dim or 0, dtype or "bf16", metric or "cosine", device, _handle=h)
+        devs = [int(d) for d in devices] if devices else [int(device)]
+        dev = (ctypes.c_int * len(devs))(*devs)
+        _check(L.hr_index_load(os.fsencode(path), len(devs), dev, ctypes.byref(h)))
+        d, dt, m, g = (ctypes.c_int(0) for _ in range(4))
+        _check(L.hr_index_info(h, ctypes.byref(d), ctypes.byref(dt), ctypes.byref(m), ctypes.byref(g)))
+        # the file's own shape (the dim / dtype / metric arguments are only checked against it)
+        dtype_f = {0: "f32", 1: "bf16", 2: "f16"}[dt.value]
+        metric_f = {0: "cosine", 1: "ip", 2: "l2"}[m.value]
+        if (dim and int(dim) != d.value) or (dtype and DTYPES.get(dtype) != dt.value) or \
+                (metric and METRICS.get(metric) != m.value):
+            L.hr_index_destroy(h)
+            raise ValueError(f"{path}: index is dim={d.value} dtype={dtype_f} metric={metric_f}, "
+                             f"not dim={dim} dtype={dtype} metric={metric}")
+        return cls(d.value, dtype_f, metric_f, devs[0], devices=devs, _handle=h)
 
 
 def gen_rows_device(seed: int, row0: int, n: int, dim: int, out_ptr: int, stream: int = 0) -> None:

@@ -31,8 +31,12 @@ class VectorRetriever(BaseRetriever):
         self.config = config or RetrieverConfig()
         self.reranker = reranker
         if self.config.enable_reranking and self.reranker is None:
-            raise ValueError("enable_reranking=True needs a reranker instance (the HTTP reranker factory of the "
-                             "reference is not part of hiprag)")
+            # the reference builds RerankerFactory.create(backend="auto", model=config.reranker_model)
+            # (base_retriever.py:36-40), an HTTP client; the MI355X replacement is the in-process
+            # cross-encoder (local checkpoint if reranker_model is a path, else the seeded preset)
+            from .rerankers import RerankerFactory
+
+            self.reranker = RerankerFactory.create(backend="rocm", model_name_or_path=self.config.reranker_model)
 
     def _to_results(self, hits, threshold: float) -> list[RetrievalResult]:
         out = []

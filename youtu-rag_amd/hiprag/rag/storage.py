@@ -9,28 +9,49 @@ the production store) with the exact-search semantics of FAISSVectorStore
   * search (chroma :90-148): exact top-k on the GPU; cosine/"dot" similarity =
     inner product (faiss :179-180; chroma's 1 - distance :135 for those spaces),
     "euclidean" similarity = 1 - squared L2 distance (chroma's "l2" space, :48-53);
-    ``filters`` are compiled to a row bitmap (plain dict or Chroma where-clause)
-    and applied inside the scan, i.e. exact top-k among matching rows;
+    ``filters`` are compiled to a row bitmap (plain dict or Chroma where-clause,
+    filters.py: cached per predicate) and applied inside the scan, i.e. exact top-k
+    among matching rows;
   * delete / delete_by_document_id / delete_by_metadata (chroma :150-222):
     row tombstones in the index + removal from the host tables;
-  * get_by_id (chroma :224-247) returns the stored (normalised, quantised) vector
-    as ``embedding``; count / clear / delete_collection.
-Host tables (row -> chunk record, chunk id -> row) play the role of FAISS's
-id_to_idx / idx_to_chunk (faiss_store.py:52-54, :112-121).  Persistence:
-``<persist_directory>/<collection>.hri`` (the device index) + ``.rows.jsonl``.
+  * get_by_id (chroma :224-247); count / clear / delete_collection.
+
+Concurrency (SURVEY §7 hard part 5).  The reference calls Chroma synchronously inside
+``async def`` (chroma_store.py:118) and its callers issue one query per
+``VectorRetriever.retrieve`` (base_retriever.py:58-63).  Here ``search`` hands the query
+to a micro-batcher: every ``search`` awaiting at the same time (same filter) becomes ONE
+GPU launch, run in a worker thread (``asyncio.to_thread``; ctypes drops the GIL), so the
+event loop keeps running and concurrent retrievers share one corpus pass.  Requests that
+arrive while a launch is in flight form the next batch (no timer: the batch size follows
+the load).  Results are identical to sequential calls (top-k of a smaller k is the prefix of
+the larger k's, order score desc / row asc).
+
+Embeddings: the index keeps the normalised vectors in ``dtype`` (bf16 by default, 2 B per
+element -- search is exact over the stored values, ranking ties at the bf16 resolution can
+differ from an fp32 store); ``dtype: f32`` keeps fp32 rows.  Chroma returns the raw fp32
+embedding it stored (chroma_store.py:233-244): ``keep_embeddings: true`` keeps a host fp32
+copy for ``get_by_id`` / ``include_embeddings``; without it they return the stored
+(normalised, quantised) row.
+
+Persistence: generation snapshots + an append-only journal (persist.py); ``add_chunks`` and
+``delete*`` write O(chunk) bytes.  ``index_params.devices`` (list of GPU ids) shards the rows
+of one collection over several GPUs inside one handle (hr_index_create with n_dev > 1).
 """
 from __future__ import annotations
 
+import asyncio
 import contextlib
 import json
 import logging
 import os
+import threading
 from typing import Any
 
 import numpy as np
 
 from .. import _native
 from . import filters as F
+from . import persist as P
 from .base import BaseVectorStore, Chunk
 from .config import VectorStoreConfig
 
@@ -39,79 +60,213 @@ logger = logging.getLogger(__name__)
 _METRIC = {"cosine": "cosine", "dot": "ip", "euclidean": "l2"}
 
 
+class _SearchBatcher:
+    """Coalesces concurrent ``search`` calls into batched launches (one per filter group)."""
+
+    def __init__(self, store: "HipVectorStore", max_batch: int):
+        self.store, self.max_batch = store, max(1, int(max_batch))
+        self.pending: list = []
+        self.running = False
+        self.launches = 0  # diagnostics
+
+    async def search(self, q: np.ndarray, top_k: int, filters):
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self.pending.append((q, int(top_k), filters, _filter_key(filters), fut))
+        if not self.running:
+            self.running = True
+            # start draining on the next loop iteration: every task that is ready now enqueues first
+            loop.call_soon(lambda: loop.create_task(self._drain()))
+        return await fut
+
+    async def _drain(self):
+        try:
+            while self.pending:
+                key = self.pending[0][3]
+                batch, rest = [], []
+                for e in self.pending:
+                    (batch if e[3] == key and len(batch) < self.max_batch else rest).append(e)
+                self.pending = rest
+                qs = np.stack([e[0] for e in batch])
+                k = max(e[1] for e in batch)
+                self.launches += 1
+                try:
+                    res = await asyncio.to_thread(self.store.search_batch, qs, k, batch[0][2])
+                except Exception as exc:  # noqa: BLE001 -- every waiter sees the failure
+                    for e in batch:
+                        if not e[4].done():
+                            e[4].set_exception(exc)
+                    continue
+                for e, r in zip(batch, res):
+                    if not e[4].done():
+                        e[4].set_result(r[: e[1]])
+        finally:
+            self.running = False
+
+
+def _filter_key(filters) -> str:
+    if not filters:
+        return ""
+    return json.dumps(filters, sort_keys=True, default=repr)
+
+
 class HipVectorStore(BaseVectorStore):
-    def __init__(self, config: VectorStoreConfig, *, index_factory=None):
+    def __init__(self, config: VectorStoreConfig, *, index_factory=None, index_loader=None):
         self.config = config
         params = dict(config.index_params or {})
         self.dtype = params.get("dtype", "bf16")
-        self.device = int(params.get("device", 0))
+        devs = params.get("devices")
+        self.devices = [int(d) for d in devs] if devs else [int(params.get("device", 0))]
+        self.device = self.devices[0]
         self.capacity = int(params.get("capacity", 0))
         self.include_embeddings = bool(params.get("include_embeddings", False))
+        self.keep_embeddings = bool(params.get("keep_embeddings", False))
         self.persist = bool(params.get("persist", True))
+        self.fsync = bool(params.get("fsync", True))
+        self.journal_fraction = float(params.get("journal_fraction", 0.25))
         self.metric = _METRIC[config.distance_metric]
         if self.dtype not in _native.DTYPES:
             raise ValueError(f"unknown index dtype {self.dtype!r}")
-        self._factory = index_factory or (lambda dim: _native.NativeIndex(dim, self.dtype, self.metric, self.device))
+        self._factory = index_factory or (lambda dim: _native.NativeIndex(dim, self.dtype, self.metric,
+                                                                          devices=self.devices))
+        self._loader = index_loader or (lambda path, dim, dtype, metric: _native.NativeIndex.load(
+            path, devices=self.devices, dim=dim, dtype=dtype, metric=metric))
+        self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)))
+        self._lock = threading.RLock()
+        self._paths = P.Paths(config.persist_directory, config.collection_name)
+        self._gen = 0
+        self._journal: P.Journal | None = None
+        self._snapshot_bytes = 0
+        self._reset_tables()
+        if self.persist:
+            self._load_if_present()
+
+    def _reset_tables(self):
         self._index = None
         self.dim: int | None = None
         self._records: list[dict | None] = []
         self._id_to_row: dict[str, int] = {}
         self._doc_rows: dict[str, list[int]] = {}
         self._cols = F.MetadataColumns()
+        self._live = np.zeros(0, bool)
+        self._raw = None  # keep_embeddings: (capacity, dim) fp32 host copy
         self._defer, self._dirty = 0, False
-        if self.persist:
-            self._load_if_present()
 
     # ---------------------------------------------------------------- persistence
-    def _paths(self):
-        base = os.path.join(self.config.persist_directory, self.config.collection_name)
-        return base + ".hri", base + ".rows.jsonl"
-
     def _load_if_present(self):
-        idx_path, rows_path = self._paths()
-        if not (os.path.exists(idx_path) and os.path.exists(rows_path)):
-            return
-        with open(rows_path) as f:
-            header = json.loads(f.readline())
-            records = [json.loads(line) for line in f]
+        pt = self._paths
+        if os.path.exists(pt.manifest):
+            with open(pt.manifest) as f:
+                man = json.load(f)
+            g = int(man["gen"])
+            idx_path, rows_path, emb_path = pt.gen(g, "hri"), pt.gen(g, "rows.jsonl"), pt.gen(g, "emb.npy")
+            self._gen = g
+        else:
+            idx_path, rows_path = pt.legacy  # round-1 layout
+            emb_path, man = None, None
+            if not (os.path.exists(idx_path) and os.path.exists(rows_path)):
+                return
+        header, records = P.read_rows(rows_path)
         self.dim = int(header["dim"])
-        self._index = _native.NativeIndex.load(idx_path, device=self.device, dim=self.dim, dtype=header["dtype"],
-                                               metric=header["metric"])
-        self._records = records
+        self.dtype, self.metric = header["dtype"], header["metric"]  # the files' own, not the config's
+        self._index = self._loader(idx_path, self.dim, self.dtype, self.metric)
+        n_idx = self._index.size()[0]
+        n_hdr = int(header.get("n_rows", len(records)))
+        if not (n_idx == n_hdr == len(records)) or (man is not None and int(man["n_rows"]) != n_idx):
+            self._index.close()
+            self._index = None
+            raise RuntimeError(f"collection files disagree on the row count (index {n_idx}, rows header {n_hdr}, "
+                               f"records {len(records)}); refusing to load {rows_path}")
+        raw = None
+        if self.keep_embeddings and emb_path and os.path.exists(emb_path):
+            raw = np.load(emb_path, allow_pickle=False)
+        self._install(records, raw)
+        self._snapshot_bytes = os.path.getsize(idx_path)
+        if man is not None:  # replay the journal of this generation
+            n_ops = 0
+            for op, a, b in P.Journal.replay(pt.gen(self._gen, "journal")):
+                if op == "add":
+                    first = self._index.add(b)
+                    if first != len(self._records):
+                        raise RuntimeError("journal replay: row numbering diverged")
+                    self._append_tables(a, b)
+                else:
+                    self._remove_tables(a.tolist(), journal=False)
+                n_ops += 1
+            if n_ops:
+                logger.info("replayed %d journal entries", n_ops)
+        logger.info("loaded %d chunks from %s", len(self._id_to_row), idx_path)
+
+    def _install(self, records: list, raw):
+        self._records = list(records)
+        self._live = np.array([r is not None for r in records], bool)
         for row, rec in enumerate(records):
             if rec is not None:
                 self._id_to_row[rec["id"]] = row
                 self._doc_rows.setdefault(rec["document_id"], []).append(row)
         self._cols.append([(rec or {}).get("metadata", {}) for rec in records])
-        logger.info("loaded %d chunks from %s", len(self._id_to_row), idx_path)
+        if self.keep_embeddings:
+            self._raw = np.zeros((max(len(records), 1024), self.dim), np.float32)
+            if raw is not None and len(raw) == len(records):
+                self._raw[: len(records)] = raw
 
     @contextlib.contextmanager
     def deferred_save(self):
-        """Write the persist files once at the end of a block of adds/deletes (bulk ingest)."""
+        """Write one snapshot at the end of a block of adds/deletes (bulk ingest) instead of
+        journaling each call."""
         self._defer += 1
         try:
             yield self
         finally:
             self._defer -= 1
             if self._defer == 0 and self._dirty:
-                self._save()
+                self.flush()
 
-    def _save(self):
+    def flush(self):
+        """Write a new snapshot generation now (folds the journal in)."""
+        with self._lock:
+            self._dirty = False
+            if not self.persist or self._index is None:
+                return
+            pt = self._paths
+            os.makedirs(self.config.persist_directory, exist_ok=True)
+            g = self._gen + 1
+            n = len(self._records)
+            self._index.save(pt.gen(g, "hri"))
+            P.write_rows(pt.gen(g, "rows.jsonl"), {"format": P.FORMAT, "gen": g, "n_rows": n, "dim": self.dim,
+                                                  "dtype": self.dtype, "metric": self.metric}, self._records)
+            if self.keep_embeddings:
+                P.fsync_write(pt.gen(g, "emb.npy"), writer=lambda f: np.save(f, self._raw[:n], allow_pickle=False))
+            P.fsync_write(pt.manifest, json.dumps({"format": P.FORMAT, "gen": g, "n_rows": n, "dim": self.dim,
+                                                   "dtype": self.dtype, "metric": self.metric}).encode())
+            old = self._gen
+            if self._journal is not None:
+                self._journal.close()
+                self._journal = None
+            self._gen = g
+            self._snapshot_bytes = os.path.getsize(pt.gen(g, "hri"))
+            for f in P.Paths(self.config.persist_directory, self.config.collection_name).all_files():
+                if f.startswith(pt.base + f".g{old}.") or f in pt.legacy:
+                    with contextlib.suppress(OSError):
+                        os.remove(f)
+
+    def _log(self, op: str, rows=None, records=None, vectors=None):
+        """Persist one mutation: journal it, or mark the deferred block dirty."""
         if not self.persist or self._index is None:
             return
-        if self._defer:
+        if self._defer or self._gen == 0:  # (no snapshot yet: the first write is a snapshot)
             self._dirty = True
+            if not self._defer:
+                self.flush()
             return
-        self._dirty = False
-        os.makedirs(self.config.persist_directory, exist_ok=True)
-        idx_path, rows_path = self._paths()
-        self._index.save(idx_path)
-        tmp = rows_path + ".tmp"
-        with open(tmp, "w") as f:
-            f.write(json.dumps({"dim": self.dim, "dtype": self.dtype, "metric": self.metric}) + "\n")
-            for rec in self._records:
-                f.write(json.dumps(rec) + "\n")
-        os.replace(tmp, rows_path)
+        if self._journal is None:
+            self._journal = P.Journal(self._paths.gen(self._gen, "journal"), fsync=self.fsync)
+        if op == "add":
+            self._journal.append_add(records, vectors)
+        else:
+            self._journal.append_delete(rows)
+        if self._journal.size > max(64 << 20, self.journal_fraction * self._snapshot_bytes):
+            self.flush()
 
     # ---------------------------------------------------------------- writes
     def _fresh(self, chunks: list[Chunk]) -> list[int]:
@@ -133,60 +288,86 @@ class HipVectorStore(BaseVectorStore):
         elif dim != self.dim:
             raise ValueError(f"embedding dim {dim} != collection dim {self.dim}")
 
-    def _register(self, fresh: list[Chunk], first: int):
-        metas = []
-        for i, c in enumerate(fresh):
-            meta = {"document_id": c.document_id, "chunk_index": c.chunk_index,
-                    **{k: v for k, v in (c.metadata or {}).items() if v is not None}}
-            rec = {"id": c.id, "document_id": c.document_id, "content": c.content, "chunk_index": c.chunk_index,
-                   "metadata": meta}
-            assert first + i == len(self._records)
+    @staticmethod
+    def _record(c: Chunk) -> dict:
+        meta = {"document_id": c.document_id, "chunk_index": c.chunk_index,
+                **{k: v for k, v in (c.metadata or {}).items() if v is not None}}
+        return {"id": c.id, "document_id": c.document_id, "content": c.content, "chunk_index": c.chunk_index,
+                "metadata": meta}
+
+    def _append_tables(self, records: list[dict], vectors: np.ndarray | None):
+        first = len(self._records)
+        for i, rec in enumerate(records):
             self._records.append(rec)
-            self._id_to_row[c.id] = first + i
-            self._doc_rows.setdefault(c.document_id, []).append(first + i)
-            metas.append(meta)
-        self._cols.append(metas)
-        self._save()
+            if rec is not None:
+                self._id_to_row[rec["id"]] = first + i
+                self._doc_rows.setdefault(rec["document_id"], []).append(first + i)
+        self._cols.append([(rec or {}).get("metadata", {}) for rec in records])
+        n = len(self._records)
+        if len(self._live) < n:
+            live = np.zeros(max(n, 2 * len(self._live), 1024), bool)
+            live[: len(self._live)] = self._live
+            self._live = live
+        self._live[first:n] = [rec is not None for rec in records]
+        if self.keep_embeddings:
+            if self._raw is None or len(self._raw) < n:
+                raw = np.zeros((max(n, 2 * (0 if self._raw is None else len(self._raw)), 1024), self.dim), np.float32)
+                if self._raw is not None:
+                    raw[: len(self._raw)] = self._raw
+                self._raw = raw
+            if vectors is not None:
+                self._raw[first:n] = vectors
+
+    def _register(self, fresh: list[Chunk], first: int, vectors: np.ndarray | None):
+        records = [self._record(c) for c in fresh]
+        if first != len(self._records):
+            raise RuntimeError(f"index row {first} != host table size {len(self._records)}")
+        self._append_tables(records, vectors)
+        self._log("add", records=records, vectors=vectors)
         logger.info("added %d chunks to %s", len(fresh), self.config.collection_name)
 
     async def add_chunks(self, chunks: list[Chunk]) -> None:
         if not chunks:
             return
-        fresh = [chunks[i] for i in self._fresh(chunks)]
-        if not fresh:
-            return
-        if any(c.embedding is None for c in fresh):
-            raise ValueError("every chunk needs an embedding")
-        emb = np.asarray([c.embedding for c in fresh], dtype=np.float32)
-        if emb.ndim != 2:
-            raise ValueError("embeddings must all have the same dimension")
-        self._ensure_index(emb.shape[1])
-        self._register(fresh, self._index.add(emb))
+        with self._lock:
+            fresh = [chunks[i] for i in self._fresh(chunks)]
+            if not fresh:
+                return
+            if any(c.embedding is None for c in fresh):
+                raise ValueError("every chunk needs an embedding")
+            emb = np.asarray([c.embedding for c in fresh], dtype=np.float32)
+            if emb.ndim != 2:
+                raise ValueError("embeddings must all have the same dimension")
+            self._ensure_index(emb.shape[1])
+            self._register(fresh, self._index.add(emb), emb)
 
     def add_chunks_device(self, chunks: list[Chunk], embeddings, stream: int | None = None) -> int:
         """add_chunks for embeddings that are already on the GPU (the in-process embedder's output):
         `embeddings` is a (len(chunks), dim) float32 device tensor; the vectors never visit the host
-        (replaces embed_texts -> add_chunks, processors.py:413-418).  Returns the number added."""
+        on the index path (replaces embed_texts -> add_chunks, processors.py:413-418; a host copy is
+        made only for the journal / keep_embeddings).  Returns the number added."""
         import torch
 
         if not chunks:
             return 0
         if embeddings.dim() != 2 or embeddings.shape[0] != len(chunks) or not embeddings.is_cuda:
             raise ValueError("embeddings must be a (len(chunks), dim) device tensor")
-        keep = self._fresh(chunks)
-        if not keep:
-            return 0
-        emb = embeddings if len(keep) == len(chunks) else embeddings[torch.as_tensor(keep, device=embeddings.device)]
-        emb = emb.to(torch.float32).contiguous()
-        self._ensure_index(emb.shape[1])
-        if stream is None:
-            stream = torch.cuda.current_stream(emb.device).cuda_stream
-        first = self._index.add_device(emb.data_ptr(), emb.shape[0], stream)
-        self._register([chunks[i] for i in keep], first)
-        return len(keep)
+        with self._lock:
+            keep = self._fresh(chunks)
+            if not keep:
+                return 0
+            emb = embeddings if len(keep) == len(chunks) else embeddings[torch.as_tensor(keep, device=embeddings.device)]
+            emb = emb.to(torch.float32).contiguous()
+            self._ensure_index(emb.shape[1])
+            if stream is None:
+                stream = torch.cuda.current_stream(emb.device).cuda_stream
+            first = self._index.add_device(emb.data_ptr(), emb.shape[0], stream)
+            need_host = self.keep_embeddings or (self.persist and not self._defer and self._gen > 0)
+            self._register([chunks[i] for i in keep], first, emb.cpu().numpy() if need_host else None)
+            return len(keep)
 
-    def _remove_rows(self, rows: list[int]) -> int:
-        rows = [r for r in rows if self._records[r] is not None]
+    def _remove_tables(self, rows: list[int], journal: bool = True) -> int:
+        rows = [int(r) for r in rows if 0 <= r < len(self._records) and self._records[r] is not None]
         if not rows:
             return 0
         self._index.remove(np.asarray(rows, np.int64))
@@ -199,36 +380,44 @@ class HipVectorStore(BaseVectorStore):
                 if not doc:
                     del self._doc_rows[rec["document_id"]]
             self._records[r] = None
-        self._save()
+            self._live[r] = False
+        if journal:
+            self._log("del", rows=rows)
         return len(rows)
 
     async def delete(self, chunk_ids: list[str]) -> None:
         if not chunk_ids or self._index is None:
             return
-        self._remove_rows([self._id_to_row[c] for c in chunk_ids if c in self._id_to_row])
+        with self._lock:
+            self._remove_tables([self._id_to_row[c] for c in chunk_ids if c in self._id_to_row])
 
     async def delete_by_document_id(self, document_id: str) -> int:
         if self._index is None:
             return 0
-        n = self._remove_rows(list(self._doc_rows.get(document_id, ())))
+        with self._lock:
+            n = self._remove_tables(list(self._doc_rows.get(document_id, ())))
         logger.info("deleted %d chunks for document_id %s", n, document_id)
         return n
 
     async def delete_by_metadata(self, metadata_filter: dict[str, Any]) -> int:
         if self._index is None or not metadata_filter:
             return 0
-        hit = F.evaluate(metadata_filter, self._cols) & self._live_mask()
-        return self._remove_rows(np.nonzero(hit)[0].tolist())
+        with self._lock:
+            n = len(self._records)
+            hit = F.evaluate(metadata_filter, self._cols) & self._live[:n]
+            return self._remove_tables(np.nonzero(hit)[0].tolist())
 
     def _clear_sync(self):
-        if self._index is not None:
-            self._index.close()
-        self._index, self.dim = None, None
-        self._records, self._id_to_row, self._doc_rows = [], {}, {}
-        self._cols.clear()
-        for p in self._paths():
-            if os.path.exists(p):
-                os.remove(p)
+        with self._lock:
+            if self._journal is not None:
+                self._journal.close()
+            if self._index is not None:
+                self._index.close()
+            self._reset_tables()
+            self._gen, self._journal = 0, None
+            for p in self._paths.all_files():
+                with contextlib.suppress(OSError):
+                    os.remove(p)
 
     async def clear(self) -> None:
         self._clear_sync()
@@ -237,56 +426,76 @@ class HipVectorStore(BaseVectorStore):
         """Drop the collection and its files (chroma_store.py:331, synchronous there too)."""
         self._clear_sync()
 
-    # ---------------------------------------------------------------- reads
-    def _live_mask(self) -> np.ndarray:
-        return np.array([rec is not None for rec in self._records], dtype=bool)
+    def close(self) -> None:
+        """Fold the journal into a snapshot and release the device index."""
+        with self._lock:
+            if self._journal is not None and self._journal.size:
+                self.flush()
+            if self._journal is not None:
+                self._journal.close()
+                self._journal = None
+            if self._index is not None:
+                self._index.close()
+                self._index = None
 
+    # ---------------------------------------------------------------- reads
     def _chunk(self, row: int, embedding=None) -> Chunk:
         rec = self._records[row]
         meta = rec["metadata"]
         return Chunk(id=rec["id"], document_id=meta.get("document_id", ""), content=rec["content"],
                      chunk_index=meta.get("chunk_index", 0), metadata=dict(meta), embedding=embedding)
 
-    def _filter_bitmap(self, filters: dict[str, Any] | None):
+    def filter_bitmap(self, filters: dict[str, Any] | None):
+        """uint64 row bitmap of a where-clause (None = no filter)."""
         if not filters:
             return None
-        return F.to_bitmap(F.evaluate(filters, self._cols))
+        return F.evaluate_words(filters, self._cols)
+
+    def _embeddings(self, rows: list[int]):
+        if self.keep_embeddings and self._raw is not None:
+            return self._raw[np.asarray(rows, np.int64)]
+        return self._index.get_rows(rows)
 
     def search_batch(self, query_embeddings, top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[list[tuple[Chunk, float]]]:
-        """Batched search: one GPU launch for all queries (used by BatchedVectorRetriever)."""
+        """Batched search: one GPU launch for all queries (BatchedVectorRetriever, the micro-batcher)."""
         q = np.asarray(query_embeddings, dtype=np.float32)
         if q.ndim == 1:
             q = q[None, :]
-        if self._index is None or self.count_sync() == 0:
-            return [[] for _ in range(len(q))]
-        if q.shape[1] != self.dim:
-            raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
-        # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
-        # search takes its exhaustive exact path (same results, one corpus pass per query)
-        if int(top_k) <= 0:
-            return [[] for _ in range(len(q))]
-        k = min(int(top_k), self.count_sync())
-        scores, rows = self._index.search(q, k, self._filter_bitmap(filters))
-        out = []
-        for b in range(len(q)):
-            valid = [(int(r), float(s)) for r, s in zip(rows[b], scores[b]) if r >= 0]
-            embs = None
-            if self.include_embeddings and valid:
-                embs = self._index.get_rows([r for r, _ in valid])
-            out.append([(self._chunk(r, None if embs is None else embs[i].tolist()), s)
-                        for i, (r, s) in enumerate(valid)])
-        return out
+        with self._lock:
+            if self._index is None or self.count_sync() == 0:
+                return [[] for _ in range(len(q))]
+            if q.shape[1] != self.dim:
+                raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
+            # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
+            # search takes its exhaustive exact path (same results, one corpus pass per query)
+            if int(top_k) <= 0:
+                return [[] for _ in range(len(q))]
+            k = min(int(top_k), self.count_sync())
+            scores, rows = self._index.search(q, k, self.filter_bitmap(filters))
+            out = []
+            for b in range(len(q)):
+                valid = [(int(r), float(s)) for r, s in zip(rows[b], scores[b]) if r >= 0]
+                embs = None
+                if self.include_embeddings and valid:
+                    embs = self._embeddings([r for r, _ in valid])
+                out.append([(self._chunk(r, None if embs is None else embs[i].tolist()), s)
+                            for i, (r, s) in enumerate(valid)])
+            return out
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:
-        return self.search_batch([query_embedding], top_k, filters)[0]
+        if int(top_k) <= 0:
+            return []
+        q = np.asarray(query_embedding, dtype=np.float32).reshape(-1)
+        return await self._batcher.search(q, top_k, filters)
 
     async def get_by_id(self, chunk_id: str) -> Chunk | None:
-        row = self._id_to_row.get(chunk_id)
-        if row is None:
-            return None
-        return self._chunk(row, self._index.get_rows([row])[0].tolist())
+        with self._lock:
+            row = self._id_to_row.get(chunk_id)
+            if row is None:
+                return None
+            return self._chunk(row, self._embeddings([row])[0].tolist())
 
     def count_sync(self) -> int:
         return len(self._id_to_row)

@@ -100,14 +100,23 @@ def test_ingestor_batches_across_documents_and_replaces_old_chunks(tmp_path):
     docs = [Document(id=f"doc{i}", content=" ".join(f"word{j}" for j in range(30 * i + 2)), metadata={"n": i})
             for i in range(6)]
     n = run(ing.ingest(docs))
-    assert n == run(store.count()) and sum(emb.batches) == n and max(emb.batches) == 4
+    # every document's chunks + its summary vector (processors.py:559-561, :423-464)
+    assert n + 6 == run(store.count()) and sum(emb.batches) == n + 6 and max(emb.batches) == 4
     assert all(b == 4 for b in emb.batches[:-1])
     c = run(store.get_by_id("doc3_chunk_0"))
     assert c.metadata["n"] == 3 and c.metadata["index_type"] == "index_content"
-    # re-ingesting a document replaces its chunks
+    sm = run(store.get_by_id("doc3_summary"))
+    assert sm.content == "doc3\n" and sm.chunk_index == -1
+    assert sm.metadata == {"document_id": "doc3", "chunk_index": -1, "n": 3, "index_type": "index_summary"}
+    # re-ingesting a document replaces its chunks and its summary
     before = run(store.count())
     old = len(store._doc_rows["doc5"])
-    m = run(ing.chunk_and_store(Document(id="doc5", content="short text", metadata={})))
-    assert run(store.count()) == before - old + m and len(store._doc_rows["doc5"]) == m
+    m = run(ing.chunk_and_store(Document(id="doc5", content="short text", metadata={"source": "s.pdf",
+                                                                                       "summary": "about x"})))
+    assert run(store.count()) == before - old + m + 1 and len(store._doc_rows["doc5"]) == m + 1
+    assert run(store.get_by_id("doc5_summary")).content == "s.pdf\nabout x"
+    no_sum = GpuIngestor(store, emb, summary_index=False)
+    assert run(no_sum.chunk_and_store(Document(id="doc9", content="a b c", metadata={}))) == 1
+    assert run(store.get_by_id("doc9_summary")) is None
     with pytest.raises(NotImplementedError):
         ing.split(Document(id="h", content="# x", metadata={"_use_hierarchical_splitter": True}))

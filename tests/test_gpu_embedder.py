@@ -67,7 +67,7 @@ def test_ingest_split_embed_add_query(tmp_path):
     cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
                             index_params={"dtype": "bf16", "persist": True})
     store = HipVectorStore(cfg)
-    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20))
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20), summary_index=False)
     seen = []  # the exact device vectors handed to the index
     inner = emb.embed_texts_device
     emb.embed_texts_device = lambda texts: seen.append(inner(texts)) or seen[-1]

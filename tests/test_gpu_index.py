@@ -709,3 +709,57 @@ def test_fuzz_filters_and_large_k_vs_oracle(native, case):
     s_ref, r_ref = oracle.c_search(stored, dtype, R.process_queries(q, metric), k,
                                    oracle.mask_from_bool(allowed & live), metric=metric)
     _check(s, r, s_ref, r_ref)
+
+
+# ---------------------------------------------------------------- query groups: > 64 queries per corpus pass
+@pytest.mark.parametrize("dim,dtype,n,B,k", [(1024, "bf16", 60_000, 256, 10), (768, "f16", 40_000, 200, 100),
+                                             (256, "bf16", 30_000, 65, 32), (1024, "bf16", 9_000, 128, 128),
+                                             (128, "f32", 20_000, 150, 10)])
+def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
+    """B > 64: ceil(B/64) workgroup groups stream the same tiles in one pass (one XCD per range
+    block), each with 64 queries in LDS; per-group private candidate regions, thresholds and
+    dynamic-tail counters.  Identical to the oracle, with and without a mask, and to the same
+    queries searched 64 at a time."""
+    rng = np.random.default_rng(dim + B + k)
+    idx = native.NativeIndex(dim, dtype, "cosine")
+    idx.add_synthetic(8, 0, n)
+    raw = R.gen_rows(8, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+    stored = oracle.c_build_synthetic(8, 0, n, dim, dtype, "cosine")
+    qn = R.process_queries(q, "cosine")
+    allowed = rng.random(n) < 0.6
+    for m in (None, allowed):
+        mk = None if m is None else oracle.mask_from_bool(m)
+        s, r = idx.search(q, k, mk)
+        _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk))
+        parts = [idx.search(q[i:i + 64], k, mk) for i in range(0, B, 64)]
+        np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))
+
+
+def test_query_groups_pipelined_vs_oracle(native):
+    """The bench's pipelined path at B = 256 and 128 (early SAMPLE, two workspaces, dual FILTER
+    streams) on a shard large enough for all of them: every batch identical to the oracle."""
+    torch = pytest.importorskip("torch")
+    from hiprag.dist import ShardedSearch
+
+    dim, n = 128, 1_300_000
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add_synthetic(29, 0, n)
+    raw = R.gen_rows(29, 0, n, dim)
+    stored = oracle.c_build_synthetic(29, 0, n, dim, "bf16", "cosine")
+    rng = np.random.default_rng(12)
+    plan = [(256, 10), (128, 100), (256, 10), (64, 10), (256, 32)]
+    qs = [np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+          for B, _ in plan]
+    q_dev = [torch.from_numpy(q).cuda() for q in qs]
+    outs = [(torch.empty((B, k), dtype=torch.float32, device="cuda"), torch.empty((B, k), dtype=torch.int64, device="cuda"))
+            for B, k in plan]
+    ready = torch.cuda.Event()
+    ready.record()
+    ss = ShardedSearch(idx, 0, max_batch=256, max_k=100, device=torch.device("cuda", 0))
+    for (B, k), q, (s_o, r_o) in zip(plan, q_dev, outs):
+        ss.submit(q, k, s_out=s_o, r_out=r_o, q_ready=ready)
+    ss.finalize_all()
+    torch.cuda.synchronize()
+    for (B, k), q, (s_o, r_o) in zip(plan, qs, outs):
+        _check(s_o.cpu().numpy(), r_o.cpu().numpy(), *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k))

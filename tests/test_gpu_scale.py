@@ -222,7 +222,7 @@ def test_c4_100k_chunk_ingest_then_retrieve(tmp_path):
     cfg = VectorStoreConfig(backend="hip", collection_name="kb100k", persist_directory=str(tmp_path),
                             index_params={"dtype": "bf16", "persist": True})
     store = HipVectorStore(cfg)
-    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20))
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=200, chunk_overlap=20), summary_index=False)
     seen = []
     inner = emb.embed_texts_device
     emb.embed_texts_device = lambda texts: seen.append(inner(texts)) or seen[-1]

@@ -326,6 +326,7 @@ extern "C" int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* met
 // ---------------------------------------------------------------- search pieces
 struct Plan {
     int QB, Bp, P;
+    int NG;  // query groups per corpus pass (each QB*32 queries in one workgroup's LDS); Bp = NG*QB*32
 };
 
 static int scan_lds_bytes(const hr_index* h, int QB) { return h->S * QB * 1024; }
@@ -335,7 +336,13 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     if (scan_lds_bytes(h, QB) > 160 * 1024)
         return set_err(HR_E_UNSUPPORTED, "dim too large for the LDS-resident query tile (max 2560)");
     p->QB = QB;
-    p->Bp = QB * 32;
+    // More than 64 queries: up to HIPRAG_MAX_GROUPS (default 4) groups of 64 share one corpus pass --
+    // each group's workgroups stream the same tiles on one XCD, the others reading them from L2
+    // (DESIGN.md "Query groups").  fp32 corpora (2 KiB k-steps) keep one group.
+    static const int mg_env = getenv("HIPRAG_MAX_GROUPS") ? atoi(getenv("HIPRAG_MAX_GROUPS")) : 4;
+    const int max_groups = std::max(1, std::min(8, mg_env));
+    p->NG = (QB == 2 && h->dtype != F32) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
+    p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
     const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
     p->P = (h->S % 16 == 0 && pmax >= 16) ? 16 : (h->S % 8 == 0 && pmax >= 8 ? 8 : 4);
@@ -344,12 +351,13 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     return HR_OK;
 }
 
-template <int MT, int DT, int QB, int P, int MODE>
+template <int MT, int DT, int QB, int P, int MODE, bool NT>
 static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
-    auto kern = k_scan<MT, DT, QB, P, MODE>;
+    const int ng = std::max(1, a.ng);
+    auto kern = k_scan<MT, DT, QB, P, MODE, NT>;
     static std::mutex attr_mu;
     static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
-    static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown)
+    static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown), per instantiation
     const int dev = h->device & 63;
     const int bucket = lds <= 40 * 1024 ? 0 : lds <= 80 * 1024 ? 1 : lds <= 120 * 1024 ? 2 : 3;
     int per_cu;
@@ -366,18 +374,23 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
         }
         per_cu = occ[dev][bucket];
     }
-    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * per_cu, (a.n_units + 7) / 8));
+    // blocks per query group (each group's workgroups cover the whole unit range); with several
+    // groups a multiple of 8, so the groups of one range block share blockIdx % 8 (k_scan)
+    int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * per_cu / ng, (a.n_units + 7) / 8));
+    if (ng > 1) blocks = std::max<int64_t>(8, blocks / 8 * 8);
     ScanArgs args = a;
+    args.ng = ng;
     if (MODE == SCAN_FILTER) {
-        const int64_t W = blocks * (kScanThreads / 64);
+        const int64_t W = blocks * (kScanThreads / 64);  // waves per group
         const int Bq = QB * 32;
-        HIP_TRY(sc.pbuf.ensure((size_t)Bq * W * kCapW * sizeof(float2)));
-        HIP_TRY(sc.pcnt.ensure((size_t)Bq * W * 4));
+        HIP_TRY(sc.pbuf.ensure((size_t)ng * Bq * W * kCapW * sizeof(float2)));
+        HIP_TRY(sc.pcnt.ensure((size_t)ng * Bq * W * 4));
         args.pbuf = sc.pbuf.as<float2>();
         args.pcnt = sc.pcnt.as<uint32_t>();
         args.capw = kCapW;
         sc.last_W = W;
         sc.last_Bp = Bq;
+        sc.last_ng = ng;
         h->last_scr = &sc;
         // dynamic tail: the last dyn_frac of the units go out in runs from the counter, but only
         // when every wave still gets a long static run (HIPRAG_DYN_PCT / HIPRAG_DYN_CHUNK: A/B)
@@ -394,7 +407,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
             args.dyn_q = sc.dyn_q.as<uint32_t>();
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kScanThreads), lds, st, args);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(blocks * ng)), dim3(kScanThreads), lds, st, args);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }
@@ -404,8 +417,10 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     int lds = scan_lds_bytes(h, pl.QB);
     // SAMPLE reduces its waves' group maxima in LDS: 8 waves x QB*16*64 floats + 8 part ids
     if (MODE == SCAN_SAMPLE) lds = std::max(lds, (kScanThreads / 64) * pl.QB * 16 * 64 * 4 + 64);
-#define HR_SCAN_CASE(QBv, Pv) \
-    if (pl.QB == QBv && pl.P == Pv) return launch_scan_t<MT, DT, QBv, Pv, MODE>(h, sc, cus, a, st, lds);
+#define HR_SCAN_CASE(QBv, Pv)                                                                     \
+    if (pl.QB == QBv && pl.P == Pv)                                                               \
+        return pl.NG > 1 ? launch_scan_t<MT, DT, QBv, Pv, MODE, false>(h, sc, cus, a, st, lds)    \
+                         : launch_scan_t<MT, DT, QBv, Pv, MODE, true>(h, sc, cus, a, st, lds);
     if constexpr (DT == F32) {
         HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
     } else {
@@ -545,7 +560,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     }
     const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
-    HIP_TRY(sc.qfrag.ensure((size_t)h->S * pl.QB * 1024));
+    HIP_TRY(sc.qfrag.ensure((size_t)pl.NG * h->S * pl.QB * 1024));
     HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
     // row parts for the group-max bound: 32 groups bound the 32nd best, so kc > 32 needs ceil(kc/32) parts
     const int np = mode == 0 ? (kc + 31) / 32 : 1;
@@ -557,7 +572,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(sc.sel_cnt.ensure((size_t)Bp * 4));
     HIP_TRY(sc.bound_approx.ensure((size_t)Bp * 4));
     HIP_TRY(sc.overflow.ensure((size_t)Bp * 4));
-    HIP_TRY(sc.dyn_q.ensure(256));
+    HIP_TRY(sc.dyn_q.ensure((size_t)std::max(4, pl.NG) * 64));
 
     const int MT = mfma_type(h->dtype);
     float* fl = (mode == 0 && !(dbg & 1)) ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
@@ -629,6 +644,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;
+    a.ng = pl.NG;
     if (n_vis > 0) {
         hr_index::ScanEvents ev{};
         // time the main pass only, not fallbacks, and only every time_every-th one: each event
@@ -716,7 +732,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const bool priv = a.private_bufs && n_vis > 0;
     hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), sort_cap * 8 + 16, st_tail, sc.cnt.as<uint32_t>(), sc.buf.as<float2>(),
                        kCap, priv ? sc.pcnt.as<uint32_t>() : nullptr, priv ? sc.pbuf.as<float2>() : nullptr,
-                       (int)sc.last_W, kCapW, Bp, sc.mkeys.as<uint32_t>(), np, sc.floor_q.as<float>(), a.use_groups, B, kc_sel,
+                       (int)sc.last_W, kCapW, pl.QB * 32, Bp, sc.mkeys.as<uint32_t>(), np, sc.floor_q.as<float>(), a.use_groups, B, kc_sel,
                        sc.sel_rows.as<uint32_t>(), sc.sel_cnt.as<int>(), sc.bound_approx.as<float>(),
                        sc.overflow.as<int>());
     HIP_TRY(hipGetLastError());
@@ -1403,14 +1419,16 @@ extern "C" int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* ma
     if (int rc = set_device(h)) return rc;
     // private per-wave counts of the last FILTER scan: pcnt[W][Bp]
     const Scratch* sc = h->last_scr;
-    const int64_t n = sc ? sc->last_W * sc->last_Bp : 0;
+    // layout [group][W][Bq]
+    const int64_t per_group = sc ? sc->last_W * sc->last_Bp : 0, ng = sc ? sc->last_ng : 1;
+    const int64_t n = per_group * ng;
     std::vector<uint32_t> c((size_t)n);
     if (n) {
         HIP_TRY(hipDeviceSynchronize());
         HIP_TRY(hipMemcpy(c.data(), sc->pcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     }
-    std::vector<int64_t> per_q((size_t)(sc ? sc->last_Bp : 0), 0);
-    for (int64_t i = 0; i < n; ++i) per_q[(size_t)(i % sc->last_Bp)] += c[(size_t)i];
+    std::vector<int64_t> per_q((size_t)(sc ? sc->last_Bp * ng : 0), 0);
+    for (int64_t i = 0; i < n; ++i) per_q[(size_t)((i / per_group) * sc->last_Bp + i % sc->last_Bp)] += c[(size_t)i];
     int64_t t = 0, m = 0;
     for (int64_t v : per_q) {
         t += v;

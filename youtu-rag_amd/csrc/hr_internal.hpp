@@ -73,7 +73,8 @@ static constexpr int kScanThreads = 512;
 struct Scratch {
     DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q,
         tl, tl_tmp;  // device-mask tile list (+ its count after the list) and its rocPRIM scratch
-    int64_t last_W = 0, last_Bp = 0;  // waves and padded batch of the most recent FILTER launch
+    int64_t last_W = 0, last_Bp = 0;  // waves (per query group) and queries per group of the most recent FILTER
+    int last_ng = 1;                  // query groups of that launch
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
     hipEvent_t sampled = nullptr;     // pre stream: this set's early query prep + SAMPLE are done

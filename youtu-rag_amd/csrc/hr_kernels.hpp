@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     if (mkeys && lane < 32)
         for (int p = 0; p < np; ++p) mkeys[((int64_t)p * Bp + b) * 32 + lane] = HR_KEY_NEG_INF;
     if (lane == 0) {
-        if (dyn_q && b == 0) *dyn_q = 0;
+        if (dyn_q && (b % (QB * 32)) == 0) dyn_q[(b / (QB * 32)) * 16] = 0;  // one counter per query group
         if (cnt) cnt[b] = 0;
         if (floor_q) floor_q[b] = real ? -__builtin_inff() : __builtin_inff();
     }
@@ -183,14 +183,15 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
         }
     }
     double e1 = 0.0, nh = 0.0, qn = 0.0;
-    const int qb = b >> 5;
+    // A-fragment layout [group][S][QB][64 lanes][8]: a group = the QB*32 queries one scan workgroup stages
+    const int qg = (b >> 5) / QB, qb = (b >> 5) % QB;
     auto put = [&](int d, float x) {
         const float y = scale ? (float)((double)x * inv) : x;
         q32[(int64_t)b * dpad + d] = y;
         const uint16_t h = quant_mt<MT>(y);
         const float dq = dequant_mt<MT>(h);
         const int s = d >> 4, sl = (b & 31) + 32 * ((d >> 3) & 1), jj = d & 7;
-        qfrag[(((int64_t)s * QB + qb) * 64 + sl) * 8 + jj] = h;
+        qfrag[((((int64_t)qg * S + s) * QB + qb) * 64 + sl) * 8 + jj] = h;
         const double e = (double)y - (double)dq;
         e1 += e * e;
         nh += (double)dq * (double)dq;
@@ -269,6 +270,9 @@ struct ScanArgs {
     const float* xnorm;
     // diagnostics (HIPRAG_STAMPS): per-wave wall-clock stamps {entry, staged, end, tiles}, nullable
     unsigned long long* stamps;
+    // query groups (more than QB*32 queries per corpus pass): ng workgroups stream the same tile range,
+    // each with its own QB*32 queries in LDS; per-query tables hold ng consecutive groups
+    int ng;
 };
 
 
@@ -282,43 +286,45 @@ __device__ inline f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c)
                                                        0, 0);
 }
 
-// X fragment of k-step chunk c (flattened tile*S + s) for this lane, converted to MT
-template <int MT, int DT>
+// X fragment of k-step chunk c (flattened tile*S + s) for this lane, converted to MT.
+// NT: non-temporal corpus loads (every byte read once per launch); query groups (ng > 1) use the
+// default policy instead, so the other groups of a range block find the tiles in the XCD's L2.
+template <int MT, int DT, bool NT = true>
 struct XFrag;
 // corpus stream loads: every byte is read once per launch, so they go out non-temporal
 // (HR_CORPUS_NT=0 builds the default-policy variant for A/B timing)
 #ifndef HR_CORPUS_NT
 #define HR_CORPUS_NT 1
 #endif
+template <bool NT>
 __device__ inline u32x4 corpus_load(const uint8_t* p) {
 #if HR_CORPUS_NT
-    return __builtin_nontemporal_load((const u32x4*)p);
-#else
-    return *(const u32x4*)p;
+    if constexpr (NT) return __builtin_nontemporal_load((const u32x4*)p);
 #endif
+    return *(const u32x4*)p;
 }
-template <int MT>
-struct XFrag<MT, BF16> {
+template <int MT, bool NT>
+struct XFrag<MT, BF16, NT> {
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        v = corpus_load(rows + c * 1024 + lane * 16);
+        v = corpus_load<NT>(rows + c * 1024 + lane * 16);
     }
     __device__ inline u32x4 get() const { return v; }
 };
-template <int MT>
-struct XFrag<MT, F16> {
+template <int MT, bool NT>
+struct XFrag<MT, F16, NT> {
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        v = corpus_load(rows + c * 1024 + lane * 16);
+        v = corpus_load<NT>(rows + c * 1024 + lane * 16);
     }
     __device__ inline u32x4 get() const { return v; }
 };
-template <int MT>
-struct XFrag<MT, F32> {
+template <int MT, bool NT>
+struct XFrag<MT, F32, NT> {
     u32x4 a, b;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
-        a = corpus_load(rows + c * 2048 + lane * 16);
-        b = corpus_load(rows + c * 2048 + 1024 + lane * 16);
+        a = corpus_load<NT>(rows + c * 2048 + lane * 16);
+        b = corpus_load<NT>(rows + c * 2048 + 1024 + lane * 16);
     }
     // fp32 corpus -> MFMA operand: packed hardware RNE conversion (v_cvt_pk_*).  Only the
     // error-bounded approximate score depends on it (the exact rescoring reads fp32).
@@ -346,7 +352,7 @@ __device__ inline int acc_query(int qb, int i, int half) { return qb * 32 + (i &
 // shared per-query buffer with atomic slot reservation; the exact fallback)
 enum { SCAN_SAMPLE = 0, SCAN_FILTER = 1, SCAN_COLLECT = 2 };
 
-template <int MT, int DT, int QB, int P, int MODE>
+template <int MT, int DT, int QB, int P, int MODE, bool NT = true>
 __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     constexpr bool FILTER = MODE != SCAN_SAMPLE;
     constexpr bool priv = MODE == SCAN_FILTER;
@@ -356,12 +362,31 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const int half = lane >> 5;
     const int g = lane & 31;
 
-    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6);  // slot of this wave's outputs
+    // Query groups: workgroup bx serves group grp of range block rb.  The ng workgroups of one range
+    // block have equal bx % 8 -- one XCD under the round-robin dispatch (speed only, never
+    // correctness) -- and walk the same tiles in the same order, so each corpus tile comes from HBM
+    // once and from that XCD's L2 for the other groups.  ng == 1: rb = bx, grp = 0.
+    const int ng = a.ng;
+    const int bx = blockIdx.x;
+    const int grp = ng > 1 ? (bx >> 3) % ng : 0;
+    const int64_t nrb = gridDim.x / ng;
+    const int64_t rb = ng > 1 ? (int64_t)((bx >> 3) / ng) * 8 + (bx & 7) : bx;
+    {
+        constexpr int Bq = QB * 32;
+        a.qfrag += (int64_t)grp * a.S * QB * 64 * 8;
+        a.mkeys += grp * Bq * 32;
+        a.floor_q += grp * Bq;
+        if (a.cnt) a.cnt += grp * Bq;
+        if (a.buf) a.buf += (int64_t)grp * Bq * a.cap;
+        if (a.dyn_q) a.dyn_q += grp * 16;
+    }
+    const int64_t W = nrb * (blockDim.x >> 6);  // waves per group
+    const int64_t w = rb * (blockDim.x >> 6) + (tid >> 6);  // slot of this wave's outputs within the group
+    const int64_t wg = (int64_t)grp * W + w;                // ... over all groups
     // unit range: contiguous per wave, numbered wave-major across workgroups so the waves that
     // get one extra unit sit on different CUs (the tail is then one tile per CU, not a
     // handful of fully loaded CUs finishing a tile after everyone else)
-    const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * gridDim.x + blockIdx.x : w;
+    const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * nrb + rb : w;
     const bool dyn = MODE == SCAN_FILTER && a.dyn_start < a.n_units;  // launch-uniform
     const int64_t n_static = dyn ? a.dyn_start : a.n_units;
     const int64_t base = n_static / W, rem = n_static % W;
@@ -378,7 +403,7 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
 
     // first loads of the corpus stream go out before the query staging, so their HBM latency
     // overlaps it
-    XFrag<MT, DT> ring[P];
+    XFrag<MT, DT, NT> ring[P];
     if (u0 < u1) {
         const int64_t c0 = tile_at(u0) * S;
 #pragma unroll
@@ -392,11 +417,11 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
     const unsigned long long t_staged = a.stamps ? wall_clock64() : 0ull;
 
     if (u0 >= u1 && FILTER) {
-        if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = 0;
+        if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = 0;
         return;
     }  // an idle SAMPLE wave stays: it takes part in the workgroup reduction below
     uint32_t mycnt = 0;  // private mode: lane q counts the candidates of query q in this wave
-    float2* const wave_buf = priv ? a.pbuf + w * (QB * 32) * a.capw : nullptr;
+    float2* const wave_buf = priv ? a.pbuf + wg * (QB * 32) * a.capw : nullptr;
 
     const u32x4* qs = (const u32x4*)lds;
 
@@ -631,12 +656,12 @@ __global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
         }
     }
 
-    if (priv && lane < QB * 32) a.pcnt[w * (QB * 32) + lane] = mycnt;
+    if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = mycnt;
     if (a.stamps && lane == 0) {
-        a.stamps[4 * w] = t_entry;
-        a.stamps[4 * w + 1] = t_staged;
-        a.stamps[4 * w + 2] = wall_clock64();
-        a.stamps[4 * w + 3] = (unsigned long long)done;
+        a.stamps[4 * wg] = t_entry;
+        a.stamps[4 * wg + 1] = t_staged;
+        a.stamps[4 * wg + 2] = wall_clock64();
+        a.stamps[4 * wg + 3] = (unsigned long long)done;
     }
     if (!FILTER && a.publish) {  // (publish == 0: timing experiments only)
         // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope
@@ -743,7 +768,7 @@ constexpr int kRankMax = 1024;  // candidate sets up to this size are ranked by 
 
 static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,
                                                  int cap, const uint32_t* __restrict__ pcnt,
-                                                 const float2* __restrict__ pbuf, int W, int capw, int Bp,
+                                                 const float2* __restrict__ pbuf, int W, int capw, int Bq, int Bp,
                                                  const uint32_t* __restrict__ mkeys, int np,
                                                  const float* __restrict__ floor_q, int use_groups, int B, int kc,
                                                  uint32_t* __restrict__ sel_rows, int* __restrict__ sel_cnt,
@@ -784,12 +809,14 @@ static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(
                 ovf = true;
         }
     };
-    if (pcnt) {  // private per-wave regions of the FILTER scan
+    if (pcnt) {  // private per-wave regions of the FILTER scan: [group][W][Bq] (the query's group only)
+        const int64_t gw0 = (int64_t)(q / Bq) * W;
+        const int ql = q % Bq;
         for (int w = tid; w < W; w += blockDim.x) {
-            const uint32_t c = pcnt[(int64_t)w * Bp + q];
+            const uint32_t c = pcnt[(gw0 + w) * Bq + ql];
             if (c > (uint32_t)capw) ovf = true;
             const int n = c < (uint32_t)capw ? (int)c : capw;
-            for (int j = 0; j < n; ++j) push(pbuf[((int64_t)w * Bp + q) * capw + j]);
+            for (int j = 0; j < n; ++j) push(pbuf[((gw0 + w) * Bq + ql) * capw + j]);
         }
     } else {
         const uint32_t c = cnt[q];

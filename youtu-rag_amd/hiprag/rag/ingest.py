@@ -11,6 +11,11 @@ What changes is where the vectors go: with the in-process TorchRocmEmbedder, tex
 many documents are packed into full embedder batches and each batch's (B, H) float32
 device tensor is appended to the index by hr_index_add_device -- the embeddings never
 visit the host.  Any other BaseEmbedder (host lists) falls back to add_chunks.
+After a document's chunks, its summary vector is added as the reference's simple-document
+processor does (processors.py:559-561 -> _create_summary_index :423-464): one chunk
+``f"{doc}_summary"`` with content ``f"{source or doc id}\n{summary}"``, chunk_index -1 and the
+document's whole metadata (``_``-keys included, as the reference stores them) plus
+index_type="index_summary" -- the vectors kb_file_search searches (kb_search_toolkit.py:530-535).
 HierarchicalMarkdownSplitter documents ("_use_hierarchical_splitter") are outside
 this slice and are rejected loudly.
 """
@@ -24,6 +29,14 @@ from .chunker import RecursiveTextSplitter
 from .config import ChunkingConfig
 
 logger = logging.getLogger(__name__)
+
+
+def summary_chunk(document: Document) -> Chunk:
+    """The document's summary-index record (processors.py:423-464)."""
+    meta = document.metadata or {}
+    content = f"{meta.get('source', document.id)}\n{meta.get('summary') or ''}"
+    return Chunk(id=f"{document.id}_summary", document_id=document.id, content=content, chunk_index=-1,
+                 metadata={**meta, "index_type": "index_summary"})
 
 
 def make_chunks(document: Document, texts: list[str], metadata: dict[str, Any] | None = None) -> list[Chunk]:
@@ -44,8 +57,9 @@ class GpuIngestor:
     """split -> embed -> add for a HipVectorStore, batching embedder work across documents."""
 
     def __init__(self, vector_store, embedder: BaseEmbedder, chunker=None, chunking: ChunkingConfig | None = None,
-                 embed_batch: int | None = None):
+                 embed_batch: int | None = None, summary_index: bool = True):
         self.vector_store = vector_store
+        self.summary_index = bool(summary_index)
         self.embedder = embedder
         self.chunker = chunker or RecursiveTextSplitter(chunking or ChunkingConfig())
         self.embed_batch = int(embed_batch or getattr(embedder, "batch_size", 64))
@@ -98,4 +112,6 @@ class GpuIngestor:
         if not chunks:
             logger.warning("no chunks created for document %s", doc.id)
         pending.extend(chunks)
+        if self.summary_index:  # created even when the document gave no chunks (processors.py:559-561)
+            pending.append(summary_chunk(doc))
         return len(chunks)

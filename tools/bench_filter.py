@@ -93,7 +93,65 @@ def pipelined(n=10_000_000):
         print(f"pipelined {name:28s} {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS", flush=True)
 
 
+def store(n=10_000_000):
+    """Where-clauses through the drop-in store: HipVectorStore.search_batch(filters=...) at n rows of
+    1000-chunk documents (+ one summary row each), the filters kb_file_search / kb_embedding_search
+    build.  Reports the where -> bitmap compile time (first call, then cached) and the end-to-end
+    search time per 64-query batch."""
+    from hiprag.rag import HipVectorStore, VectorStoreConfig
+    from hiprag.rag import filters as F
+
+    D, B, K = 1024, 64, 10
+    idx = _native.NativeIndex(D, "bf16", "cosine")
+    idx.reserve(n)
+    idx.add_synthetic(0, 0, n)
+    cfg = VectorStoreConfig(backend="hip", collection_name="bench", persist_directory="/tmp/hiprag_bench",
+                            index_params={"dtype": "bf16", "persist": False})
+    st = HipVectorStore(cfg, index_factory=lambda d: idx)
+    st._ensure_index(D)
+    t0 = time.perf_counter()
+    recs = []
+    for r in range(n):
+        d, i = divmod(r, 1000)
+        recs.append({"id": f"doc{d}_chunk_{i}", "document_id": f"doc{d}", "content": "", "chunk_index": i,
+                     "metadata": {"document_id": f"doc{d}", "chunk_index": i, "source": f"file_{d % 5000}.pdf",
+                                  "index_type": "index_summary" if i == 999 else "index_content"}})
+        if len(recs) == 1_000_000:
+            st._append_tables(recs, None)
+            recs = []
+    if recs:
+        st._append_tables(recs, None)
+    print(f"host tables for {n} rows in {time.perf_counter() - t0:.1f}s", flush=True)
+    q, _ = synth.planted_queries(0, n, D, B, qseed=7)
+    cases = [("none", None), ("index_type == index_summary (kb_file_search)", {"index_type": {"$eq": "index_summary"}}),
+             ("source $in 2 files", {"source": {"$in": ["file_17.pdf", "file_4000.pdf"]}}),
+             ("document_id == doc777", {"document_id": "doc777"}),
+             ("summary AND source $in", {"$and": [{"source": {"$in": ["file_1.pdf", "file_2.pdf"]}},
+                                                  {"index_type": {"$eq": "index_summary"}}]}),
+             ("chunk_index < 500 (dense)", {"chunk_index": {"$lt": 500}})]
+    for name, f in cases:
+        t0 = time.perf_counter()
+        if f:
+            F.evaluate_words(f, st._cols)
+        first = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        if f:
+            for _ in range(10):
+                F.evaluate_words(f, st._cols)
+        cached = (time.perf_counter() - t0) * 1e3 / 10
+        st.search_batch(q, K, f)
+        t0 = time.perf_counter()
+        for _ in range(10):
+            res = st.search_batch(q, K, f)
+        ms = (time.perf_counter() - t0) * 1e3 / 10
+        print(f"store {name:46s} compile first {first:7.2f} ms, cached {cached:6.3f} ms; search_batch {ms:8.3f} "
+              f"ms/batch ({sum(len(r) for r in res) / B:.1f} hits/query)", flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("STORE") == "1":
+        store(int(float(sys.argv[1])) if len(sys.argv) > 1 else 10_000_000)
+        sys.exit(0)
     if os.environ.get("PIPELINED") == "1":
         pipelined(int(float(sys.argv[1])) if len(sys.argv) > 1 else 10_000_000)
         sys.exit(0)

@@ -156,8 +156,12 @@ class MetadataColumns:
         if op == "in":  # arg: frozenset of codes
             if not arg:
                 return np.zeros(r1 - r0, bool)
-            if len(arg) == 1:
-                return codes == next(iter(arg))
+            if len(arg) <= 8:  # a few values ($in of some files): OR of compares beats np.isin's sort
+                it = iter(arg)
+                out = codes == next(it)
+                for c in it:
+                    out |= codes == c
+                return out
             return np.isin(codes, np.fromiter(arg, np.int32, len(arg)))
         with np.errstate(invalid="ignore"):
             return _CMP[op](c.num[r0:r1], arg)  # NaN (absent / not a number) compares False

@@ -13,10 +13,13 @@ torch.distributed.run (one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
 
 Inputs are resident in HBM before the timed region: every rank generates its shard
 on its GPU with the counter-based generator (hiprag.synth) and all query batches
-are uploaded up front.  ``cpu_baseline`` (rank 0, N=1 only) times the CPU oracle's
-exact search (oracle/, test infrastructure) on a bounded row sample and scales it
-to the full corpus; ``recall_at_10`` compares the GPU's first batch with the oracle's
-exact answer over the FULL corpus for a few queries.
+are uploaded up front.  ``cpu_baseline`` (rank 0, N=1 only) times the reference's CPU
+search path (FAISS IndexFlatIP semantics = BLAS sgemm + top-k over the fp32 store, its
+per-query loop and the CPU query embedding) on a bounded row sample and scales it to the
+full corpus; ``cpu_oracle`` times the exact fp64 checker (oracle/, test infrastructure);
+``recall_at_10`` compares the GPU's first batch with the oracle's exact answer over the
+FULL corpus for a few queries.  ``--single-process`` runs one process with one index handle
+striped over the GPUs instead (hr_index_create with n_dev > 1).
 """
 from __future__ import annotations
 
@@ -55,6 +58,8 @@ def parse():
     p.add_argument("--cpu-embed-preset", default="bge-large")
     p.add_argument("--recall-queries", type=int, default=4)
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
+    p.add_argument("--single-process", action="store_true",
+                   help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()
 
 
@@ -178,8 +183,68 @@ def cpu_reference_baseline(args, qbatches, N, D, K, B):
     return out
 
 
+def main_single_process(args):
+    """--single-process: ONE process, ONE index handle over --gpus devices (hr_index_create with
+    n_dev > 1: rows striped over the GPUs by tile, per-shard scans on every device at once, the
+    candidates peer-copied to device 0 and merged there) -- the reference's deployment shape (one
+    FastAPI process, one store per collection).  Batches run synchronously through
+    hr_index_search_device; same JSON line as the multi-process path."""
+    import torch
+
+    from hiprag import _native, synth
+
+    n_vis = torch.cuda.device_count()
+    devs = [i % max(1, n_vis) for i in range(args.gpus)]
+    N, D, B, K = args.rows, args.dim, args.batch, args.k
+    torch.cuda.set_device(devs[0])
+    dev = torch.device("cuda", devs[0])
+    t0 = time.time()
+    index = _native.NativeIndex(D, args.dtype, "cosine", devices=devs)
+    index.reserve(N)
+    index.add_synthetic(args.seed, 0, N)
+    torch.cuda.synchronize()
+    log(f"one handle over devices {devs}: {N} rows built in {time.time() - t0:.1f}s")
+    n_batches = args.warmup + args.steps
+    q_dev = torch.from_numpy(np.stack([synth.planted_queries(args.seed, N, D, B, qseed=1000 + i)[0]
+                                       for i in range(n_batches)])).to(dev)
+    s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
+    r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for i in range(args.warmup):
+        index.search_device(q_dev[i].data_ptr(), B, K, s_dev[i].data_ptr(), r_dev[i].data_ptr(), stream=st)
+    for d in set(devs):
+        torch.cuda.synchronize(d)
+    t_start = time.perf_counter()
+    for i in range(args.warmup, n_batches):
+        index.search_device(q_dev[i].data_ptr(), B, K, s_dev[i].data_ptr(), r_dev[i].data_ptr(), stream=st)
+    for d in set(devs):
+        torch.cuda.synchronize(d)
+    elapsed = time.perf_counter() - t_start
+    result = {"metric": METRIC, "value": round(args.steps * B / elapsed, 2), "unit": "queries/s",
+              "n_gpus": len(set(devs)), "steps": args.steps, "warmup": args.warmup,
+              "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+              "vs_baseline": None, "dtype": args.dtype,
+              "data": "synthetic: counter-based corpus generator (hiprag.synth), planted queries",
+              "config": {"workload": f"{N / 1e6:g}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, one handle "
+                                     f"striped over {len(devs)} shards", "rows": N, "dim": D, "batch": B, "k": K,
+                         "parallelism": f"onehandle{len(devs)}", "devices": devs}}
+    if not args.no_cpu:
+        import oracle
+        from oracle import ref_numpy as R
+
+        nq = min(args.recall_queries, B)
+        s_ref, r_ref = oracle.c_search_synthetic(args.seed, 0, N, D, args.dtype, "cosine",
+                                                 R.process_queries(q_dev[args.warmup, :nq].cpu().numpy(), "cosine"), K)
+        got = r_dev[args.warmup, :nq].cpu().numpy()
+        result["ids_identical"] = bool(np.array_equal(got, r_ref))
+        result["recall_at_10"] = float(np.mean([len(set(got[i]) & set(r_ref[i])) / K for i in range(nq)]))
+    print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
+    if args.single_process:
+        return main_single_process(args)
     import torch
     import torch.distributed as dist
 

@@ -134,3 +134,42 @@ def test_fused_layernorm_embedder_matches_unfused(dtype, atol):
     plain = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=4, fused_layernorm=False)
     assert fused.fused_layers == 24 and plain.fused_layers == 0
     torch.testing.assert_close(fused.encode_passages(texts), plain.encode_passages(texts), rtol=0, atol=atol)
+
+
+def test_ingest_writes_summary_vectors_that_kb_file_search_finds(tmp_path):
+    """GpuIngestor adds each document's index_summary vector (processors.py:423-464), so the KB tools'
+    kb_file_search (kb_search_toolkit.py:446-676) over a hiprag-built KB returns the files: every
+    returned file's summary row is the exact top hit among the summary rows (oracle, same vectors)."""
+    import json
+
+    from hiprag.rag.kb_tools import KBSearchToolkit
+
+    emb = TorchRocmEmbedder(preset="tiny", batch_size=64, max_length=96, seed=5)
+    cfg = VectorStoreConfig(backend="hip", collection_name="kbsum", persist_directory=str(tmp_path),
+                            index_params={"dtype": "bf16", "persist": False})
+    store = HipVectorStore(cfg)
+    seen = []
+    inner = emb.embed_texts_device
+    emb.embed_texts_device = lambda texts: seen.append(inner(texts)) or seen[-1]
+    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=150, chunk_overlap=10))
+    rng = np.random.default_rng(4)
+    words = [f"w{i}" for i in range(300)]
+    docs = [Document(id=f"doc{d}", content=". ".join(" ".join(rng.choice(words, 8)) for _ in range(12)),
+                     metadata={"source": f"file_{d}.pdf", "summary": " ".join(rng.choice(words, 10))})
+            for d in range(30)]
+    asyncio.run(ing.ingest(docs))
+    recs = store._records
+    summ_rows = [i for i, r in enumerate(recs) if r["metadata"].get("index_type") == "index_summary"]
+    assert len(summ_rows) == 30 and all(recs[i]["id"].endswith("_summary") for i in summ_rows)
+    tk = KBSearchToolkit(config={}, kb_resolver=lambda kb: ("kbsum", "kb"), store_factory=lambda c: store)
+    tk._embedder_cache = emb
+    out = json.loads(asyncio.run(tk.kb_file_search(kb_id=1, query=docs[7].metadata["summary"], top_k=5,
+                                                   auto_rerank=False)))
+    assert out["total_files"] == 5 and len(out["files"]) == 5
+    vecs = torch.cat(seen).cpu().numpy()
+    stored = R.process_rows(vecs, "cosine", "bf16")
+    qv = R.process_queries(emb.encode_queries([docs[7].metadata["summary"]]).cpu().numpy(), "cosine")
+    allowed = np.zeros(len(recs), bool)
+    allowed[summ_rows] = True
+    s_ref, r_ref = oracle.c_search(stored, "bf16", qv, 5, oracle.mask_from_bool(allowed))
+    assert [f["file_name"] for f in out["files"]] == [recs[r]["metadata"]["source"] for r in r_ref[0]]

@@ -1,0 +1,111 @@
+// stream_ceiling.hip -- the practical read-only HBM streaming ceiling of one MI355X, for the scan's
+// roofline.  Reads a buffer of the scan's size (default 20.48 GB = 10M x 1024 bf16)
+// once per launch with the scan's access shape: every wave streams a contiguous range of 1 KiB
+// chunks, one 16-byte load per lane, a ring of P loads in flight, a trivial reduction so nothing is
+// optimised away.  Variants: non-temporal vs default-policy loads, all CUs vs the scan's n_cu - 32,
+// 8 or 16 waves per CU.  Prints one line per variant: bytes / (average launch time from HIP events).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_ceiling.hip -o tools/stream_ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                                   \
+    do {                                                                                           \
+        hipError_t e = (x);                                                                        \
+        if (e != hipSuccess) {                                                                     \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                            \
+            std::exit(1);                                                                          \
+        }                                                                                          \
+    } while (0)
+
+template <bool NT, int P>
+__global__ __launch_bounds__(512) void k_stream(const u32x4* __restrict__ src, long long n_chunks,
+                                               unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const long long W = (long long)gridDim.x * (blockDim.x >> 6);
+    const long long w = (long long)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;  // wave-major, as the scan
+    const long long base = n_chunks / W, rem = n_chunks % W;
+    const long long c0 = w * base + (w < rem ? w : rem);
+    const long long c1 = c0 + base + (w < rem ? 1 : 0);
+    u32x4 ring[P];
+    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+        ring[i] = (c0 + i < c1) ? (NT ? __builtin_nontemporal_load(src + (c0 + i) * 64 + lane) : src[(c0 + i) * 64 + lane])
+                                : u32x4{0u, 0u, 0u, 0u};
+    // branch-free main loop while a whole ring of prefetches stays inside the range, then the rest
+    long long c = c0;
+    for (; c + 2 * P <= c1; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            acc ^= ring[i];
+            ring[i] = NT ? __builtin_nontemporal_load(src + (c + P + i) * 64 + lane) : src[(c + P + i) * 64 + lane];
+        }
+    }
+    for (; c < c1; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            if (c + i < c1) acc ^= ring[i];
+            const long long nx = c + P + i;
+            if (nx < c1) ring[i] = NT ? __builtin_nontemporal_load(src + nx * 64 + lane) : src[nx * 64 + lane];
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;  // never true in practice
+}
+
+template <bool NT, int P>
+static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    hipLaunchKernelGGL((k_stream<NT, P>), dim3(blocks), dim3(threads), 0, 0, buf, n_chunks, sink);  // warm
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a, 0));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_stream<NT, P>), dim3(blocks), dim3(threads), 0, 0, buf, n_chunks, sink);
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const double gb = argc > 1 ? atof(argv[1]) : 20.48;
+    const long long bytes = (long long)(gb * 1e9) / 1024 * 1024;
+    const long long n_chunks = bytes / 1024;
+    hipDeviceProp_t prop;
+    CHECK(hipGetDeviceProperties(&prop, 0));
+    const int n_cu = prop.multiProcessorCount;
+    u32x4* buf = nullptr;
+    unsigned* sink = nullptr;
+    CHECK(hipMalloc(&buf, bytes));
+    CHECK(hipMalloc(&sink, 4));
+    CHECK(hipMemset(buf, 1, bytes));
+    CHECK(hipDeviceSynchronize());
+    const int reps = 10;
+    struct V { const char* name; bool nt; int cus; int threads; };
+    for (const V& v : std::vector<V>{{"nt, ring 32, n_cu-32 CUs, 8 waves/CU", true, n_cu - 32, 512}}) {
+        const double ms = run<true, 32>(buf, n_chunks, sink, v.cus, v.threads, reps);
+        std::printf("{\"variant\": \"%s\", \"bytes\": %lld, \"ms\": %.4f, \"TBps\": %.4f, \"frac_of_8TBps\": %.4f}\n",
+                    v.name, bytes, ms, bytes / (ms * 1e-3) / 1e12, bytes / (ms * 1e-3) / 8e12);
+    }
+    std::vector<V> vs = {{"nt, n_cu-32 CUs, 8 waves/CU (the scan's launch)", true, n_cu - 32, 512},
+                         {"nt, all CUs, 8 waves/CU", true, n_cu, 512},
+                         {"default policy, n_cu-32 CUs, 8 waves/CU", false, n_cu - 32, 512},
+                         {"nt, all CUs, 16 waves/CU (2 blocks/CU)", true, 2 * n_cu, 512}};
+    for (const V& v : vs) {
+        const double ms = v.nt ? run<true, 16>(buf, n_chunks, sink, v.cus, v.threads, reps)
+                               : run<false, 16>(buf, n_chunks, sink, v.cus, v.threads, reps);
+        std::printf("{\"variant\": \"%s\", \"bytes\": %lld, \"ms\": %.4f, \"TBps\": %.4f, \"frac_of_8TBps\": %.4f}\n",
+                    v.name, bytes, ms, bytes / (ms * 1e-3) / 1e12, bytes / (ms * 1e-3) / 8e12);
+    }
+    CHECK(hipFree(buf));
+    CHECK(hipFree(sink));
+    return 0;
+}

@@ -351,10 +351,10 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     return HR_OK;
 }
 
-template <int MT, int DT, int QB, int P, int MODE, bool NT>
+template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
 static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
     const int ng = std::max(1, a.ng);
-    auto kern = k_scan<MT, DT, QB, P, MODE, NT>;
+    auto kern = k_scan<MT, DT, QB, P, MODE, NT, TPB>;
     static std::mutex attr_mu;
     static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
     static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown), per instantiation
@@ -369,7 +369,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
         }
         if (!occ[dev][bucket]) {
             int o = 0;
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kScanThreads, lds));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, TPB, lds));
             occ[dev][bucket] = std::max(1, o);
         }
         per_cu = occ[dev][bucket];
@@ -381,7 +381,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
     ScanArgs args = a;
     args.ng = ng;
     if (MODE == SCAN_FILTER) {
-        const int64_t W = blocks * (kScanThreads / 64);  // waves per group
+        const int64_t W = blocks * (TPB / 64);  // waves per group
         const int Bq = QB * 32;
         HIP_TRY(sc.pbuf.ensure((size_t)ng * Bq * W * kCapW * sizeof(float2)));
         HIP_TRY(sc.pcnt.ensure((size_t)ng * Bq * W * 4));
@@ -407,7 +407,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
             args.dyn_q = sc.dyn_q.as<uint32_t>();
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(blocks * ng)), dim3(kScanThreads), lds, st, args);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(blocks * ng)), dim3(TPB), lds, st, args);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }

@@ -27,7 +27,10 @@ namespace {
 // Exact canonical fp64 score of every (query, centroid) pair (oracle order: lane-strided partial
 // sums + butterfly).  A 1024-thread workgroup = 16 waves = 16 centroids; the processed queries
 // are staged through LDS up to 32 at a time (128 KiB at dpad 1024), so L2 serves each query once per
-// workgroup instead of once per wave.
+// workgroup instead of once per wave.  CJ > 0: the wave's centroid row (CJ = dpad/64 values per lane)
+// is held in registers for all queries -- re-loading it from memory inside the query loop made every
+// iteration wait one memory round trip (165 us per 64 x 8192 x 1024 batch, latency-bound).
+template <int CJ>
 __global__ __launch_bounds__(1024) void k_coarse(const float* __restrict__ cent, int nlist, int dpad,
                                                  const float* __restrict__ q32, int B, int qgroup,
                                                  Cand* __restrict__ out) {
@@ -35,6 +38,16 @@ __global__ __launch_bounds__(1024) void k_coarse(const float* __restrict__ cent,
     const int lane = threadIdx.x & 63;
     const int l = blockIdx.x * 16 + (threadIdx.x >> 6);
     const float* c = cent + (int64_t)(l < nlist ? l : 0) * dpad;
+    double cr[CJ > 0 ? CJ : 1];
+    if constexpr (CJ > 0) {
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) cr[j] = (double)c[lane + 64 * j];
+    }
+    auto cval = [&](int j, int d) -> double {
+        if constexpr (CJ > 0) return cr[j];
+        return (double)c[d];
+    };
+    const int nj = dpad / 64;
     for (int b0 = 0; b0 < B; b0 += qgroup) {
         const int nb = B - b0 < qgroup ? B - b0 : qgroup;
         __syncthreads();  // previous group done with LDS
@@ -45,12 +58,16 @@ __global__ __launch_bounds__(1024) void k_coarse(const float* __restrict__ cent,
             int b = 0;
             for (; b + 4 <= nb; b += 4) {  // four independent sums and butterflies interleave (ILP)
                 double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-                for (int d = lane; d < dpad; d += 64) {
-                    const double cd = (double)c[d];
-                    p0 = p0 + cd * (double)qs[(b + 0) * dpad + d];
-                    p1 = p1 + cd * (double)qs[(b + 1) * dpad + d];
-                    p2 = p2 + cd * (double)qs[(b + 2) * dpad + d];
-                    p3 = p3 + cd * (double)qs[(b + 3) * dpad + d];
+#pragma unroll
+                for (int j = 0; j < (CJ > 0 ? CJ : 1); ++j) {
+                    for (int jj = (CJ > 0 ? j : 0); jj < (CJ > 0 ? j + 1 : nj); ++jj) {
+                        const int d = lane + 64 * jj;
+                        const double cd = cval(jj, d);
+                        p0 = p0 + cd * (double)qs[(b + 0) * dpad + d];
+                        p1 = p1 + cd * (double)qs[(b + 1) * dpad + d];
+                        p2 = p2 + cd * (double)qs[(b + 2) * dpad + d];
+                        p3 = p3 + cd * (double)qs[(b + 3) * dpad + d];
+                    }
                 }
                 p0 = wave_butterfly_sum(p0);
                 p1 = wave_butterfly_sum(p1);
@@ -67,7 +84,10 @@ __global__ __launch_bounds__(1024) void k_coarse(const float* __restrict__ cent,
             for (; b < nb; ++b) {
                 const float* qv = qs + b * dpad;
                 double p = 0.0;
-                for (int d = lane; d < dpad; d += 64) p = p + (double)c[d] * (double)qv[d];
+                for (int jj = 0; jj < nj; ++jj) {
+                    const int d = lane + 64 * jj;
+                    p = p + cval(CJ > 0 ? (jj < CJ ? jj : 0) : 0, d) * (double)qv[d];
+                }
                 p = wave_butterfly_sum(p);
                 if (lane == 0) out[(int64_t)(b0 + b) * nlist + l] = Cand{p, l};
             }
@@ -466,13 +486,19 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
             hipLaunchKernelGGL((k_prep_q<F16>), dim3((Bp + 3) / 4), dim3(256), 0, st, qb, bc, Bp, h->dim, dpad, h->S,
                                QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
                                nullptr, 1, nullptr, nullptr, nullptr);
-        static bool coarse_attr[64] = {};
-        if (!coarse_attr[h->device & 63]) {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_coarse, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            coarse_attr[h->device & 63] = true;
+        // centroid row in registers for dpad <= 1024 (CJ = dpad / 64 values per lane)
+        auto coarse = dpad == 1024 ? k_coarse<16> : dpad == 768 ? k_coarse<12> : dpad == 512 ? k_coarse<8>
+                      : dpad == 384 ? k_coarse<6> : dpad == 256 ? k_coarse<4> : dpad == 128 ? k_coarse<2>
+                      : dpad == 64 ? k_coarse<1> : k_coarse<0>;
+        static bool coarse_attr[64][17] = {};
+        const int ci = (dpad == 1024 || dpad == 768 || dpad == 512 || dpad == 384 || dpad == 256 || dpad == 128 ||
+                        dpad == 64) ? dpad / 64 : 0;  // the CJ of the instantiation chosen above
+        if (!coarse_attr[h->device & 63][ci]) {
+            HIP_TRY(hipFuncSetAttribute((const void*)coarse, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            coarse_attr[h->device & 63][ci] = true;
         }
         const int qgroup = std::max(1, std::min(32, (160 * 1024) / (dpad * 4)));  // queries per LDS stage
-        hipLaunchKernelGGL(k_coarse, dim3((nlist + 15) / 16), dim3(1024), (size_t)qgroup * dpad * 4, st,
+        hipLaunchKernelGGL(coarse, dim3((nlist + 15) / 16), dim3(1024), (size_t)qgroup * dpad * 4, st,
                            centroids_dev, nlist, dpad, sc.q32.as<float>(), bc, qgroup, h->ivf_coarse.as<Cand>());
         hipLaunchKernelGGL(k_topk_cand, dim3(bc), dim3(1024), 0, st, h->ivf_coarse.as<Cand>(), (const int64_t*)nullptr,
                            1, (int64_t)nlist, bc, nprobe, h->ivf_probe.as<Cand>());

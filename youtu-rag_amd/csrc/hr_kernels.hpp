@@ -352,8 +352,11 @@ __device__ inline int acc_query(int qb, int i, int half) { return qb * 32 + (i &
 // shared per-query buffer with atomic slot reservation; the exact fallback)
 enum { SCAN_SAMPLE = 0, SCAN_FILTER = 1, SCAN_COLLECT = 2 };
 
-template <int MT, int DT, int QB, int P, int MODE, bool NT = true>
-__global__ __launch_bounds__(512, 2) void k_scan(ScanArgs a) {
+// TPB: threads per workgroup (512 = 8 waves, 2 per SIMD, <= 256 registers each).  A 4-wave variant
+// with a 32- / 64-deep corpus ring (one wave per SIMD, up to 512 registers) was measured for the
+// query-group launches and was slower (B = 128 at 10M rows: 5.7 / 6.3 ms vs 4.6 ms), so it is not built.
+template <int MT, int DT, int QB, int P, int MODE, bool NT = true, int TPB = 512>
+__global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) {  // (2nd: min waves per SIMD)
     constexpr bool FILTER = MODE != SCAN_SAMPLE;
     constexpr bool priv = MODE == SCAN_FILTER;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];

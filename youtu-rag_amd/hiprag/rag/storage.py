@@ -442,8 +442,9 @@ class HipVectorStore(BaseVectorStore):
     def _chunk(self, row: int, embedding=None) -> Chunk:
         rec = self._records[row]
         meta = rec["metadata"]
-        return Chunk(id=rec["id"], document_id=meta.get("document_id", ""), content=rec["content"],
-                     chunk_index=meta.get("chunk_index", 0), metadata=dict(meta), embedding=embedding)
+        # a fresh metadata dict per result, as Chroma returns (callers may mutate it)
+        return Chunk(rec["id"], meta.get("document_id", ""), rec["content"], meta.get("chunk_index", 0), dict(meta),
+                     embedding)
 
     def filter_bitmap(self, filters: dict[str, Any] | None):
         """uint64 row bitmap of a where-clause (None = no filter)."""
@@ -473,9 +474,10 @@ class HipVectorStore(BaseVectorStore):
                 return [[] for _ in range(len(q))]
             k = min(int(top_k), self.count_sync())
             scores, rows = self._index.search(q, k, self.filter_bitmap(filters))
+            rows_l, scores_l = rows.tolist(), scores.tolist()  # Python ints / floats once, not per element
             out = []
             for b in range(len(q)):
-                valid = [(int(r), float(s)) for r, s in zip(rows[b], scores[b]) if r >= 0]
+                valid = [(r, sc) for r, sc in zip(rows_l[b], scores_l[b]) if r >= 0]
                 embs = None
                 if self.include_embeddings and valid:
                     embs = self._embeddings([r for r, _ in valid])

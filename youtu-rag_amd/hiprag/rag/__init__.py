@@ -2,6 +2,7 @@
 from .base import (BaseEmbedder, BaseKnowledgeBuilder, BaseReranker, BaseRetriever, BaseStorageMonitor,
                    BaseTextSplitter, BaseVectorStore, BuildStatus, Chunk, Document, HealthStatus, QueryRequest,
                    QueryResponse, RetrievalResult)
+from .builder import CourseSearcher, KnowledgeBuilder
 from .chunker import RecursiveTextSplitter
 from .config import (ChunkingConfig, EmbeddingConfig, KnowledgeBuilderConfig, MonitorConfig, RAGConfig,
                      RetrieverConfig, VectorStoreConfig)
@@ -16,5 +17,5 @@ __all__ = [
     "RetrievalResult", "RecursiveTextSplitter", "ChunkingConfig", "EmbeddingConfig", "KnowledgeBuilderConfig",
     "MonitorConfig", "RAGConfig", "RetrieverConfig", "VectorStoreConfig", "EmbedderFactory", "ServiceEmbedder",
     "create_embedder", "BatchedVectorRetriever", "HybridRetriever", "VectorRetriever", "HipVectorStore",
-    "VectorStoreFactory", "RerankerFactory", "TorchRocmReranker",
+    "VectorStoreFactory", "RerankerFactory", "TorchRocmReranker", "KnowledgeBuilder", "CourseSearcher",
 ]

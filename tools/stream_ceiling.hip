@@ -57,6 +57,54 @@ __global__ __launch_bounds__(512) void k_stream(const u32x4* __restrict__ src, l
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;  // never true in practice
 }
 
+// The scan's stream with a pinned slice: chunks of every pin-th 64-KiB tile are loaded with the default
+// policy (they allocate in, and after the first pass hit, the Infinity Cache), all others non-temporal.
+template <int P>
+__global__ __launch_bounds__(512) void k_stream_pin(const u32x4* __restrict__ src, long long n_chunks, int pin,
+                                                    unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const long long W = (long long)gridDim.x * (blockDim.x >> 6);
+    const long long w = (long long)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const long long base = n_chunks / W, rem = n_chunks % W;
+    const long long c0 = w * base + (w < rem ? w : rem);
+    const long long c1 = c0 + base + (w < rem ? 1 : 0);
+    auto ld = [&](long long c) -> u32x4 {
+        if (((c >> 6) & (long long)(pin - 1)) == 0) return src[c * 64 + lane];  // pin: a power of two
+        return __builtin_nontemporal_load(src + c * 64 + lane);
+    };
+    u32x4 ring[P];
+    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < P; ++i) ring[i] = (c0 + i < c1) ? ld(c0 + i) : u32x4{0u, 0u, 0u, 0u};
+    long long c = c0;
+    // the policy is chosen once per batch of P chunks (P divides a tile's 64): two unrolled copies
+    // of the batch, so no branch sits between a load and the use of its ring slot
+    for (; c + 2 * P <= c1; c += P) {
+        if ((((c + P) >> 6) & (long long)(pin - 1)) == 0) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                acc ^= ring[i];
+                ring[i] = src[(c + P + i) * 64 + lane];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                acc ^= ring[i];
+                ring[i] = __builtin_nontemporal_load(src + (c + P + i) * 64 + lane);
+            }
+        }
+    }
+    for (; c < c1; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            if (c + i < c1) acc ^= ring[i];
+            const long long nx = c + P + i;
+            if (nx < c1) ring[i] = ld(nx);
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
+}
+
 template <bool NT, int P>
 static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
     hipEvent_t a, b;
@@ -104,6 +152,66 @@ int main(int argc, char** argv) {
                                : run<false, 16>(buf, n_chunks, sink, v.cus, v.threads, reps);
         std::printf("{\"variant\": \"%s\", \"bytes\": %lld, \"ms\": %.4f, \"TBps\": %.4f, \"frac_of_8TBps\": %.4f}\n",
                     v.name, bytes, ms, bytes / (ms * 1e-3) / 1e12, bytes / (ms * 1e-3) / 8e12);
+    }
+    // Infinity Cache residency behind the scan's stream: read a sample-sized table (128 MiB, default
+    // policy), stream the big buffer (non-temporal or default loads), then time a re-read of the table.
+    // Compared with a re-read right after the first read (resident) and one after a default-policy
+    // stream (evicted): tells whether nt streaming leaves a small, repeatedly read set in the L3.
+    if (argc > 2 && atoi(argv[2]) == 2) {  // pinned slice: every pin-th tile default-policy, rest nt
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        for (int pin : {1 << 30, 64, 32, 16, 8}) {
+            for (int r = 0; r < 3; ++r)  // warm: the pinned slice settles in the cache
+                hipLaunchKernelGGL((k_stream_pin<16>), dim3(n_cu - 32), dim3(512), 0, 0, buf, n_chunks, pin, sink);
+            CHECK(hipEventRecord(a, 0));
+            for (int r = 0; r < reps; ++r)
+                hipLaunchKernelGGL((k_stream_pin<16>), dim3(n_cu - 32), dim3(512), 0, 0, buf, n_chunks, pin, sink);
+            CHECK(hipEventRecord(b, 0));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0.f;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            const double t = ms / reps;
+            const long long pinned = pin >= (1 << 30) ? 0 : (n_chunks / 64 + pin - 1) / pin * 65536ll;
+            std::printf("{\"variant\": \"nt stream, every %d-th tile default policy\", \"bytes\": %lld, \"pinned_bytes\": %lld, "
+                        "\"ms\": %.4f, \"TBps\": %.4f, \"frac_of_8TBps\": %.4f}\n",
+                        pin >= (1 << 30) ? 0 : pin, bytes, pinned, t, bytes / (t * 1e-3) / 1e12, bytes / (t * 1e-3) / 8e12);
+        }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+    }
+    if (argc > 2 && atoi(argv[2]) == 1) {
+        const long long tb = 128ll << 20, t_chunks = tb / 1024;
+        u32x4* tab = nullptr;
+        CHECK(hipMalloc(&tab, tb));
+        CHECK(hipMemset(tab, 2, tb));
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        const int blocks = n_cu, threads = 512, R = 20;
+        for (int mode = 0; mode < 3; ++mode) {  // 0: nothing between, 1: nt stream between, 2: default stream
+            double tot = 0.0;
+            for (int r = 0; r < R; ++r) {
+                hipLaunchKernelGGL((k_stream<false, 16>), dim3(blocks), dim3(threads), 0, 0, tab, t_chunks, sink);
+                if (mode == 1) hipLaunchKernelGGL((k_stream<true, 16>), dim3(n_cu - 32), dim3(512), 0, 0, buf, n_chunks, sink);
+                if (mode == 2) hipLaunchKernelGGL((k_stream<false, 16>), dim3(n_cu - 32), dim3(512), 0, 0, buf, n_chunks, sink);
+                CHECK(hipEventRecord(a, 0));
+                hipLaunchKernelGGL((k_stream<false, 16>), dim3(blocks), dim3(threads), 0, 0, tab, t_chunks, sink);
+                CHECK(hipEventRecord(b, 0));
+                CHECK(hipEventSynchronize(b));
+                float ms = 0.f;
+                CHECK(hipEventElapsedTime(&ms, a, b));
+                tot += ms;
+            }
+            const double ms = tot / R;
+            static const char* names[3] = {"table re-read, nothing between", "table re-read after nt stream of buffer",
+                                           "table re-read after default-policy stream of buffer"};
+            std::printf("{\"variant\": \"%s\", \"table_bytes\": %lld, \"stream_bytes\": %lld, \"ms\": %.4f, \"TBps\": %.4f}\n",
+                        names[mode], tb, mode ? bytes : 0ll, ms, tb / (ms * 1e-3) / 1e12);
+        }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+        CHECK(hipFree(tab));
     }
     CHECK(hipFree(buf));
     CHECK(hipFree(sink));

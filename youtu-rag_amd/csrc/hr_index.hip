@@ -417,10 +417,17 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     int lds = scan_lds_bytes(h, pl.QB);
     // SAMPLE reduces its waves' group maxima in LDS: 8 waves x QB*16*64 floats + 8 part ids
     if (MODE == SCAN_SAMPLE) lds = std::max(lds, (kScanThreads / 64) * pl.QB * 16 * 64 * 4 + 64);
+    // Default-policy corpus loads for query groups (the other groups read the tiles from L2) and for
+    // the SAMPLE pass: its tiles are the same every batch (unit * stride), and the FILTER's
+    // non-temporal stream does not evict them from the Infinity Cache, so after the first batch the
+    // SAMPLE is served on-die instead of taking HBM time from the FILTER beside it
+    // (HIPRAG_SAMPLE_NT=1: non-temporal SAMPLE loads, for A/B)
+    static const bool sample_nt = getenv("HIPRAG_SAMPLE_NT") && atoi(getenv("HIPRAG_SAMPLE_NT")) != 0;
+    const bool dflt = pl.NG > 1 || (MODE == SCAN_SAMPLE && !sample_nt);
 #define HR_SCAN_CASE(QBv, Pv)                                                                     \
     if (pl.QB == QBv && pl.P == Pv)                                                               \
-        return pl.NG > 1 ? launch_scan_t<MT, DT, QBv, Pv, MODE, false>(h, sc, cus, a, st, lds)    \
-                         : launch_scan_t<MT, DT, QBv, Pv, MODE, true>(h, sc, cus, a, st, lds);
+        return dflt ? launch_scan_t<MT, DT, QBv, Pv, MODE, false>(h, sc, cus, a, st, lds)         \
+                    : launch_scan_t<MT, DT, QBv, Pv, MODE, true>(h, sc, cus, a, st, lds);
     if constexpr (DT == F32) {
         HR_SCAN_CASE(1, 8) HR_SCAN_CASE(1, 4) HR_SCAN_CASE(2, 4)
     } else {

@@ -118,5 +118,8 @@ def test_ingestor_batches_across_documents_and_replaces_old_chunks(tmp_path):
     no_sum = GpuIngestor(store, emb, summary_index=False)
     assert run(no_sum.chunk_and_store(Document(id="doc9", content="a b c", metadata={}))) == 1
     assert run(store.get_by_id("doc9_summary")) is None
-    with pytest.raises(NotImplementedError):
-        ing.split(Document(id="h", content="# x", metadata={"_use_hierarchical_splitter": True}))
+    # chunklevel.md documents take the hierarchical splitter (processors.py:371-379); "_" keys stay out
+    hc = ing.split(Document(id="h", content="# T\n## S\nline a\nline b", metadata={"_use_hierarchical_splitter": True,
+                                                                                   "source": "c.md"}))
+    assert [c.content for c in hc] == ["# T\n## S\n\nline a\nline b"]
+    assert hc[0].metadata == {"source": "c.md", "index_type": "index_content"} and hc[0].id == "h_chunk_0"

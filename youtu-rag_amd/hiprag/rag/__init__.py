@@ -3,7 +3,7 @@ from .base import (BaseEmbedder, BaseKnowledgeBuilder, BaseReranker, BaseRetriev
                    BaseTextSplitter, BaseVectorStore, BuildStatus, Chunk, Document, HealthStatus, QueryRequest,
                    QueryResponse, RetrievalResult)
 from .builder import CourseSearcher, KnowledgeBuilder
-from .chunker import RecursiveTextSplitter
+from .chunker import HierarchicalMarkdownSplitter, RecursiveTextSplitter
 from .config import (ChunkingConfig, EmbeddingConfig, KnowledgeBuilderConfig, MonitorConfig, RAGConfig,
                      RetrieverConfig, VectorStoreConfig)
 from .embeddings import EmbedderFactory, ServiceEmbedder, create_embedder
@@ -14,7 +14,7 @@ from .storage import HipVectorStore, VectorStoreFactory
 __all__ = [
     "BaseEmbedder", "BaseKnowledgeBuilder", "BaseReranker", "BaseRetriever", "BaseStorageMonitor", "BaseTextSplitter",
     "BaseVectorStore", "BuildStatus", "Chunk", "Document", "HealthStatus", "QueryRequest", "QueryResponse",
-    "RetrievalResult", "RecursiveTextSplitter", "ChunkingConfig", "EmbeddingConfig", "KnowledgeBuilderConfig",
+    "RetrievalResult", "RecursiveTextSplitter", "HierarchicalMarkdownSplitter", "ChunkingConfig", "EmbeddingConfig", "KnowledgeBuilderConfig",
     "MonitorConfig", "RAGConfig", "RetrieverConfig", "VectorStoreConfig", "EmbedderFactory", "ServiceEmbedder",
     "create_embedder", "BatchedVectorRetriever", "HybridRetriever", "VectorRetriever", "HipVectorStore",
     "VectorStoreFactory", "RerankerFactory", "TorchRocmReranker", "KnowledgeBuilder", "CourseSearcher",

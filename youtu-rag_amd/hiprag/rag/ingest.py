@@ -16,8 +16,8 @@ processor does (processors.py:559-561 -> _create_summary_index :423-464): one ch
 ``f"{doc}_summary"`` with content ``f"{source or doc id}\n{summary}"``, chunk_index -1 and the
 document's whole metadata (``_``-keys included, as the reference stores them) plus
 index_type="index_summary" -- the vectors kb_file_search searches (kb_search_toolkit.py:530-535).
-HierarchicalMarkdownSplitter documents ("_use_hierarchical_splitter") are outside
-this slice and are rejected loudly.
+Documents flagged ``_use_hierarchical_splitter`` (chunklevel.md, processors.py:226-332) are split by
+HierarchicalMarkdownSplitter with the configured chunk size and overlap (processors.py:371-379).
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ import logging
 from typing import Any
 
 from .base import BaseEmbedder, Chunk, Document
-from .chunker import RecursiveTextSplitter
+from .chunker import HierarchicalMarkdownSplitter, RecursiveTextSplitter
 from .config import ChunkingConfig
 
 logger = logging.getLogger(__name__)
@@ -66,9 +66,12 @@ class GpuIngestor:
         self._device = hasattr(embedder, "embed_texts_device") and hasattr(vector_store, "add_chunks_device")
 
     def split(self, document: Document, metadata: dict[str, Any] | None = None) -> list[Chunk]:
+        chunker = self.chunker
         if (document.metadata or {}).get("_use_hierarchical_splitter", False):
-            raise NotImplementedError("HierarchicalMarkdownSplitter documents are outside the GPU ingest slice")
-        return make_chunks(document, self.chunker.split_text(document.content, document.metadata), metadata)
+            cfg = getattr(self.chunker, "config", None) or ChunkingConfig()
+            chunker = HierarchicalMarkdownSplitter(ChunkingConfig(strategy="hierarchical", chunk_size=cfg.chunk_size,
+                                                                  chunk_overlap=cfg.chunk_overlap))
+        return make_chunks(document, chunker.split_text(document.content, document.metadata), metadata)
 
     async def _store(self, chunks: list[Chunk]) -> int:
         if not chunks:

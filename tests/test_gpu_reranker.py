@@ -105,3 +105,32 @@ def test_fused_layernorm_reranker_matches_unfused():
     assert a.fused_layers > 0 and b.fused_layers == 0
     np.testing.assert_allclose(a.score_pairs(["w1 w2 w9"], [texts])[0].cpu().numpy(),
                                b.score_pairs(["w1 w2 w9"], [texts])[0].cpu().numpy(), rtol=0, atol=1e-5)
+
+
+def test_reranker_matches_hf_cross_encoder_fp32(golden_dir):
+    """A local checkpoint (tests/golden/tiny_ce) scored by TorchRocmReranker on the GPU vs Hugging Face's own
+    pair encoding (tokenizer(query, passage, truncation=True)) and forward on the CPU in fp32: relevance =
+    sigmoid(logit) within 1e-5 for every pair, including truncated, empty and [UNK]-heavy passages."""
+    import os
+
+    import torch
+    from transformers import AutoModelForSequenceClassification, AutoTokenizer
+
+    from hiprag.rag.rerankers import TorchRocmReranker
+
+    path = os.path.join(golden_dir, "tiny_ce")
+    rr = TorchRocmReranker(path, dtype="float32", batch_size=5, max_length=64)
+    tok = AutoTokenizer.from_pretrained(path, local_files_only=True)
+    ref_model = AutoModelForSequenceClassification.from_pretrained(path, local_files_only=True).eval()
+    words = open(os.path.join(path, "vocab.txt")).read().split()[13:]
+    rng = np.random.default_rng(4)
+    queries = ["which course grade", "revenue by region in the quarter?"]
+    passages = [[" ".join(rng.choice(words, int(n))) for n in rng.integers(1, 90, 23)] + ["", "zyx qwv unknown"]
+                for _ in queries]
+    got = [s.cpu().numpy() for s in rr.score_pairs(queries, passages)]
+    with torch.inference_mode():
+        for q, ps, g in zip(queries, passages, got):
+            # one call per pair: Hugging Face encodes text_pair="" as a single sequence only there
+            want = [torch.sigmoid(ref_model(**tok(q, p, truncation=True, max_length=64, return_tensors="pt"))
+                                  .logits[0, 0]).item() for p in ps]
+            np.testing.assert_allclose(g, np.asarray(want, np.float32), rtol=0, atol=1e-5)

@@ -303,18 +303,27 @@ __global__ __launch_bounds__(1024) void k_ivf_units(const Cand* __restrict__ pro
         const int64_t l = probes[p].row;
         mine += l >= 0 ? list_tiles[l + 1] - list_tiles[l] : 0;
     }
-    part[tid] = mine;
+    // exclusive scan over the 1024 partials: inclusive scan inside each wave (shuffles), then over
+    // the 16 wave totals (a serial scan by one thread cost ~40 us: 1024 dependent LDS round trips)
+    int64_t incl = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = __shfl_up(incl, off, 64);
+        if ((tid & 63) >= off) incl += o;
+    }
+    if ((tid & 63) == 63) part[tid >> 6] = incl;
     __syncthreads();
-    if (tid == 0) {  // exclusive scan over 1024 partials
-        int64_t acc = 0;
-        for (int i = 0; i < (int)blockDim.x; ++i) {
-            const int64_t v = part[i];
-            part[i] = acc;
-            acc += v;
+    if (tid < 64) {
+        int64_t w = tid < (int)(blockDim.x >> 6) ? part[tid] : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = __shfl_up(w, off, 64);
+            if (tid >= off) w += o;
         }
+        part[64 + tid] = w;  // inclusive over waves
     }
     __syncthreads();
-    int64_t pos = part[tid];
+    int64_t pos = incl - mine + ((tid >> 6) ? part[64 + (tid >> 6) - 1] : 0);
     for (int j = 0; j < per; ++j) {
         const int p = tid * per + j;
         if (p >= np) break;
@@ -376,6 +385,11 @@ __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ ro
                                                   int dpad, const uint32_t* __restrict__ units,
                                                   const int64_t* __restrict__ uoff, int B, Cand* __restrict__ out) {
     static_assert(P % 4 == 0, "ring depth is a multiple of the 4-step canonical cycle");
+    // the wave's current query lives in LDS (dpad floats per wave): its reads then count against
+    // lgkmcnt, not vmcnt, so they never make the corpus ring drain (a global query load after the
+    // ring loads would have to wait for all of them)
+    extern __shared__ __attribute__((aligned(16))) float qlds[];
+    float* const myq = qlds + (int64_t)(threadIdx.x >> 6) * dpad;
     const int lane = threadIdx.x & 63;
     const int r = lane & 31, h = lane >> 5;
     const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -385,6 +399,14 @@ __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ ro
     const int64_t u0 = w * base + (w < rem ? w : rem);
     const int64_t u1 = u0 + base + (w < rem ? 1 : 0);
     if (u0 >= u1) return;
+    auto stage_query = [&](int b) {  // the wave's own LDS rows; LDS ops of one wave execute in order
+        const float4* src = (const float4*)(q32 + (int64_t)b * dpad);
+        for (int e = lane; e < dpad / 4; e += 64) ((float4*)myq)[e] = src[e];
+        __builtin_amdgcn_wave_barrier();
+    };
+    // first query before the first ring loads: its wait then leaves the ring in flight
+    int cur_b = (int)(units[u0] >> 26);
+    stage_query(cur_b);
     RawChunk<DT> ring[P];
     int64_t t_next = units[u0] & 0x3FFFFFFu;
 #pragma unroll
@@ -393,8 +415,13 @@ __global__ __launch_bounds__(256) void k_ivf_scan(const uint8_t* __restrict__ ro
         const uint32_t pk = units[u];
         const int64_t t = pk & 0x3FFFFFFu;
         const int b = (int)(pk >> 26);
+        if (b != cur_b) {  // a query change (units are query-major: about once per wave)
+            __builtin_amdgcn_wave_barrier();
+            stage_query(b);
+            cur_b = b;
+        }
         const int64_t tn = u + 1 < u1 ? (int64_t)(units[u + 1] & 0x3FFFFFFu) : t;  // prefetch target after t
-        const float* qv = q32 + (int64_t)b * dpad + 8 * h;
+        const float* qv = myq + 8 * h;
         double acc[4][8];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -505,7 +532,9 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         hipLaunchKernelGGL(k_ivf_units, dim3(1), dim3(1024), 0, st, h->ivf_probe.as<Cand>(), bc, nprobe,
                            list_tiles_dev, h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), cap);
         HIP_TRY(hipGetLastError());
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * 8, (cap + 3) / 4));
+        static const int bpc_env = getenv("HIPRAG_IVF_BPC") ? atoi(getenv("HIPRAG_IVF_BPC")) : 8;  // A/B timing
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * std::max(1, bpc_env),
+                                                                      (cap + 3) / 4));
         int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
             constexpr int DT = decltype(dt)::value;
             // ring depth (chunks in flight per wave): fp32 rows 4 (8 KiB; deeper rings spill), 16-bit
@@ -513,7 +542,15 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
             static const int ring_env = getenv("HIPRAG_IVF_RING") ? atoi(getenv("HIPRAG_IVF_RING")) : 16;
             const int ring = DT == F32 ? 4 : (h->S % ring_env == 0 ? ring_env : (h->S % 8 == 0 ? 8 : 4));
             auto kern = ring == 16 ? k_ivf_scan<DT, 16> : ring == 8 ? k_ivf_scan<DT, 8> : k_ivf_scan<DT, 4>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, h->rows, h->S, h->live,
+            const size_t qbytes = (size_t)4 * dpad * sizeof(float);  // one query per wave
+            static bool scan_attr[64][3] = {};
+            const int ri = ring == 16 ? 2 : ring == 8 ? 1 : 0;
+            if (qbytes > 64 * 1024 && !scan_attr[h->device & 63][ri]) {
+                HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                scan_attr[h->device & 63][ri] = true;
+            }
+            if (qbytes > 160 * 1024) return set_err(HR_E_UNSUPPORTED, "IVF scan: dim too large for the LDS query");
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), qbytes, st, h->rows, h->S, h->live,
                                (const uint32_t*)row_mask_dev, ids_dev, sc.q32.as<float>(), dpad,
                                h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), bc, h->ivf_out.as<Cand>());
             HIP_TRY(hipGetLastError());

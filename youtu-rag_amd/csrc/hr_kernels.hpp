@@ -296,6 +296,27 @@ struct XFrag;
 #ifndef HR_CORPUS_NT
 #define HR_CORPUS_NT 1
 #endif
+// HR_RING_SCHED=1: keep every refill right after the use of its slot (sched barriers), a textbook ring
+// with vmcnt(15) before every k-step.  Measured SLOWER than the compiler's own schedule, which waits
+// for the whole ring early in each batch of P k-steps and then issues the P refills back to back
+// (10M rows 3.15 vs 3.00 ms, 1.25M 0.442 vs 0.434, B = 128 4.96 vs 4.51; tools/ab_ring.sh): each wave
+// then sends one contiguous P KiB burst at a time, which the HBM serves better than P requests
+// trickled between the MFMAs of 8 waves.  Kept as an A/B build switch.
+#ifndef HR_RING_SCHED
+#define HR_RING_SCHED 0
+#endif
+// a wave-uniform 64-bit value in scalar registers (the compiler cannot prove threadIdx.x >> 6 uniform)
+__device__ inline int64_t wave_uniform(int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// read-only word at a wave-uniform index through the constant address space: a scalar load, counted
+// by lgkmcnt -- a vector load here would be counted by vmcnt behind the corpus ring, and reading it
+// would wait for every ring load issued after it
+__device__ inline uint32_t scalar_word(const uint32_t* p, int64_t i) {
+    return ((const __attribute__((address_space(4))) uint32_t*)p)[i];
+}
 template <bool NT>
 __device__ inline u32x4 corpus_load(const uint8_t* p) {
 #if HR_CORPUS_NT
@@ -399,8 +420,8 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     const int S = a.S;
     // tile of unit u (wave-uniform: a scalar load when a tile list is given)
     auto tile_at = [&](int64_t u) -> int64_t {
-        const int64_t i = u * stride;
-        return a.tile_list ? (int64_t)a.tile_list[i] : i;
+        const int64_t i = wave_uniform(u * stride);
+        return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };
     const unsigned long long t_entry = a.stamps ? wall_clock64() : 0ull;
 
@@ -410,7 +431,12 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     if (u0 < u1) {
         const int64_t c0 = tile_at(u0) * S;
 #pragma unroll
-        for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
+        for (int i = 0; i < P; ++i) {
+            ring[i].load(a.rows, c0 + i, lane);
+#if HR_RING_SCHED
+            __builtin_amdgcn_sched_barrier(0);  // slot order = issue order, as in the loop (no partial drains)
+#endif
+        }
     }
 
     // stage the query fragments (QB*S KiB) into LDS once per launch; 8 loads in flight per
@@ -552,8 +578,8 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
             issued = true;
         }
         if (dyn && u + 1 == u_end) pend = grab_resolve(graw);  // this unit's last k-steps prefetch its first unit
-        const int64_t t = tile_at(u);
-        const int64_t tn = (u + 1 < u_end) ? tile_at(u + 1) : (pend >= 0 ? tile_at(pend) : t);
+        const int64_t t = wave_uniform(tile_at(u));
+        const int64_t tn = wave_uniform((u + 1 < u_end) ? tile_at(u + 1) : (pend >= 0 ? tile_at(pend) : t));
         if (t >= part_end) {  // wave-uniform; never taken with one part
             if (MODE != SCAN_COLLECT && a.use_groups) flush();
             const int64_t np_ = t / a.part_tiles;
@@ -569,34 +595,65 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
             for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
         // row held by this lane's slot (slot swizzle, hr_common.hpp)
         const int rg = slot_row(t, g);
-        // euclidean: this tile's row norms, loaded before the k-loop so they are back by the epilogue
-        const float xs = a.xnorm ? a.xnorm[t * 32 + rg] : 0.0f;
-        const float xmul = a.xnorm ? 2.0f : 1.0f;
 
+        // this tile's live / mask words, issued before the k-loop: read in the epilogue, they are then
+        // older than the ring loads in flight (a load issued after them would make that read wait for
+        // the whole ring: vmcnt(0) at every tile)
+        uint32_t allow = scalar_word(a.live, t);
+        if (a.mask) allow &= scalar_word(a.mask, t);
         for (int sb = 0; sb < S; sb += P) {
             const bool same = sb + P < S;
             const int64_t nc = same ? t * S + sb + P : tn * S;
+#if HR_RING_SCHED
+            // query fragments one k-step ahead (LDS latency under the MFMAs of the step before)
+            u32x4 qn[QB];
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) qn[qb] = qs[(sb * QB + qb) * 64 + lane];
+#endif
 #pragma unroll
             for (int i = 0; i < P; ++i) {
                 const u32x4 xf = ring[i].get();
+#if HR_RING_SCHED
+                u32x4 qc[QB];
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) qc[qb] = qn[qb];
+                if (i + 1 < P) {
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb) qn[qb] = qs[((sb + i + 1) * QB + qb) * 64 + lane];
+                }
+                __builtin_amdgcn_sched_barrier(0);  // the next step's LDS reads go out before these MFMAs
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma32<MT>(qc[qb], xf, acc[qb]);
+                // refill slot i after its last use and keep it there: the new value can then take the
+                // slot's own registers.  Refilling before the MFMAs that read the old value (or letting
+                // the scheduler sink all P refills to the end of the batch) makes the two values
+                // overlap, the loop back-edge then needs register copies of in-flight slots, and every
+                // copy waits for its load: the ring drained to vmcnt(0..2) once per P chunks.
+                ring[i].load(a.rows, nc + i, lane);
+                __builtin_amdgcn_sched_barrier(0);
+#else
                 ring[i].load(a.rows, nc + i, lane);
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const u32x4 qf = qs[((sb + i) * QB + qb) * 64 + lane];
                     acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
                 }
+#endif
             }
         }
 
         // epilogue: (euclidean) approximate score, predicate, group max, threshold filter
         if (a.xnorm) {
+            // euclidean: this tile's row norms, read here and only here -- a vector load issued before
+            // the k-loop would make even the cosine path's epilogue wait for the whole ring (vmcnt(0)
+            // at the join; the loop's trip count is not known to the compiler)
+            const float xs = a.xnorm[t * 32 + rg];
+            const float xmul = 2.0f;
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[qb][i] = __builtin_fmaf(xmul, acc[qb][i], -xs);
         }
-        uint32_t allow = a.live[t];
-        if (a.mask) allow &= a.mask[t];
         const bool ok = (allow >> rg) & 1u;
         const uint32_t row = (uint32_t)(t * 32 + rg);
         uint64_t any = 0;

@@ -28,7 +28,7 @@ def _docs(ds):
 
 
 def _ids(store):
-    return [r["id"] for r in store._records if r is not None]
+    return [r[0] for r in store._records if r is not None]
 
 
 def _run(golden, tmp_path, monkeypatch, device: bool):
@@ -54,7 +54,7 @@ def _run(golden, tmp_path, monkeypatch, device: bool):
         assert _ids(store) == steps[name]["store_ids"], name
         assert asyncio.run(kb.get_build_status()) is st
     snap = [{"id": r["id"], "content": r["content"], "metadata": r["metadata"]}
-            for r in store._records if r is not None]
+            for r in map(store.record, range(len(store._records))) if r is not None]
     assert snap == golden["store_after_add_b"]
 
     for k, v in golden["env"].items():

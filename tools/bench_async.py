@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""The reference's call pattern through the drop-in store: many concurrent single-query
+``await store.search(query_embedding=..., top_k=10)`` calls (VectorRetriever.retrieve,
+base_retriever.py:58-63), coalesced by HipVectorStore's micro-batcher into batched launches.
+
+Builds a HipVectorStore over n synthetic rows (10M x 1024 bf16 by default, 1000-chunk documents, as
+tools/bench_filter.py STORE=1), then for each concurrency C runs C client coroutines that each issue
+sequential searches with planted queries for a fixed wall time, and reports queries/s, latency
+percentiles, the mean launch size and launches.  One JSON line per (max_batch, C).
+Usage: python tools/bench_async.py [--rows 10000000 --clients 1,16,64,256,1024 --max-batch 64,256 --seconds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "youtu-rag_amd"), REPO]
+
+
+def build_store(n: int, max_batch: int, idx=None):
+    from hiprag import _native
+    from hiprag.rag import HipVectorStore, VectorStoreConfig
+
+    D = 1024
+    if idx is None:
+        idx = _native.NativeIndex(D, "bf16", "cosine")
+        idx.reserve(n)
+        idx.add_synthetic(0, 0, n)
+    cfg = VectorStoreConfig(backend="hip", collection_name="bench", persist_directory="/tmp/hiprag_bench_async",
+                            index_params={"dtype": "bf16", "persist": False, "max_batch": max_batch})
+    st = HipVectorStore(cfg, index_factory=lambda d: idx)
+    st._ensure_index(D)
+    recs = []
+    for r in range(n):
+        d, i = divmod(r, 1000)
+        recs.append({"id": f"doc{d}_chunk_{i}", "document_id": f"doc{d}", "content": "", "chunk_index": i,
+                     "metadata": {"document_id": f"doc{d}", "chunk_index": i}})
+        if len(recs) == 1_000_000:
+            st._append_tables(recs, None)
+            recs = []
+    if recs:
+        st._append_tables(recs, None)
+    return st, idx
+
+
+async def run_clients(st, queries, C: int, seconds: float, k: int):
+    lat: list[float] = []
+    stop = time.perf_counter() + seconds
+    nq = len(queries)
+
+    async def client(c):
+        j = c
+        while time.perf_counter() < stop:
+            t0 = time.perf_counter()
+            res = await st.search(query_embedding=queries[j % nq], top_k=k)
+            lat.append(time.perf_counter() - t0)
+            assert len(res) == k
+            j += C
+
+    launches0 = st._batcher.launches
+    t0 = time.perf_counter()
+    await asyncio.gather(*(client(c) for c in range(C)))
+    wall = time.perf_counter() - t0
+    return lat, wall, st._batcher.launches - launches0
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", type=int, default=10_000_000)
+    p.add_argument("--clients", default="1,16,64,256,1024")
+    p.add_argument("--max-batch", default="64,256")
+    p.add_argument("--depth", default="2", help="launches in flight (comma list: A/B)")
+    p.add_argument("--gc-freeze", default="0", help="0/1 list: gc.freeze() after building the store (A/B)")
+    p.add_argument("--seconds", type=float, default=3.0)
+    p.add_argument("--k", type=int, default=10)
+    args = p.parse_args()
+
+    import gc
+
+    import numpy as np
+
+    from hiprag import synth
+
+    q, _ = synth.planted_queries(0, args.rows, 1024, 2048, qseed=11)
+    queries = [np.asarray(x, np.float32) for x in q]
+    t0 = time.perf_counter()
+    st, _ = build_store(args.rows, 64)
+    print(f"# store of {args.rows} rows in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    gc.collect()
+    print(f"# full collection {1e3 * (time.perf_counter() - t0):.1f} ms over {len(gc.get_objects())} tracked objects",
+          file=sys.stderr, flush=True)
+    for fz in (int(x) for x in args.gc_freeze.split(",")):
+        if fz:
+            gc.collect()
+            gc.freeze()
+        for depth in (int(x) for x in args.depth.split(",")):
+            for mb in (int(x) for x in args.max_batch.split(",")):
+                st._batcher.max_batch, st._batcher.depth = mb, depth
+                asyncio.run(run_clients(st, queries, 64, 0.5, args.k))  # warm
+                for C in (int(x) for x in args.clients.split(",")):
+                    gc0 = sum(s["collections"] for s in gc.get_stats())
+                    lat, wall, launches = asyncio.run(run_clients(st, queries, C, args.seconds, args.k))
+                    a = np.asarray(lat) * 1e3
+                    print(json.dumps({"rows": args.rows, "max_batch": mb, "depth": depth, "gc_freeze": fz, "clients": C,
+                                      "queries": len(lat), "qps": round(len(lat) / wall, 1),
+                                      "latency_ms_p50": round(float(np.percentile(a, 50)), 3),
+                                      "latency_ms_p99": round(float(np.percentile(a, 99)), 3),
+                                      "launches": launches, "mean_launch_size": round(len(lat) / max(1, launches), 1),
+                                      "gc_collections": sum(s["collections"] for s in gc.get_stats()) - gc0}),
+                          flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -45,6 +45,7 @@ import json
 import logging
 import os
 import threading
+from array import array
 from typing import Any
 
 import numpy as np
@@ -60,11 +61,52 @@ logger = logging.getLogger(__name__)
 _METRIC = {"cosine": "cosine", "dot": "ip", "euclidean": "l2"}
 
 
-class _SearchBatcher:
-    """Coalesces concurrent ``search`` calls into batched launches (one per filter group)."""
+class _ObjColumn:
+    """A growable per-row column of Python objects in a numpy object array.  Used instead of a list for
+    the 10M-entry host tables: an object ndarray is not tracked by Python's cycle collector, a list is,
+    and every full collection walked the lists' 10M entries (~0.1 s each; p99 search latency under
+    load 600 ms without it, 6-70 ms with it -- tools/bench_async.py).  Holds only acyclic values."""
 
-    def __init__(self, store: "HipVectorStore", max_batch: int):
-        self.store, self.max_batch = store, max(1, int(max_batch))
+    __slots__ = ("a", "n")
+
+    def __init__(self, values=()):
+        values = list(values)
+        self.a = np.empty(max(1024, len(values)), object)
+        for i, v in enumerate(values):  # element-wise: tuples must stay objects, not become array rows
+            self.a[i] = v
+        self.n = len(values)
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return self.a[i]
+
+    def __setitem__(self, i, v):
+        self.a[i] = v
+
+    def __iter__(self):
+        return iter(self.a[: self.n])
+
+    def append(self, v):
+        if self.n == len(self.a):
+            grown = np.empty(2 * len(self.a), object)
+            grown[: self.n] = self.a
+            self.a = grown
+        self.a[self.n] = v
+        self.n += 1
+
+
+class _SearchBatcher:
+    """Coalesces concurrent ``search`` calls into batched launches (one per filter group).
+
+    Up to ``depth`` launches are in flight: a worker thread runs only the native search (ctypes drops
+    the GIL), and the Chunk objects are assembled on the event-loop thread while the next launch already
+    runs -- the GPU does not idle during host work, and a worker holding the GIL cannot be starved by a
+    busy event loop (with 1024 clients that convoy cut throughput 4x)."""
+
+    def __init__(self, store: "HipVectorStore", max_batch: int, depth: int = 2):
+        self.store, self.max_batch, self.depth = store, max(1, int(max_batch)), max(1, int(depth))
         self.pending: list = []
         self.running = False
         self.launches = 0  # diagnostics
@@ -79,27 +121,47 @@ class _SearchBatcher:
             loop.call_soon(lambda: loop.create_task(self._drain()))
         return await fut
 
+    def _take(self):
+        key = self.pending[0][3]
+        batch, rest = [], []
+        for e in self.pending:
+            (batch if e[3] == key and len(batch) < self.max_batch else rest).append(e)
+        self.pending = rest
+        return batch
+
     async def _drain(self):
+        inflight: dict = {}  # task -> batch
         try:
-            while self.pending:
-                key = self.pending[0][3]
-                batch, rest = [], []
-                for e in self.pending:
-                    (batch if e[3] == key and len(batch) < self.max_batch else rest).append(e)
-                self.pending = rest
-                qs = np.stack([e[0] for e in batch])
-                k = max(e[1] for e in batch)
-                self.launches += 1
-                try:
-                    res = await asyncio.to_thread(self.store.search_batch, qs, k, batch[0][2])
-                except Exception as exc:  # noqa: BLE001 -- every waiter sees the failure
-                    for e in batch:
-                        if not e[4].done():
-                            e[4].set_exception(exc)
+            while self.pending or inflight:
+                while self.pending and len(inflight) < self.depth:
+                    batch = self._take()
+                    qs = np.stack([e[0] for e in batch])
+                    k = max(e[1] for e in batch)
+                    self.launches += 1
+                    try:
+                        prep = self.store._prep_search(qs, k, batch[0][2])
+                    except Exception as exc:  # noqa: BLE001
+                        for e in batch:
+                            if not e[4].done():
+                                e[4].set_exception(exc)
+                        continue
+                    task = asyncio.ensure_future(asyncio.to_thread(self.store._run_search, prep))
+                    inflight[task] = (batch, prep)
+                if not inflight:
                     continue
-                for e, r in zip(batch, res):
-                    if not e[4].done():
-                        e[4].set_result(r[: e[1]])
+                done, _ = await asyncio.wait(list(inflight), return_when=asyncio.FIRST_COMPLETED)
+                for task in done:
+                    batch, prep = inflight.pop(task)
+                    try:
+                        res = self.store._assemble(prep, task.result())
+                    except Exception as exc:  # noqa: BLE001 -- every waiter sees the failure
+                        for e in batch:
+                            if not e[4].done():
+                                e[4].set_exception(exc)
+                        continue
+                    for e, r in zip(batch, res):
+                        if not e[4].done():
+                            e[4].set_result(r[: e[1]])
         finally:
             self.running = False
 
@@ -131,7 +193,7 @@ class HipVectorStore(BaseVectorStore):
                                                                           devices=self.devices))
         self._loader = index_loader or (lambda path, dim, dtype, metric: _native.NativeIndex.load(
             path, devices=self.devices, dim=dim, dtype=dtype, metric=metric))
-        self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)))
+        self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)), int(params.get("search_depth", 2)))
         self._lock = threading.RLock()
         self._paths = P.Paths(config.persist_directory, config.collection_name)
         self._gen = 0
@@ -144,9 +206,14 @@ class HipVectorStore(BaseVectorStore):
     def _reset_tables(self):
         self._index = None
         self.dim: int | None = None
-        self._records: list[dict | None] = []
+        # host tables, one entry per index row (None = deleted): a tuple of atoms (id, document_id, content,
+        # chunk_index) and the stored metadata dict.  Kept apart on purpose: a tuple of atoms and a dict of
+        # atoms are untracked by Python's cycle collector, a record dict holding a dict is not -- at 10M
+        # rows every full collection then walked 20M+ objects (seconds-long pauses under load)
+        self._records = _ObjColumn()  # per row: (id, document_id, content, chunk_index) or None
+        self._metas = _ObjColumn()    # per row: the stored metadata dict or None
         self._id_to_row: dict[str, int] = {}
-        self._doc_rows: dict[str, list[int]] = {}
+        self._doc_rows: dict[str, array] = {}  # document -> its rows (array('q'): not GC-tracked either)
         self._cols = F.MetadataColumns()
         self._live = np.zeros(0, bool)
         self._raw = None  # keep_embeddings: (capacity, dim) fp32 host copy
@@ -197,14 +264,30 @@ class HipVectorStore(BaseVectorStore):
                 logger.info("replayed %d journal entries", n_ops)
         logger.info("loaded %d chunks from %s", len(self._id_to_row), idx_path)
 
+    @staticmethod
+    def _split_record(rec: dict | None):
+        if rec is None:
+            return None, None
+        return (rec["id"], rec["document_id"], rec["content"], rec.get("chunk_index", 0)), rec.get("metadata", {})
+
+    def record(self, row: int) -> dict | None:
+        """The stored record of a row as the persisted dict (None if deleted)."""
+        t = self._records[row]
+        if t is None:
+            return None
+        return {"id": t[0], "document_id": t[1], "content": t[2], "chunk_index": t[3], "metadata": self._metas[row]}
+
     def _install(self, records: list, raw):
-        self._records = list(records)
+        split = [self._split_record(rec) for rec in records]
+        self._records = _ObjColumn(t for t, _ in split)
+        self._metas = _ObjColumn(m for _, m in split)
+        del split
         self._live = np.array([r is not None for r in records], bool)
-        for row, rec in enumerate(records):
+        for row, rec in enumerate(self._records):
             if rec is not None:
-                self._id_to_row[rec["id"]] = row
-                self._doc_rows.setdefault(rec["document_id"], []).append(row)
-        self._cols.append([(rec or {}).get("metadata", {}) for rec in records])
+                self._id_to_row[rec[0]] = row
+                self._doc_rows.setdefault(rec[1], array("q")).append(row)
+        self._cols.append([m or {} for m in self._metas])
         if self.keep_embeddings:
             self._raw = np.zeros((max(len(records), 1024), self.dim), np.float32)
             if raw is not None and len(raw) == len(records):
@@ -234,7 +317,8 @@ class HipVectorStore(BaseVectorStore):
             n = len(self._records)
             self._index.save(pt.gen(g, "hri"))
             P.write_rows(pt.gen(g, "rows.jsonl"), {"format": P.FORMAT, "gen": g, "n_rows": n, "dim": self.dim,
-                                                  "dtype": self.dtype, "metric": self.metric}, self._records)
+                                                  "dtype": self.dtype, "metric": self.metric},
+                         (self.record(r) for r in range(n)))
             if self.keep_embeddings:
                 P.fsync_write(pt.gen(g, "emb.npy"), writer=lambda f: np.save(f, self._raw[:n], allow_pickle=False))
             P.fsync_write(pt.manifest, json.dumps({"format": P.FORMAT, "gen": g, "n_rows": n, "dim": self.dim,
@@ -298,10 +382,12 @@ class HipVectorStore(BaseVectorStore):
     def _append_tables(self, records: list[dict], vectors: np.ndarray | None):
         first = len(self._records)
         for i, rec in enumerate(records):
-            self._records.append(rec)
+            t, m = self._split_record(rec)
+            self._records.append(t)
+            self._metas.append(m)
             if rec is not None:
                 self._id_to_row[rec["id"]] = first + i
-                self._doc_rows.setdefault(rec["document_id"], []).append(first + i)
+                self._doc_rows.setdefault(rec["document_id"], array("q")).append(first + i)
         self._cols.append([(rec or {}).get("metadata", {}) for rec in records])
         n = len(self._records)
         if len(self._live) < n:
@@ -373,13 +459,14 @@ class HipVectorStore(BaseVectorStore):
         self._index.remove(np.asarray(rows, np.int64))
         for r in rows:
             rec = self._records[r]
-            self._id_to_row.pop(rec["id"], None)
-            doc = self._doc_rows.get(rec["document_id"])
+            self._id_to_row.pop(rec[0], None)
+            doc = self._doc_rows.get(rec[1])
             if doc is not None:
                 doc.remove(r)
                 if not doc:
-                    del self._doc_rows[rec["document_id"]]
+                    del self._doc_rows[rec[1]]
             self._records[r] = None
+            self._metas[r] = None
             self._live[r] = False
         if journal:
             self._log("del", rows=rows)
@@ -441,9 +528,9 @@ class HipVectorStore(BaseVectorStore):
     # ---------------------------------------------------------------- reads
     def _chunk(self, row: int, embedding=None) -> Chunk:
         rec = self._records[row]
-        meta = rec["metadata"]
+        meta = self._metas[row]
         # a fresh metadata dict per result, as Chroma returns (callers may mutate it)
-        return Chunk(rec["id"], meta.get("document_id", ""), rec["content"], meta.get("chunk_index", 0), dict(meta),
+        return Chunk(rec[0], meta.get("document_id", ""), rec[2], meta.get("chunk_index", 0), dict(meta),
                      embedding)
 
     def filter_bitmap(self, filters: dict[str, Any] | None):
@@ -460,30 +547,50 @@ class HipVectorStore(BaseVectorStore):
     def search_batch(self, query_embeddings, top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[list[tuple[Chunk, float]]]:
         """Batched search: one GPU launch for all queries (BatchedVectorRetriever, the micro-batcher)."""
+        prep = self._prep_search(query_embeddings, top_k, filters)
+        return self._assemble(prep, self._run_search(prep))
+
+    # search_batch in three steps, so the micro-batcher can run only the middle one in a worker thread
+    # (it holds the GIL for nothing but the ctypes call; a worker doing the Python parts was starved by
+    # a busy event loop) and assemble on the event-loop thread while the next launch runs
+    def _prep_search(self, query_embeddings, top_k: int, filters):
         q = np.asarray(query_embeddings, dtype=np.float32)
         if q.ndim == 1:
             q = q[None, :]
-        with self._lock:
-            if self._index is None or self.count_sync() == 0:
-                return [[] for _ in range(len(q))]
-            if q.shape[1] != self.dim:
-                raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
-            # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
-            # search takes its exhaustive exact path (same results, one corpus pass per query)
-            if int(top_k) <= 0:
-                return [[] for _ in range(len(q))]
-            k = min(int(top_k), self.count_sync())
-            scores, rows = self._index.search(q, k, self.filter_bitmap(filters))
-            rows_l, scores_l = rows.tolist(), scores.tolist()  # Python ints / floats once, not per element
-            out = []
-            for b in range(len(q)):
-                valid = [(r, sc) for r, sc in zip(rows_l[b], scores_l[b]) if r >= 0]
-                embs = None
-                if self.include_embeddings and valid:
+        if self._index is None or self.count_sync() == 0 or int(top_k) <= 0:
+            return (q, 0, None)
+        if q.shape[1] != self.dim:
+            raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
+        # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
+        # search takes its exhaustive exact path (same results, one corpus pass per query)
+        return (q, min(int(top_k), self.count_sync()), self.filter_bitmap(filters))
+
+    def _run_search(self, prep):
+        q, k, bitmap = prep
+        if k == 0:
+            return None
+        with self._lock:  # ordered against mutations
+            if self._index is None:
+                return None
+            return self._index.search(q, k, bitmap)
+
+    def _assemble(self, prep, raw) -> list[list[tuple[Chunk, float]]]:
+        n = len(prep[0])
+        if raw is None:
+            return [[] for _ in range(n)]
+        scores, rows = raw
+        rows_l, scores_l = rows.tolist(), scores.tolist()  # Python ints / floats once, not per element
+        recs = self._records  # append-only list; a row deleted since the search reads None and is dropped
+        out = []
+        for b in range(n):
+            valid = [(r, sc) for r, sc in zip(rows_l[b], scores_l[b]) if r >= 0 and recs[r] is not None]
+            embs = None
+            if self.include_embeddings and valid:
+                with self._lock:
                     embs = self._embeddings([r for r, _ in valid])
-                out.append([(self._chunk(r, None if embs is None else embs[i].tolist()), s)
-                            for i, (r, s) in enumerate(valid)])
-            return out
+            out.append([(self._chunk(r, None if embs is None else embs[i].tolist()), s)
+                        for i, (r, s) in enumerate(valid)])
+        return out
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:

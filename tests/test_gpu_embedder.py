@@ -78,7 +78,7 @@ def test_ingest_split_embed_add_query(tmp_path):
     n = asyncio.run(ing.ingest(docs))
     assert n == asyncio.run(store.count()) > 300
     # the stored rows are exactly the oracle's bf16 quantisation of the embedder's vectors
-    records = [r for r in store._records if r is not None]
+    records = [r for r in map(store.record, range(len(store._records))) if r is not None]
     vecs = torch.cat(seen).cpu().numpy()
     assert len(vecs) == len(records)
     rows = np.array([store._id_to_row[r["id"]] for r in records])
@@ -158,7 +158,7 @@ def test_ingest_writes_summary_vectors_that_kb_file_search_finds(tmp_path):
                      metadata={"source": f"file_{d}.pdf", "summary": " ".join(rng.choice(words, 10))})
             for d in range(30)]
     asyncio.run(ing.ingest(docs))
-    recs = store._records
+    recs = [store.record(i) for i in range(len(store._records))]
     summ_rows = [i for i, r in enumerate(recs) if r["metadata"].get("index_type") == "index_summary"]
     assert len(summ_rows) == 30 and all(recs[i]["id"].endswith("_summary") for i in summ_rows)
     tk = KBSearchToolkit(config={}, kb_resolver=lambda kb: ("kbsum", "kb"), store_factory=lambda c: store)

@@ -240,7 +240,7 @@ def test_c4_100k_chunk_ingest_then_retrieve(tmp_path):
     stored = store._index.get_rows(np.arange(n))
     expect = R.process_rows(vecs, "cosine", "bf16")
     np.testing.assert_array_equal(stored, R.dequantize(expect, "bf16"))
-    ids = [r["id"] for r in store._records]
+    ids = [r[0] for r in store._records]
     queries = [" ".join(rng.choice(words, 5)) for _ in range(16)]
     retr = BatchedVectorRetriever(store, emb, RetrieverConfig(top_k=10, similarity_threshold=0.0))
     got = asyncio.run(retr.batch_retrieve(queries, top_k=10))
@@ -261,5 +261,5 @@ def test_c4_100k_chunk_ingest_then_retrieve(tmp_path):
     allowed = np.concatenate([allowed, np.ones(len(vec_new), bool)])
     got2 = asyncio.run(retr.batch_retrieve(queries[:4], top_k=10))
     s2, r2 = oracle.c_search(all_stored, "bf16", qv[:4], 10, oracle.mask_from_bool(allowed))
-    ids2 = [r["id"] if r is not None else None for r in store._records]
+    ids2 = [r[0] if r is not None else None for r in store._records]
     assert [[x.chunk.id for x in res] for res in got2] == [[ids2[j] for j in rr] for rr in r2]

@@ -381,6 +381,8 @@ def main():
             result["roofline"]["traffic_unit"] = "GB per launch (HBM read, PMC)"
             result["roofline"]["traffic_source"] = os.path.relpath(summaries[-1], REPO)
             result["roofline"]["profiled_avg_launch_ms"] = round(prof["k_scan_filter_ms_avg"], 4)
+            if prof.get("k_scan_sample_fetch_bytes"):  # the SAMPLE pass beside it (L3 hits included)
+                result["roofline"]["sample_traffic"] = round(prof["k_scan_sample_fetch_bytes"] / 1e9, 3)
             if prof.get("k_scan_filter_busy_ms_per_launch"):  # overlapping launches (dual FILTER streams)
                 result["roofline"]["profiled_busy_ms_per_launch"] = round(prof["k_scan_filter_busy_ms_per_launch"], 4)
 

@@ -108,3 +108,30 @@ def test_factory(monkeypatch):
         RerankerFactory.create("jina", api_key="x")
     m = build_random_cross_encoder("tiny", seed=3)
     assert m.config.num_labels == 1 and m.config.hidden_size == 256
+
+
+def test_vectorised_pair_batches_match_per_pair_forward():
+    """score_pairs assembles length-sorted batches with numpy (query / passage / [SEP] scatter, token
+    types, masks, longest_first truncation, empty passages as single sequences): on the CPU its scores
+    equal a per-pair forward of rr._pair's encoding, for a max_length that truncates."""
+    import numpy as np
+    import torch
+
+    from hiprag.rag.rerankers import TorchRocmReranker
+
+    rr = TorchRocmReranker(preset="tiny", dtype="float32", batch_size=7, max_length=24, device="cpu")
+    words = [f"w{i}" for i in range(300)]
+    rng = np.random.default_rng(1)
+    queries = ["w1 w2 w3", " ".join(rng.choice(words, 30)), "w9"]
+    passages = [[" ".join(rng.choice(words, int(k))) for k in rng.integers(1, 40, 9)] + [""] for _ in queries]
+    got = [s.numpy() for s in rr.score_pairs(queries, passages)]
+    with torch.inference_mode():
+        for q, ps, g in zip(queries, passages, got):
+            q_ids = rr._text_ids(q, cache=False)
+            want = []
+            for p in ps:
+                ids, types = rr._pair(q_ids, rr._text_ids(p, cache=True), passage_is_empty=not p)
+                assert len(ids) <= 24
+                logit = rr.model(input_ids=torch.tensor([ids]), token_type_ids=torch.tensor([types])).logits[0, 0]
+                want.append(torch.sigmoid(logit.float()).item())
+            np.testing.assert_allclose(g, want, rtol=0, atol=1e-5)

@@ -114,6 +114,7 @@ class TorchRocmReranker(BaseReranker):
         if self.batch_size < 1:
             raise ValueError("batch_size must be at least one")
         self._cache: dict[str, list[int]] = {}
+        self._cache_np: dict[str, np.ndarray] = {}
         self._cache_size = int(cache_size)
         self.model_name = model_name_or_path or f"random-init {preset}"
 
@@ -150,42 +151,100 @@ class TorchRocmReranker(BaseReranker):
         return ids, types
 
     # ------------------------------------------------------------------ scoring
+    def _np_ids(self, text: str) -> np.ndarray:
+        """Cached token ids of a passage as an int64 array (the pair assembly below is vectorised)."""
+        a = self._cache_np.get(text)
+        if a is None:
+            a = np.asarray(self._text_ids(text, cache=True), np.int64)
+            if len(self._cache_np) >= self._cache_size:
+                self._cache_np.clear()
+            self._cache_np[text] = a
+        return a
+
+    @staticmethod
+    def _pair_lengths(n1: np.ndarray, n2: np.ndarray, max_length: int):
+        """truncate_pair's longest_first lengths, vectorised over pairs."""
+        target = max(0, int(max_length) - 3)
+        over = n1 + n2 > target
+        if not over.any():
+            return n1, n2
+        a1, a2 = n1.copy(), n2.copy()
+        swap = n1 > n2
+        s1, s2 = np.where(swap, n2, n1), np.where(swap, n1, n2)
+        t2 = np.where(s1 > target, s1, np.maximum(s1, target - s1))
+        both = s1 + t2 > target
+        t1 = np.where(both, target // 2, s1)
+        t2 = np.where(both, target // 2 + target % 2, t2)
+        a1 = np.where(over, np.where(swap, t2, t1), a1)
+        a2 = np.where(over, np.where(swap, t1, t2), a2)
+        return a1, a2
+
     def score_pairs(self, queries: list[str], passages: list[list[str]]):
         """Relevance (sigmoid of the cross-encoder logit) of every (query, passage) pair, as a list of
-        float32 device tensors, one per query."""
+        float32 device tensors, one per query.
+
+        Pairs are encoded [CLS] q [SEP] p [SEP] (token types 0 / 1, longest_first truncation; an empty
+        passage is the single sequence [CLS] q [SEP]) and run in length-sorted batches.  The batch
+        matrices are assembled with vectorised numpy from cached per-passage id arrays and staged in
+        pinned memory, so the host builds batch i+1 while the GPU runs batch i."""
         torch = self.torch
-        pairs = []  # (query index, passage index, ids, types)
-        for qi, (q, ps) in enumerate(zip(queries, passages)):
-            q_ids = self._text_ids(q, cache=False)
-            for pi, p in enumerate(ps):
-                ids, types = self._pair(q_ids, self._text_ids(p, cache=True), passage_is_empty=not p)
-                pairs.append((qi, pi, ids, types))
+        cls_id = getattr(self.tokenizer, "cls_token_id", 101)
+        sep_id = getattr(self.tokenizer, "sep_token_id", 102)
+        pad_id = getattr(self.tokenizer, "pad_token_id", 0) or 0
+        q_arr = [np.asarray(self._text_ids(q, cache=False), np.int64) for q in queries]
         offs = [0]
         for ps in passages:
             offs.append(offs[-1] + len(ps))
-        flat = torch.empty(offs[-1], dtype=torch.float32, device=self.device)
-        order = sorted(range(len(pairs)), key=lambda i: -len(pairs[i][2]))  # length-sorted batches
-        pad_id = getattr(self.tokenizer, "pad_token_id", 0) or 0
+        n = offs[-1]
+        flat = torch.empty(n, dtype=torch.float32, device=self.device)
+        if n == 0:
+            return [flat[offs[i]:offs[i + 1]] for i in range(len(queries))]
+        qi = np.repeat(np.arange(len(queries)), [len(ps) for ps in passages])
+        p_arr = [self._np_ids(p) if p else np.zeros(0, np.int64) for ps in passages for p in ps]
+        empty = np.fromiter((not p for ps in passages for p in ps), bool, n)
+        nq = np.fromiter((len(q_arr[i]) for i in qi), np.int64, n)
+        npass = np.fromiter((len(a) for a in p_arr), np.int64, n)
+        n1, n2 = self._pair_lengths(nq, npass, self.max_length)
+        n1 = np.where(empty, np.minimum(nq, max(0, self.max_length - 2)), n1)  # single sequence
+        n2 = np.where(empty, 0, n2)
+        total = np.where(empty, n1 + 2, n1 + n2 + 3)
+        order = np.argsort(-total, kind="stable")  # length-sorted batches (longest first)
+        pin = self.device.type == "cuda"
+        outs = []
         with torch.inference_mode():
-            for b0 in range(0, len(order), self.batch_size):
+            for b0 in range(0, n, self.batch_size):
                 sel = order[b0:b0 + self.batch_size]
-                width = len(pairs[sel[0]][2])
-                ids = np.full((len(sel), width), pad_id, dtype=np.int64)
-                types = np.zeros((len(sel), width), dtype=np.int64)
-                lens = np.empty(len(sel), dtype=np.int64)
-                dst = np.empty(len(sel), dtype=np.int64)
-                for row, i in enumerate(sel):
-                    qi, pi, t_ids, t_types = pairs[i]
-                    n = len(t_ids)
-                    ids[row, :n] = t_ids
-                    types[row, :n] = t_types
-                    lens[row] = n
-                    dst[row] = offs[qi] + pi
-                mask = (np.arange(width)[None, :] < lens[:, None]).astype(np.int64)
-                logits = self.model(input_ids=torch.from_numpy(ids).to(self.device, non_blocking=True),
-                                    attention_mask=torch.from_numpy(mask).to(self.device, non_blocking=True),
-                                    token_type_ids=torch.from_numpy(types).to(self.device, non_blocking=True)).logits
-                flat[torch.from_numpy(dst).to(self.device)] = torch.sigmoid(logits[:, 0].float())
+                nb, W = len(sel), int(total[sel[0]])
+                s1, s2, emp = n1[sel], n2[sel], empty[sel]
+                col = np.arange(W)[None, :]
+                ids = np.full((nb, W), pad_id, np.int64)
+                ids[:, 0] = cls_id
+                rows = np.arange(nb)
+                # query tokens at columns 1 .. n1, passage tokens at n1 + 2 .. n1 + n2 + 1
+                qr = np.repeat(rows, s1)
+                qc = 1 + np.arange(int(s1.sum())) - np.repeat(np.cumsum(s1) - s1, s1)
+                ids[qr, qc] = np.concatenate([q_arr[qi[j]][:k] for j, k in zip(sel, s1)]) if len(qr) else 0
+                ids[rows, 1 + s1] = sep_id
+                pr = np.repeat(rows, s2)
+                pc = (np.repeat(s1, s2) + 2 + np.arange(int(s2.sum())) - np.repeat(np.cumsum(s2) - s2, s2))
+                if len(pr):
+                    ids[pr, pc] = np.concatenate([p_arr[j][:k] for j, k in zip(sel, s2)])
+                has_b = ~emp
+                ids[rows[has_b], (s1 + s2 + 2)[has_b]] = sep_id
+                L = total[sel][:, None]
+                mask = (col < L).astype(np.int64)
+                types = ((col >= (s1 + 2)[:, None]) & (col < L) & has_b[:, None]).astype(np.int64)
+                t_ids, t_mask, t_types = (torch.from_numpy(x) for x in (ids, mask, types))
+                if pin:
+                    t_ids, t_mask, t_types = (t.pin_memory() for t in (t_ids, t_mask, t_types))
+                logits = self.model(input_ids=t_ids.to(self.device, non_blocking=pin),
+                                    attention_mask=t_mask.to(self.device, non_blocking=pin),
+                                    token_type_ids=t_types.to(self.device, non_blocking=pin)).logits
+                outs.append(torch.sigmoid(logits[:, 0].float()))
+            dst = torch.from_numpy(order)
+            if pin:
+                dst = dst.pin_memory()
+            flat[dst.to(self.device, non_blocking=pin)] = torch.cat(outs)
         return [flat[offs[i]:offs[i + 1]] for i in range(len(queries))]
 
     def _select(self, scores: list, top_ns: list[int]) -> list[list[tuple[int, float]]]:

@@ -1,7 +1,7 @@
 # A/B: corpus ring kept in issue order (sched barriers, scalar live/mask, default) vs the compiler's
 # schedule (libhiprag_ab.so built with -DHR_RING_SCHED=0); quick parity first
 set -e
-timeout -k 10 300 python -u -m pytest tests/test_gpu_index.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ring_tests.log 2>&1
+HIPRAG_LIB_OVERRIDE=$PWD/youtu-rag_amd/hiprag/libhiprag_ab.so timeout -k 10 300 python -u -m pytest tests/test_gpu_index.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ring_tests.log 2>&1
 for rep in 1 2; do
   for lib in youtu-rag_amd/hiprag/libhiprag.so youtu-rag_amd/hiprag/libhiprag_ab.so; do
     tag=$(basename $lib .so)_$rep

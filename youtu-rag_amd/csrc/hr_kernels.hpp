@@ -301,7 +301,9 @@ struct XFrag;
 // for the whole ring early in each batch of P k-steps and then issues the P refills back to back
 // (10M rows 3.15 vs 3.00 ms, 1.25M 0.442 vs 0.434, B = 128 4.96 vs 4.51; tools/ab_ring.sh): each wave
 // then sends one contiguous P KiB burst at a time, which the HBM serves better than P requests
-// trickled between the MFMAs of 8 waves.  Kept as an A/B build switch.
+// trickled between the MFMAs of 8 waves.  HR_RING_SCHED=2 double-buffers (compute half the ring, refill
+// it as one P/2 KiB burst while the other half is in flight): 1.25M 0.431 vs 0.433 ms, but 10M 3.18 vs
+// 3.06 ms and B = 128 4.76 vs 4.45 ms.  Both kept as A/B build switches; the default is the compiler's.
 #ifndef HR_RING_SCHED
 #define HR_RING_SCHED 0
 #endif
@@ -604,16 +606,14 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         for (int sb = 0; sb < S; sb += P) {
             const bool same = sb + P < S;
             const int64_t nc = same ? t * S + sb + P : tn * S;
-#if HR_RING_SCHED
+#if HR_RING_SCHED == 1
             // query fragments one k-step ahead (LDS latency under the MFMAs of the step before)
             u32x4 qn[QB];
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) qn[qb] = qs[(sb * QB + qb) * 64 + lane];
-#endif
 #pragma unroll
             for (int i = 0; i < P; ++i) {
                 const u32x4 xf = ring[i].get();
-#if HR_RING_SCHED
                 u32x4 qc[QB];
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) qc[qb] = qn[qb];
@@ -631,15 +631,37 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
                 // copy waits for its load: the ring drained to vmcnt(0..2) once per P chunks.
                 ring[i].load(a.rows, nc + i, lane);
                 __builtin_amdgcn_sched_barrier(0);
+            }
+#elif HR_RING_SCHED == 2
+            // double-buffered halves: compute half h, then refill it as one P/2 KiB burst while the
+            // other half's loads are in flight
+            constexpr int H = P / 2;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int j = 0; j < H; ++j) {
+                    const u32x4 xf = ring[h * H + j].get();
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb)
+                        acc[qb] = mfma32<MT>(qs[((sb + h * H + j) * QB + qb) * 64 + lane], xf, acc[qb]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < H; ++j) ring[h * H + j].load(a.rows, nc + h * H + j, lane);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #else
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                const u32x4 xf = ring[i].get();
                 ring[i].load(a.rows, nc + i, lane);
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const u32x4 qf = qs[((sb + i) * QB + qb) * 64 + lane];
                     acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
                 }
-#endif
             }
+#endif
         }
 
         // epilogue: (euclidean) approximate score, predicate, group max, threshold filter

@@ -257,10 +257,18 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     G = world
+    # rehearsal of the N > 1 flow on a one-GPU box (never the measured configuration): every rank on
+    # GPU 0 and the gloo backend, as HIPRAG_BENCH_REHEARSE=1 (the exchange then takes the host path)
+    rehearse = os.environ.get("HIPRAG_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if G > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     N, D, B, K = args.rows, args.dim, args.batch, args.k
     start = N * rank // G

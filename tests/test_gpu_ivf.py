@@ -32,7 +32,9 @@ def _build(x, nlist, dtype, metric="cosine", chunk=1 << 18):
 
 
 @pytest.mark.parametrize("dim,dtype,n,nlist,B,k", [(128, "bf16", 20000, 64, 32, 10), (96, "f16", 9000, 50, 17, 100),
-                                                   (256, "f32", 6000, 24, 40, 32), (1024, "f16", 30000, 128, 64, 100)])
+                                                   (256, "f32", 6000, 24, 40, 32), (1024, "f16", 30000, 128, 64, 100),
+                                                   (384, "bf16", 5000, 32, 20, 10), (768, "f16", 8000, 40, 33, 50),
+                                                   (1100, "bf16", 3000, 16, 9, 10)])
 def test_ivf_matches_oracle(dim, dtype, n, nlist, B, k):
     import torch
 

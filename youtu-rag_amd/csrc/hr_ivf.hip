@@ -104,6 +104,23 @@ constexpr int kTopkMax = 1024;
 __device__ inline uint64_t cand_key(const Cand& e) { return e.row < 0 ? 0ull : d2key(e.score); }
 __device__ inline uint64_t id_key(int64_t id) { return (uint64_t)id ^ 0x8000000000000000ull; }
 
+// f(record) for every record of a segment, this thread's share: U independent loads in flight per
+// iteration (one at a time left every radix pass waiting on one L2 round trip per record)
+template <class F>
+__device__ inline void for_each_record(const Cand* __restrict__ seg, int64_t n, F&& f) {
+    constexpr int U = 4;
+    const int64_t st = blockDim.x;
+    int64_t i = threadIdx.x;
+    for (; i + (U - 1) * st < n; i += U * st) {
+        Cand e[U];
+#pragma unroll
+        for (int r = 0; r < U; ++r) e[r] = seg[i + r * st];
+#pragma unroll
+        for (int r = 0; r < U; ++r) f(e[r]);
+    }
+    for (; i < n; i += st) f(seg[i]);
+}
+
 __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in, const int64_t* __restrict__ seg_off,
                                                     int seg_scale, int64_t seg_stride, int B, int m,
                                                     Cand* __restrict__ out) {
@@ -129,14 +146,12 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
         for (int shift = 56; shift >= 0; shift -= 8) {
             for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
             __syncthreads();
-            for (int64_t i = tid; i < n; i += blockDim.x) {
-                const Cand e = seg[i];
+            for_each_record(seg, n, [&](const Cand& e) {
                 const uint64_t k = cand_key(e);
-                if (k == 0) continue;
-                if (by_id && k != key_eq) continue;
+                if (k == 0 || (by_id && k != key_eq)) return;
                 const uint64_t v = by_id ? ~id_key(e.row) : k;  // ids: smallest first = largest complement
                 if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255], 1u);
-            }
+            });
             __syncthreads();
             if (tid == 0) {
                 int64_t need = sh_need, above = 0;
@@ -159,7 +174,7 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
     if (tid == 0) sh_cnt = 0;
     __syncthreads();
     int my = 0;
-    for (int64_t i = tid; i < n; i += blockDim.x) my += cand_key(seg[i]) != 0;
+    for_each_record(seg, n, [&](const Cand& e) { my += cand_key(e) != 0; });
     if (my) atomicAdd(&sh_cnt, my);
     __syncthreads();
     const int64_t n_valid = sh_cnt;
@@ -176,10 +191,10 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
         for (int shift = 56; shift >= 32; shift -= 8) {
             for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
             __syncthreads();
-            for (int64_t i = tid; i < n; i += blockDim.x) {
-                const uint64_t k = cand_key(seg[i]);
+            for_each_record(seg, n, [&](const Cand& e) {
+                const uint64_t k = cand_key(e);
                 if (k != 0 && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
-            }
+            });
             __syncthreads();
             if (tid == 0) {
                 int64_t need = sh_need, above = 0;
@@ -198,17 +213,16 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
         // records with upper key >= the m-th: gather if they fit
         if (tid == 0) sh_cnt = 0;
         __syncthreads();
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            const Cand e = seg[i];
+        for_each_record(seg, n, [&](const Cand& e) {
             const uint64_t k = cand_key(e);
-            if (k == 0 || (k & mask) < prefix) continue;
+            if (k == 0 || (k & mask) < prefix) return;
             const int p = atomicAdd(&sh_cnt, 1);
             if (p < kTopkMax) {
                 skey[p] = k;
                 sid[p] = e.row;
                 ssc[p] = e.score;
             }
-        }
+        });
         __syncthreads();
         done = sh_cnt <= kTopkMax;
         __syncthreads();
@@ -221,7 +235,7 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
         if (tid == 0) sh_cnt = 0;
         __syncthreads();
         int t = 0;
-        for (int64_t i = tid; i < n; i += blockDim.x) t += cand_key(seg[i]) == kth;
+        for_each_record(seg, n, [&](const Cand& e) { t += cand_key(e) == kth; });
         if (t) atomicAdd(&sh_cnt, t);
         __syncthreads();
         const int64_t n_ties = sh_cnt;
@@ -233,19 +247,18 @@ __global__ __launch_bounds__(1024) void k_topk_cand(const Cand* __restrict__ in,
     if (!done || n_valid <= m) {
     if (tid == 0) sh_cnt = 0;
     __syncthreads();
-    for (int64_t i = tid; i < n; i += blockDim.x) {
-        const Cand e = seg[i];
+    for_each_record(seg, n, [&](const Cand& e) {
         const uint64_t k = cand_key(e);
-        if (k == 0) continue;
-        bool win = n_valid <= m || k > kth || (k == kth && ~id_key(e.row) >= id_thr);
-        if (!win) continue;
+        if (k == 0) return;
+        const bool win = n_valid <= m || k > kth || (k == kth && ~id_key(e.row) >= id_thr);
+        if (!win) return;
         const int p = atomicAdd(&sh_cnt, 1);
         if (p < kTopkMax) {
             skey[p] = k;
             sid[p] = e.row;
             ssc[p] = e.score;
         }
-    }
+    });
     }
     __syncthreads();
     const int cnt = sh_cnt < kTopkMax ? sh_cnt : kTopkMax;

@@ -57,6 +57,25 @@ class _Slot:
         self.fail_h = torch.empty((B,), dtype=torch.int32, pin_memory=pinned)
         self.event = torch.cuda.Event() if pinned else None
         self.ticket = None  # (q, k, s_out, r_out, mask_ptr, B) while in flight
+        self._views: dict = {}
+
+    def views(self, B: int, kc: int):
+        """(L, record, cand, bound) of a B-query batch -- cached: views cost host time every batch."""
+        v = self._views.get(("r", B))
+        if v is None:
+            L = _record_len(B, kc)
+            rec = self.rec[:L]
+            v = self._views[("r", B)] = (L, rec, *_record_views(rec, B, kc))
+        return v
+
+    def views_all(self, B: int, kc: int, G: int):
+        """(rec_all, cand_all, bound_all, kth, fail) of a B-query batch over G ranks (cached)."""
+        v = self._views.get(("a", B))
+        if v is None:
+            L, rec = self.views(B, kc)[:2]
+            rec_all = rec.view(1, L) if G == 1 else self.rec_all.view(-1)[: G * L].view(G, L)
+            v = self._views[("a", B)] = (rec_all, *_record_views(rec_all, B, kc), self.kth[:B], self.fail[:B])
+        return v
 
 
 class ShardedSearch:
@@ -76,6 +95,7 @@ class ShardedSearch:
         self.max_batch = int(max_batch)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         pinned = self.device.type == "cuda"
+        self._dev_index = self.device.index if self.device.index is not None else 0
         self.slots = [_Slot(torch, self.device, self.G, self.max_batch, self.kc, pinned) for _ in range(max(1, depth))]
         self._next = 0
         # tail stream: select/rescore, all-gather, merge and the flag copy of each batch
@@ -83,6 +103,11 @@ class ShardedSearch:
 
     # hooks (overridden in CPU tests of the orchestration logic)
     def _stream(self) -> int:
+        # the raw handle of the current stream without torch.cuda.current_stream's Python layers (called
+        # several times per batch; on a small collection the host submission bounds the step)
+        raw = getattr(self.torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            return raw(self._dev_index)
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
     def _merge(self, cand_all, bound_all, G, B, kc, k, s_out, r_out, kth, fail):
@@ -137,9 +162,7 @@ class ShardedSearch:
         q = q.contiguous()
         s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
         r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
-        L = _record_len(B, self.kc)
-        rec = slot.rec[:L]
-        cand, bound = _record_views(rec, B, self.kc)
+        L, rec, cand, bound = slot.views(B, self.kc)
         self._shard_search(q, k, cand, bound, mask_ptr, q_ready)
         if self.tail is not None:
             # The caller's earlier writes to s_out/r_out (allocation, earlier use) were enqueued on its
@@ -155,13 +178,9 @@ class ShardedSearch:
 
     def _exchange_and_merge(self, slot, rec, L, B, k, s_out, r_out):
         torch = self.torch
-        if self.G == 1:  # nothing to exchange: merge straight from this shard's candidates
-            rec_all = rec.view(1, L)
-        else:  # ONE collective per batch: every rank's packed record
-            rec_all = slot.rec_all.view(-1)[: self.G * L].view(self.G, L)
+        rec_all, cand_all, bound_all, kth, fail = slot.views_all(B, self.kc, self.G)
+        if self.G > 1:  # ONE collective per batch: every rank's packed record
             self._all_gather(rec_all, rec)
-        cand_all, bound_all = _record_views(rec_all, B, self.kc)
-        kth, fail = slot.kth[:B], slot.fail[:B]
         self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
         if slot.event is not None:
             slot.fail_h[:B].copy_(fail, non_blocking=True)

@@ -90,6 +90,10 @@ def _worker(rank, world, port, result_path):
 
     ss = CpuSharded(index=None, row_offset=lo, max_batch=B, device=torch.device("cpu"))
     s, r = ss.search(torch.from_numpy(q), K)
+    # the same batch known only to rank 1: broadcast first (src_rank), identical results
+    q_in = torch.from_numpy(q) if rank == 1 else torch.zeros((B, DIM))
+    s2, r2 = ss.search(q_in, K, src_rank=1)
+    assert torch.equal(s2, s) and torch.equal(r2, r)
     if rank == 0:
         np.savez(result_path, s=s.numpy(), r=r.numpy())
     dist.barrier()

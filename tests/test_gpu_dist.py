@@ -56,6 +56,13 @@ def _worker(rank, world, port, path):
     r2 = torch.empty_like(r)
     ss.finalize(ss.submit(q, K, s_out=s2, r_out=r2))  # pipelined entry points agree
     assert torch.equal(r, r2) and torch.equal(s, s2)
+    # the batch known to rank 0 only, broadcast before the scan (early SAMPLE waits for the broadcast)
+    ready = torch.cuda.Event()
+    ready.record()
+    q_in = q if rank == 0 else torch.zeros_like(q)
+    s3, r3 = torch.empty_like(s), torch.empty_like(r)
+    ss.finalize(ss.submit(q_in, K, s_out=s3, r_out=r3, q_ready=ready, src_rank=0))
+    assert torch.equal(r, r3) and torch.equal(s, s3)
     np.savez(f"{path}.{rank}.npz", s=s.cpu().numpy(), r=r.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()

@@ -58,6 +58,16 @@ class _Slot:
         self.event = torch.cuda.Event() if pinned else None
         self.ticket = None  # (q, k, s_out, r_out, mask_ptr, B) while in flight
         self._views: dict = {}
+        self._qbuf = None
+        self.q_event = torch.cuda.Event() if pinned else None
+
+    def qbuf(self, shape, dtype):
+        """This slot's query buffer for broadcast batches (the slot owns it until finalize)."""
+        import torch
+
+        if self._qbuf is None or self._qbuf.shape != shape or self._qbuf.dtype != dtype:
+            self._qbuf = torch.empty(shape, dtype=dtype, device=self.kth.device)
+        return self._qbuf
 
     def views(self, B: int, kc: int):
         """(L, record, cand, bound) of a B-query batch -- cached: views cost host time every batch."""
@@ -143,7 +153,15 @@ class ShardedSearch:
                 self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
     # the search
-    def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0, q_ready=None):
+    def _broadcast(self, t, src: int):
+        if t.is_cuda and self.dist.get_backend(self.group) != "nccl":  # gloo (tests): host staging
+            h = t.cpu()
+            self.dist.broadcast(h, src, group=self.group)
+            t.copy_(h)
+        else:
+            self.dist.broadcast(t, src, group=self.group)
+
+    def submit(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0, q_ready=None, src_rank: int | None = None):
         """Enqueue one batch; returns a ticket for finalize().  q: (B, dim) float32 device tensor,
         identical on every rank.  q_ready: optional recorded torch.cuda.Event after which q (and
         the mask) are ready; then a large shard preps the queries and runs its SAMPLE pass beside
@@ -160,6 +178,16 @@ class ShardedSearch:
         if slot.ticket is not None:
             self.finalize(slot)
         q = q.contiguous()
+        if src_rank is not None and self.G > 1:
+            # the batch arrives on one rank: ONE broadcast (RCCL over xGMI, 4*B*dim bytes) on the scan
+            # stream puts it on every rank before the scan (queries sent with a broadcast)
+            qb = slot.qbuf(q.shape, q.dtype)
+            qb.copy_(q)
+            self._broadcast(qb, src_rank)
+            q = qb
+            if q_ready is not None:  # the early SAMPLE must wait for the broadcast, not the caller's event
+                q_ready = slot.q_event
+                q_ready.record()
         s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
         r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
         L, rec, cand, bound = slot.views(B, self.kc)
@@ -207,10 +235,11 @@ class ShardedSearch:
             if slot.ticket is not None:
                 self.finalize(slot)
 
-    def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0):
-        """Synchronous search of one batch.  Returns (scores, rows) device tensors."""
+    def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0, src_rank: int | None = None):
+        """Synchronous search of one batch.  Returns (scores, rows) device tensors.  src_rank: the batch
+        is only valid on that rank and is broadcast first (other ranks pass a tensor of the same shape)."""
         self.finalize_all()
-        return self.finalize(self.submit(q, k, s_out, r_out, mask_ptr))
+        return self.finalize(self.submit(q, k, s_out, r_out, mask_ptr, src_rank=src_rank))
 
     def _fallback(self, q, k, failed, kth, s_out, r_out, mask_ptr):
         torch = self.torch

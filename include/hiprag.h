@@ -190,6 +190,10 @@ int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query
 /* Diagnostics: cumulative counters since creation -- out[0] main scan passes, out[1] queries that
  * failed the exactness guard (collect fallback), out[2] queries answered by the exhaustive pass. */
 int hr_index_stats(hr_index* h, int64_t out[3]);
+/* Diagnostics: hr_index_search calls answered by replaying a captured HIP graph (an unmasked,
+ * untimed search with k <= HR_MAX_K, from the second call of a (B, k) shape on; HIPRAG_SYNC_GRAPH=0
+ * turns the graphs off).  The results are those of the normal path: the graph is that path, captured. */
+int hr_index_graph_replays(hr_index* h, int64_t* out);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

@@ -396,6 +396,59 @@ def test_massive_ties_use_exact_fallback(native):
     np.testing.assert_array_equal(r[0], dups[:10])
 
 
+def test_graph_replay_vs_oracle(native):
+    """hr_index_search from the second call of a (B, k) shape on replays a captured HIP graph
+    (hr_index_graph_replays): its results must be the oracle's on every call -- new queries each
+    time, after an add (rows grow: the graph is recaptured), after a remove (live bits change on
+    the device: the same graph still applies), with a guard failure (massive ties: the fallback
+    runs after the replay), and beside masked and large-k calls that take the normal path."""
+    rng = np.random.default_rng(21)
+    dim, n = 256, 6000
+    raw = R.gen_rows(13, 0, n + 1500, dim)
+    dups = np.sort(rng.choice(n, 60, replace=False))
+    raw[dups] = raw[dups[0]]
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw[:n])
+    alive = np.zeros(n + 1500, bool)
+    alive[:n] = True
+    stored = R.process_rows(raw, "cosine", "bf16")
+
+    def run(q, k, mask=None):
+        s, r = idx.search(q, k, None if mask is None else oracle.mask_from_bool(mask))
+        eff = alive[: idx.size()[0]] if mask is None else (alive[: idx.size()[0]] & mask)
+        s_ref, r_ref = oracle.c_search(stored[: idx.size()[0]], "bf16", R.process_queries(q, "cosine"), k,
+                                       oracle.mask_from_bool(eff))
+        _check(s, r, s_ref, r_ref)
+        return r
+
+    r0 = idx.graph_replays()
+    for it in range(4):
+        run(_planted_queries(raw[:n], 16, rng), 10)
+        run(_planted_queries(raw[:n], 1, rng), 5)
+    assert idx.graph_replays() - r0 >= 6  # each shape: first call normal, then replays
+    # ties: the replayed pass flags the guard, the exact fallback finishes the query
+    q_t = np.concatenate([raw[dups[:1]], _planted_queries(raw[:n], 15, rng)])
+    before = idx.stats()["guard_failures"]
+    for _ in range(2):
+        r = run(q_t, 10)
+        np.testing.assert_array_equal(r[0], dups[:10])
+    assert idx.stats()["guard_failures"] >= before + 2
+    # a masked call and a k > HR_MAX_K call in between take the normal path
+    run(_planted_queries(raw[:n], 16, rng), 10, rng.random(n) < 0.5)
+    run(_planted_queries(raw[:n], 2, rng), native.HR_MAX_K + 3)
+    # remove: live bits change in place, the captured graph reads them at run time
+    gone = rng.choice(n, 500, replace=False)
+    idx.remove(gone)
+    alive[gone] = False
+    run(_planted_queries(raw[:n], 16, rng), 10)
+    # add: the row count changes, the graph is recaptured for the new size
+    idx.add(raw[n:])
+    alive[n:] = True
+    for _ in range(3):
+        run(_planted_queries(raw, 16, rng), 10)
+    assert idx.graph_replays() - r0 >= 10
+
+
 def test_save_load_roundtrip(native, tmp_path):
     raw = R.gen_rows(4, 0, 1500, 192)
     idx = native.NativeIndex(192, "f16", "cosine")

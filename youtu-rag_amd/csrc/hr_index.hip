@@ -834,10 +834,9 @@ int launch_merge(int device, const Cand* cand, const double* bounds, int G, int 
 }
 
 
-// full single-shard search on device-resident queries, with the exact fallback
-static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
-                              int64_t* r_out, hipStream_t st) {
-    if (int rc = validate_search(h, B, k)) return rc;
+// main pass of a single-shard search on device-resident queries: candidates, merge, guard flags
+static int search_main(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
+                       int64_t* r_out, hipStream_t st) {
     const int kc = hr_kc_for_k(k);
     HIP_TRY(h->cand.ensure((size_t)B * kc * sizeof(Cand)));
     HIP_TRY(h->bound.ensure((size_t)B * 8));
@@ -845,21 +844,15 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     HIP_TRY(h->fail.ensure((size_t)B * 4));
     if (int rc = shard_search(h, q_dev, B, kc, mask_dev, 0, h->cand.as<Cand>(), h->bound.as<double>(), st, st))
         return rc;
-    if (int rc = launch_merge(h->device, h->cand.as<Cand>(), h->bound.as<double>(), 1, B, kc, k, s_out, r_out,
-                              h->kth.as<double>(), h->fail.as<int32_t>(), st))
-        return rc;
-    std::vector<int32_t> fail((size_t)B);
-    std::vector<double> kth((size_t)B);
-    HIP_TRY(hipMemcpyAsync(fail.data(), h->fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(kth.data(), h->kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    std::vector<int> failed;
-    for (int b = 0; b < B; ++b)
-        if (fail[(size_t)b]) failed.push_back(b);
-    if (failed.empty()) return HR_OK;
+    return launch_merge(h->device, h->cand.as<Cand>(), h->bound.as<double>(), 1, B, kc, k, s_out, r_out,
+                        h->kth.as<double>(), h->fail.as<int32_t>(), st);
+}
+
+// exact fallback for the queries whose guard failed: ONE collect re-scan of all of them (every row
+// with approx >= kth - E, rescored exactly), merged, then scattered back to their rows of the outputs
+static int search_fallback(hr_index* h, const float* q_dev, int k, const uint64_t* mask_dev, float* s_out,
+                           int64_t* r_out, const std::vector<int>& failed, const double* kth, hipStream_t st) {
     h->n_guard_fail += (int64_t)failed.size();
-    // exact fallback: ONE collect re-scan of all failing queries (every row with approx >= kth - E,
-    // rescored exactly), merged, then scattered back to the failing rows of the outputs
     const int nf = (int)failed.size(), kc2 = kFallbackCapMax;
     HIP_TRY(h->fb_q.ensure((size_t)nf * h->dim * 4));
     HIP_TRY(h->fb_cand.ensure((size_t)nf * kc2 * sizeof(Cand)));
@@ -871,7 +864,7 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     int32_t* ff = (int32_t*)(fk + nf);
     std::vector<double> kf((size_t)nf);
     for (int i = 0; i < nf; ++i) {
-        kf[(size_t)i] = kth[(size_t)failed[(size_t)i]];
+        kf[(size_t)i] = kth[failed[(size_t)i]];
         HIP_TRY(hipMemcpyAsync(h->fb_q.as<float>() + (int64_t)i * h->dim, q_dev + (int64_t)failed[(size_t)i] * h->dim,
                                (size_t)h->dim * 4, hipMemcpyDeviceToDevice, st));
     }
@@ -896,6 +889,137 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
     HIP_TRY(hipStreamSynchronize(st));
     for (int i = 0; i < nf; ++i)
         if (ff_h[(size_t)i]) return set_err(HR_E_OVERFLOW, "exact fallback overflowed its candidate buffer (massive ties?)");
+    return HR_OK;
+}
+
+// full single-shard search on device-resident queries, with the exact fallback
+static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
+                              int64_t* r_out, hipStream_t st) {
+    if (int rc = validate_search(h, B, k)) return rc;
+    if (int rc = search_main(h, q_dev, B, k, mask_dev, s_out, r_out, st)) return rc;
+    std::vector<int32_t> fail((size_t)B);
+    std::vector<double> kth((size_t)B);
+    HIP_TRY(hipMemcpyAsync(fail.data(), h->fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(kth.data(), h->kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[(size_t)b]) failed.push_back(b);
+    if (failed.empty()) return HR_OK;
+    return search_fallback(h, q_dev, k, mask_dev, s_out, r_out, failed, kth.data(), st);
+}
+
+// hr_index_search through a captured HIP graph (no mask, k <= HR_MAX_K, untimed): the host work of a
+// small search -- ~10 launches, 6 copies, 2 waits -- was most of its latency on small collections.
+// Returns HR_E_UNSUPPORTED when the normal path must run instead (a shape's first use, a failed capture).
+static int sync_graph_search(hr_index* h, const float* q, int B, int k, float* scores_out, int64_t* rows_out) {
+    hipStream_t st = h->stream;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t qb = (size_t)B * h->dim * 4, sb = (size_t)B * k * 4, rb = (size_t)B * k * 8;
+    const size_t o_s = up(qb), o_r = o_s + up(sb), o_f = o_r + up(rb), o_k = o_f + up((size_t)B * 4);
+    const size_t total = o_k + up((size_t)B * 8);
+    hr_index::SyncGraph* e = nullptr;
+    for (auto& g : h->sync_graphs)
+        if (g.B == B && g.k == k) e = &g;
+    if (!e) {
+        if (h->sync_graphs.size() >= 16) {  // bounded cache: drop the oldest shape
+            if (h->sync_graphs.front().exec) (void)hipGraphExecDestroy(h->sync_graphs.front().exec);
+            h->sync_graphs.erase(h->sync_graphs.begin());
+        }
+        h->sync_graphs.push_back({});
+        e = &h->sync_graphs.back();
+        e->B = B;
+        e->k = k;
+    }
+    if (e->disabled) return HR_E_UNSUPPORTED;
+    auto current = [&](const hr_index::SyncGraph& g) {
+        return g.exec && g.n == h->n && g.rows == h->rows && g.live == h->live && g.xnorm == h->xnorm &&
+               g.max_norm2 == h->max_norm2 && g.pin == h->pin && g.buf_gen == g_buf_gen.load();
+    };
+    if (!current(*e)) {
+        if (e->exec) {  // stale: recapture right away after a buffer moved; after the rows changed
+            // (add, compaction) the normal path runs once first, to size the buffers for the new count
+            (void)hipGraphExecDestroy(e->exec);
+            e->exec = nullptr;
+            if (e->n != h->n || e->rows != h->rows || e->live != h->live || e->xnorm != h->xnorm) e->uses = 0;
+        }
+        // first use of the shape: the normal path runs and sizes every buffer the pass needs, so the
+        // capture below allocates nothing (an allocation fails the capture, or bumps g_buf_gen, and
+        // the shape then takes the normal path once more)
+        if (++e->uses < 2) return HR_E_UNSUPPORTED;
+        if (h->pin_bytes < total) {
+            if (h->pin) (void)hipHostFree(h->pin);
+            h->pin = nullptr;
+            h->pin_bytes = 0;
+            HIP_TRY(hipHostMalloc(&h->pin, total, hipHostMallocDefault));
+            h->pin_bytes = total;
+        }
+        HIP_TRY(h->q_in.ensure(qb));
+        HIP_TRY(h->sync_out.ensure(up(sb) + rb));
+        // captured on a stream of its own: a failed capture can leave its stream unusable
+        hipStream_t cs = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        const uint64_t gen0 = g_buf_gen.load();
+        uint8_t* pin = (uint8_t*)h->pin;
+        float* s_dev = h->sync_out.as<float>();
+        int64_t* r_dev = (int64_t*)(h->sync_out.as<uint8_t>() + up(sb));
+        const int64_t passes0 = h->main_passes;
+        const bool began = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        int rc = began ? HR_OK : HR_E_HIP;
+        if (!rc && hipMemcpyAsync(h->q_in.p, pin, qb, hipMemcpyHostToDevice, cs) != hipSuccess) rc = HR_E_HIP;
+        if (!rc) rc = search_main(h, h->q_in.as<float>(), B, k, nullptr, s_dev, r_dev, cs);
+        if (!rc && (hipMemcpyAsync(pin + o_s, s_dev, sb, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                    hipMemcpyAsync(pin + o_r, r_dev, rb, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                    hipMemcpyAsync(pin + o_f, h->fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                    hipMemcpyAsync(pin + o_k, h->kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, cs) != hipSuccess))
+            rc = HR_E_HIP;
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = began ? hipStreamEndCapture(cs, &graph) : hipErrorUnknown;
+        const bool moved = g_buf_gen.load() != gen0;  // a buffer was reallocated while capturing
+        if (!rc && ec == hipSuccess && graph && !moved)
+            rc = hipGraphInstantiate(&e->exec, graph, nullptr, nullptr, 0) == hipSuccess ? HR_OK : HR_E_HIP;
+        else
+            rc = HR_E_HIP;
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipStreamDestroy(cs);
+        (void)hipGetLastError();
+        e->chunks = (int)std::max<int64_t>(1, h->main_passes - passes0);
+        h->main_passes = passes0;  // (nothing ran: the replays count their passes)
+        if (rc) {
+            e->exec = nullptr;
+            e->uses = 0;
+            if (!moved) e->disabled = true;  // the capture itself failed: this shape keeps the normal path
+            return HR_E_UNSUPPORTED;
+        }
+        e->n = h->n;
+        e->rows = h->rows;
+        e->live = h->live;
+        e->xnorm = h->xnorm;
+        e->max_norm2 = h->max_norm2;
+        e->pin = h->pin;
+        e->buf_gen = gen0;
+    }
+    uint8_t* pin = (uint8_t*)h->pin;
+    std::memcpy(pin, q, qb);
+    HIP_TRY(hipGraphLaunch(e->exec, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    h->main_passes += e->chunks;
+    h->n_graph_replays++;
+    const int32_t* fail = (const int32_t*)(pin + o_f);
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[b]) failed.push_back(b);
+    if (failed.empty()) {
+        std::memcpy(scores_out, pin + o_s, sb);
+        std::memcpy(rows_out, pin + o_r, rb);
+        return HR_OK;
+    }
+    float* s_dev = h->sync_out.as<float>();
+    int64_t* r_dev = (int64_t*)(h->sync_out.as<uint8_t>() + up(sb));
+    if (int rc = search_fallback(h, h->q_in.as<float>(), k, nullptr, s_dev, r_dev, failed, (const double*)(pin + o_k), st))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(scores_out, s_dev, sb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(rows_out, r_dev, rb, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return HR_OK;
 }
@@ -1000,6 +1124,11 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
             rows_out[i] = -1;
         }
         return HR_OK;
+    }
+    static const int graph_env = getenv("HIPRAG_SYNC_GRAPH") ? atoi(getenv("HIPRAG_SYNC_GRAPH")) : 1;
+    if (graph_env && !row_mask && k <= HR_MAX_K && h->time_every == 0) {
+        const int rc = sync_graph_search(h, q, B, k, scores_out, rows_out);
+        if (rc != HR_E_UNSUPPORTED) return rc;
     }
     HIP_TRY(h->q_in.ensure((size_t)B * h->dim * 4));
     DevBuf& so = h->stage;
@@ -1347,8 +1476,11 @@ extern "C" void hr_index_destroy(hr_index* h) {
     if (h->xnorm) (void)hipFree(h->xnorm);
     if (h->norm_bits) (void)hipFree(h->norm_bits);
     (void)hipDeviceSynchronize();  // pipelined batches may still run on caller streams
+    for (auto& g : h->sync_graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (h->pin) (void)hipHostFree(h->pin);
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
-                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl, &h->s_mask,
+                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl, &h->s_mask, &h->sync_out,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();
@@ -1423,6 +1555,13 @@ extern "C" int hr_index_stats(hr_index* h, int64_t out[3]) {
     out[1] = h->n_guard_fail;
     out[2] = h->n_exhaustive;
     if (h->G > 1) group_stats(h, out);
+    return HR_OK;
+}
+
+extern "C" int hr_index_graph_replays(hr_index* h, int64_t* out) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *out = h->n_graph_replays;
     return HR_OK;
 }
 

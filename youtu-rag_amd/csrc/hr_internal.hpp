@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <unistd.h>
+#include <atomic>
 
 #include <algorithm>
 #include <cmath>
@@ -29,6 +30,10 @@ int set_err(int code, const std::string& msg);  // thread-local message for hr_l
     } while (0)
 
 // ---------------------------------------------------------------- device buffers
+// bumped whenever a work buffer is (re)allocated or freed: a captured HIP graph holds raw buffer
+// addresses, so a graph captured before the bump is stale (see SyncGraph)
+inline std::atomic<uint64_t> g_buf_gen{0};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -37,12 +42,16 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
+        g_buf_gen.fetch_add(1);
         hipError_t e = hipMalloc(&p, need);
         if (e == hipSuccess) bytes = need;
         return e;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            g_buf_gen.fetch_add(1);
+        }
         p = nullptr;
         bytes = 0;
     }
@@ -135,6 +144,28 @@ struct hr_index {
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
     int64_t n_guard_fail = 0;         // queries that failed the exactness guard (collect fallback)
     std::vector<float> floor_host;
+    // ---- hr_index_search (host queries, no mask) replayed as one HIP graph per batch shape: H2D of
+    // the queries from pinned staging, prep, SAMPLE, FILTER, select, rescore, merge, D2H of results
+    // and guard flags.  Captured on a shape's second use (the first allocates every buffer); stale once
+    // the corpus, its buffers or any work buffer changes (address / size snapshot below).
+    struct SyncGraph {
+        int B = 0, k = 0, uses = 0;
+        bool disabled = false;
+        int64_t n = -1;
+        const void* rows = nullptr;
+        const void* live = nullptr;
+        const void* xnorm = nullptr;
+        const void* pin = nullptr;
+        double max_norm2 = 0.0;
+        uint64_t buf_gen = 0;
+        int chunks = 1;
+        hipGraphExec_t exec = nullptr;
+    };
+    std::vector<SyncGraph> sync_graphs;
+    void* pin = nullptr;      // pinned host staging of the graph path (hipHostMalloc)
+    size_t pin_bytes = 0;
+    DevBuf sync_out;          // device results of the graph path
+    int64_t n_graph_replays = 0;
     // ---- multi-device handles (hr_index_create with n_dev > 1, hr_group.hip)
     // A group handle owns G shard handles (one per dev_ids entry, repeats allowed) and stripes its
     // rows over them by 32-row tile (stripe_row, hr_common.hpp); it holds no rows itself.  Its

@@ -41,7 +41,7 @@ EXPORTS = [
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
-    "hr_add_layernorm", "hr_index_info",
+    "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays",
 ]
 
 _lib = None
@@ -105,6 +105,7 @@ def load_library(path: str | None = None):
             "hr_index_debug_approx": [vp, vp, i32, vp, vp],
             "hr_index_last_candidates": [vp, vp, vp],
             "hr_index_stats": [vp, vp],
+            "hr_index_graph_replays": [vp, vp],
             "hr_add_layernorm": [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, i32, vp],
         }
         for name, args in sig.items():
@@ -299,6 +300,12 @@ class NativeIndex:
         out = (ctypes.c_int64 * 3)()
         _check(self.lib.hr_index_stats(self._h, out))
         return {"main_passes": out[0], "guard_failures": out[1], "exhaustive": out[2]}
+
+    def graph_replays(self) -> int:
+        """hr_index_search calls answered by a captured HIP graph (hr_index_graph_replays)."""
+        n = ctypes.c_int64(0)
+        _check(self.lib.hr_index_graph_replays(self._h, ctypes.byref(n)))
+        return n.value
 
     def set_scan_timing(self, every: int) -> None:
         """Record HIP events around every `every`-th main-pass scan (0 = off, the default)."""

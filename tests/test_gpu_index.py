@@ -767,7 +767,9 @@ def test_fuzz_filters_and_large_k_vs_oracle(native, case):
 # ---------------------------------------------------------------- query groups: > 64 queries per corpus pass
 @pytest.mark.parametrize("dim,dtype,n,B,k", [(1024, "bf16", 60_000, 256, 10), (768, "f16", 40_000, 200, 100),
                                              (256, "bf16", 30_000, 65, 32), (1024, "bf16", 9_000, 128, 128),
-                                             (128, "f32", 20_000, 150, 10)])
+                                             (128, "f32", 20_000, 150, 10), (1024, "bf16", 100_000, 128, 10),
+                                             (768, "bf16", 50_000, 100, 20), (1024, "f16", 30_000, 150, 5),
+                                             (768, "f16", 20_000, 192, 32)])
 def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
     """B > 64: ceil(B/64) workgroup groups stream the same tiles in one pass (one XCD per range
     block), each with 64 queries in LDS; per-group private candidate regions, thresholds and
@@ -787,6 +789,41 @@ def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
         _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk))
         parts = [idx.search(q[i:i + 64], k, mk) for i in range(0, B, 64)]
         np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))
+
+
+@pytest.mark.parametrize("dim,dtype,metric", [(1024, "bf16", "cosine"), (768, "f16", "cosine"), (1024, "bf16", "ip")])
+def test_wide_filter_edges_vs_oracle(native, dim, dtype, metric):
+    """The wide FILTER (k_scan_wide: 128 queries per workgroup, LDS-DMA corpus ring; 65..256 queries,
+    k <= 32, D = 768 / 1024): fewer tiles than workgroups, ragged ranges, a selective filter (tile
+    list), a removed stretch, and massive ties that overflow a region's 256 candidate slots (the
+    guard then sends the query to the exact fallback) -- identical to the oracle every time."""
+    rng = np.random.default_rng(dim + 3)
+    for n, B, k in ((500, 65, 10), (9_001, 128, 32), (70_000, 256, 1), (40_000, 130, 16)):
+        raw = R.gen_rows(31, 0, n, dim)
+        if n == 40_000:  # 600 copies of one row inside one workgroup's range
+            raw[1000:1600] = raw[1000]
+        idx = native.NativeIndex(dim, dtype, metric)
+        idx.add(raw)
+        stored = R.process_rows(raw, metric, dtype)
+        q = np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)])
+        if n == 40_000:
+            q[:3] = raw[1000]
+        qn = R.process_queries(q, metric)
+        sel = np.zeros(n, bool)
+        sel[n // 3: n // 3 + max(40, n // 50)] = True
+        for mask in (None, sel):
+            mk = None if mask is None else oracle.mask_from_bool(mask)
+            s, r = idx.search(q, k, mk)
+            _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk, metric=metric))
+        if n == 40_000:
+            s, r = idx.search(q, k)
+            np.testing.assert_array_equal(r[0], np.arange(1000, 1000 + k))
+        gone = np.arange(n // 2, n // 2 + n // 10)
+        idx.remove(gone)
+        live = np.ones(n, bool)
+        live[gone] = False
+        s, r = idx.search(q, k)
+        _check(s, r, *oracle.c_search(stored, dtype, qn, k, oracle.mask_from_bool(live), metric=metric))
 
 
 def test_query_groups_pipelined_vs_oracle(native):

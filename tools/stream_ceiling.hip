@@ -7,6 +7,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_ceiling.hip -o tools/stream_ceiling
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -105,6 +106,45 @@ __global__ __launch_bounds__(512) void k_stream_pin(const u32x4* __restrict__ sr
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
 }
 
+// The query-group launch's access shape without its arithmetic: ng workgroups per range block (equal
+// blockIdx % 8, so one XCD), each streaming the SAME tiles in the same order with default-policy loads
+// (the first to touch a line brings it into L2, the others hit or wait on the same fill) -- the memory
+// system's own ceiling for B = ng x 64 queries, and how it moves with waves per CU.
+template <int P>
+__global__ __launch_bounds__(1024) void k_stream_groups(const u32x4* __restrict__ src, long long n_chunks, int ng,
+                                                        unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const int bx = blockIdx.x;
+    const long long nrb = gridDim.x / ng;
+    const long long rb = ng > 1 ? (long long)((bx >> 3) / ng) * 8 + (bx & 7) : bx;
+    const long long W = nrb * (blockDim.x >> 6);
+    const long long w = (long long)(threadIdx.x >> 6) * nrb + rb;
+    const long long base = n_chunks / W, rem = n_chunks % W;
+    const long long c0 = w * base + (w < rem ? w : rem);
+    const long long c1 = c0 + base + (w < rem ? 1 : 0);
+    u32x4 ring[P];
+    u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < P; ++i) ring[i] = (c0 + i < c1) ? src[(c0 + i) * 64 + lane] : u32x4{0u, 0u, 0u, 0u};
+    long long c = c0;
+    for (; c + 2 * P <= c1; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            acc ^= ring[i];
+            ring[i] = src[(c + P + i) * 64 + lane];
+        }
+    }
+    for (; c < c1; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            if (c + i < c1) acc ^= ring[i];
+            const long long nx = c + P + i;
+            if (nx < c1) ring[i] = src[nx * 64 + lane];
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
+}
+
 template <bool NT, int P>
 static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
     hipEvent_t a, b;
@@ -177,6 +217,31 @@ int main(int argc, char** argv) {
                         "\"ms\": %.4f, \"TBps\": %.4f, \"frac_of_8TBps\": %.4f}\n",
                         pin >= (1 << 30) ? 0 : pin, bytes, pinned, t, bytes / (t * 1e-3) / 1e12, bytes / (t * 1e-3) / 8e12);
         }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+    }
+    if (argc > 2 && atoi(argv[2]) == 3) {  // query-group access shape: ng x waves per CU
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        const int cus = n_cu - 32;
+        for (int ng : {1, 2, 4})
+            for (int threads : {512, 768, 1024}) {
+                const int blocks = std::max(8, cus / ng / 8 * 8) * ng;
+                hipLaunchKernelGGL((k_stream_groups<16>), dim3(blocks), dim3(threads), 0, 0, buf, n_chunks, ng, sink);
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipEventRecord(a, 0));
+                for (int r = 0; r < reps; ++r)
+                    hipLaunchKernelGGL((k_stream_groups<16>), dim3(blocks), dim3(threads), 0, 0, buf, n_chunks, ng, sink);
+                CHECK(hipEventRecord(b, 0));
+                CHECK(hipEventSynchronize(b));
+                float ms = 0.f;
+                CHECK(hipEventElapsedTime(&ms, a, b));
+                const double t = ms / reps;
+                std::printf("{\"variant\": \"query-group shape, default policy\", \"ng\": %d, \"waves_per_cu\": %d, "
+                            "\"blocks\": %d, \"bytes\": %lld, \"ms\": %.4f, \"unique_TBps\": %.4f}\n",
+                            ng, threads / 64, blocks, bytes, t, bytes / (t * 1e-3) / 1e12);
+            }
         CHECK(hipEventDestroy(a));
         CHECK(hipEventDestroy(b));
     }

@@ -74,6 +74,7 @@ int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles,
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
 static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
+static constexpr int kCapWide = 256;    // ... per (workgroup, query) of the wide FILTER (8x a wave's tiles)
 static constexpr int kScanThreads = 512;
 
 // Per-batch search workspace.  Two sets ping-pong between consecutive pipelined batches
@@ -84,6 +85,7 @@ struct Scratch {
         tl, tl_tmp;  // device-mask tile list (+ its count after the list) and its rocPRIM scratch
     int64_t last_W = 0, last_Bp = 0;  // waves (per query group) and queries per group of the most recent FILTER
     int last_ng = 1;                  // query groups of that launch
+    int last_capw = kCapW;            // candidate slots per (region, query) of that launch
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
     hipEvent_t sampled = nullptr;     // pre stream: this set's early query prep + SAMPLE are done

@@ -145,6 +145,59 @@ __global__ __launch_bounds__(1024) void k_stream_groups(const u32x4* __restrict_
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
 }
 
+// Lagged groups: as k_stream_groups, but group g walks its range rotated by g * lag chunks (wrapping),
+// so a trailing group re-reads what the leading one read lag chunks earlier -- from L2 / the Infinity
+// Cache rather than by waiting on the same fill.  ntl: the trailing groups load non-temporal.
+template <int P>
+__global__ __launch_bounds__(512) void k_stream_lag(const u32x4* __restrict__ src, long long n_chunks, int ng,
+                                                    long long lag, int ntl, unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const int bx = blockIdx.x;
+    const int grp = ng > 1 ? (bx >> 3) % ng : 0;
+    const long long nrb = gridDim.x / ng;
+    const long long rb = ng > 1 ? (long long)((bx >> 3) / ng) * 8 + (bx & 7) : bx;
+    const long long W = nrb * (blockDim.x >> 6);
+    const long long w = (long long)(threadIdx.x >> 6) * nrb + rb;
+    const long long base = n_chunks / W, rem = n_chunks % W;
+    const long long c0 = w * base + (w < rem ? w : rem);
+    const long long len = base + (w < rem ? 1 : 0);
+    const long long off = len > 0 ? (grp * lag) % len : 0;
+    const bool nt = ntl && grp > 0;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    u32x4 ring[P];
+    auto at = [&](long long i) -> const u32x4* {
+        long long j = i + off;
+        if (j >= len) j -= len;
+        return src + (c0 + j) * 64 + lane;
+    };
+#pragma unroll
+    for (int i = 0; i < P; ++i) ring[i] = i < len ? (nt ? __builtin_nontemporal_load(at(i)) : *at(i)) : u32x4{0u, 0u, 0u, 0u};
+    long long c = 0;
+    for (; c + 2 * P <= len; c += P) {
+        if (nt) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                acc ^= ring[i];
+                ring[i] = __builtin_nontemporal_load(at(c + P + i));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                acc ^= ring[i];
+                ring[i] = *at(c + P + i);
+            }
+        }
+    }
+    for (; c < len; c += P) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            if (c + i < len) acc ^= ring[i];
+            if (c + P + i < len) ring[i] = *at(c + P + i);
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
+}
+
 template <bool NT, int P>
 static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
     hipEvent_t a, b;
@@ -242,6 +295,33 @@ int main(int argc, char** argv) {
                             "\"blocks\": %d, \"bytes\": %lld, \"ms\": %.4f, \"unique_TBps\": %.4f}\n",
                             ng, threads / 64, blocks, bytes, t, bytes / (t * 1e-3) / 1e12);
             }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+    }
+    if (argc > 2 && atoi(argv[2]) == 4) {  // lagged groups: ng x lag x trailing-group policy
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        const int cus = n_cu - 32;
+        for (int ng : {2, 4})
+            for (long long lag : {0ll, 16ll, 64ll, 128ll, 256ll, 1024ll})
+                for (int ntl : {0, 1}) {
+                    if (lag == 0 && ntl) continue;
+                    const int blocks = std::max(8, cus / ng / 8 * 8) * ng;
+                    hipLaunchKernelGGL((k_stream_lag<16>), dim3(blocks), dim3(512), 0, 0, buf, n_chunks, ng, lag, ntl, sink);
+                    CHECK(hipDeviceSynchronize());
+                    CHECK(hipEventRecord(a, 0));
+                    for (int r = 0; r < reps; ++r)
+                        hipLaunchKernelGGL((k_stream_lag<16>), dim3(blocks), dim3(512), 0, 0, buf, n_chunks, ng, lag, ntl, sink);
+                    CHECK(hipEventRecord(b, 0));
+                    CHECK(hipEventSynchronize(b));
+                    float ms = 0.f;
+                    CHECK(hipEventElapsedTime(&ms, a, b));
+                    const double t = ms / reps;
+                    std::printf("{\"variant\": \"lagged groups\", \"ng\": %d, \"lag_KiB\": %lld, \"trailing_nt\": %d, "
+                                "\"bytes\": %lld, \"ms\": %.4f, \"unique_TBps\": %.4f}\n",
+                                ng, lag, ntl, bytes, t, bytes / (t * 1e-3) / 1e12);
+                }
         CHECK(hipEventDestroy(a));
         CHECK(hipEventDestroy(b));
     }

@@ -198,6 +198,28 @@ __global__ __launch_bounds__(512) void k_stream_lag(const u32x4* __restrict__ sr
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
 }
 
+// Tile-strided assignment: wave w streams tiles (64 chunks) w, w + W, w + 2W, ... instead of one
+// contiguous range, so at any moment the chip's waves read one ~W x 64 KiB window of the buffer in order.
+template <int P>
+__global__ __launch_bounds__(512) void k_stream_strided(const u32x4* __restrict__ src, long long n_tiles, int tile_chunks,
+                                                        unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const long long W = (long long)gridDim.x * (blockDim.x >> 6);
+    const long long w = (long long)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (long long t = w; t < n_tiles; t += W) {
+        const u32x4* base = src + t * tile_chunks * 64 + lane;
+        for (int c = 0; c < tile_chunks; c += P) {
+            u32x4 ring[P];
+#pragma unroll
+            for (int i = 0; i < P; ++i) ring[i] = __builtin_nontemporal_load(base + (c + i) * 64);
+#pragma unroll
+            for (int i = 0; i < P; ++i) acc ^= ring[i];
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
+}
+
 template <bool NT, int P>
 static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
     hipEvent_t a, b;
@@ -322,6 +344,30 @@ int main(int argc, char** argv) {
                                 "\"bytes\": %lld, \"ms\": %.4f, \"unique_TBps\": %.4f}\n",
                                 ng, lag, ntl, bytes, t, bytes / (t * 1e-3) / 1e12);
                 }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+    }
+    if (argc > 2 && atoi(argv[2]) == 5) {  // contiguous ranges vs tile-strided assignment
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        const int cus = n_cu - 32;
+        for (int tc : {16, 64, 256}) {
+            const long long n_tiles = n_chunks / tc;
+            hipLaunchKernelGGL((k_stream_strided<16>), dim3(cus), dim3(512), 0, 0, buf, n_tiles, tc, sink);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(a, 0));
+            for (int r = 0; r < reps; ++r)
+                hipLaunchKernelGGL((k_stream_strided<16>), dim3(cus), dim3(512), 0, 0, buf, n_tiles, tc, sink);
+            CHECK(hipEventRecord(b, 0));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0.f;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            const double t = ms / reps;
+            const long long by = n_tiles * tc * 1024;
+            std::printf("{\"variant\": \"tile-strided, nt, n_cu-32 CUs, 8 waves/CU\", \"tile_KiB\": %d, \"bytes\": %lld, "
+                        "\"ms\": %.4f, \"TBps\": %.4f}\n", tc, by, t, by / (t * 1e-3) / 1e12);
+        }
         CHECK(hipEventDestroy(a));
         CHECK(hipEventDestroy(b));
     }

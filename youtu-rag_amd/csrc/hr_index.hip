@@ -716,6 +716,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.private_bufs = mode == 0 ? 1 : 0;
     static const int wm_env = getenv("HIPRAG_WAVE_MAJOR") ? atoi(getenv("HIPRAG_WAVE_MAJOR")) : 1;
     a.wave_major = wm_env;
+    static const int strided_env = getenv("HIPRAG_STRIDED") ? atoi(getenv("HIPRAG_STRIDED")) : 1;  // A/B: 0 = ranges
+    a.strided = strided_env;
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;

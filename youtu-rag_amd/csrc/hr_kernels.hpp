@@ -256,6 +256,7 @@ struct ScanArgs {
     // pointers: those cost ~150 VGPRs of spills in the fully unrolled epilogue).
     int private_bufs;
     int wave_major;          // unit ranges numbered wave-major across workgroups (spreads the tail)
+    int strided;             // static units dealt round-robin (wave wr: wr, wr + W, ...) instead of in ranges
     float2* pbuf;
     uint32_t* pcnt;
     int capw;
@@ -416,13 +417,18 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * nrb + rb : w;
     const bool dyn = MODE == SCAN_FILTER && a.dyn_start < a.n_units;  // launch-uniform
     const int64_t n_static = dyn ? a.dyn_start : a.n_units;
+    // static units: a contiguous range per wave, or (strided) every W-th unit from wr, so that at any
+    // moment the chip's waves read one window of consecutive tiles; u then counts the wave's own units
     const int64_t base = n_static / W, rem = n_static % W;
-    const int64_t u0 = wr * base + (wr < rem ? wr : rem);
-    const int64_t u1 = u0 + base + (wr < rem ? 1 : 0);
+    const bool strided = a.strided != 0;
+    const int64_t u0 = strided ? 0 : wr * base + (wr < rem ? wr : rem);
+    const int64_t u1 = strided ? (wr < n_static ? (n_static - 1 - wr) / W + 1 : 0) : u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
     const int S = a.S;
+    bool in_static = true;  // u indexes this wave's static units (else a dynamic unit itself)
     // tile of unit u (wave-uniform: a scalar load when a tile list is given)
     auto tile_at = [&](int64_t u) -> int64_t {
+        if (strided && in_static) u = u * W + wr;
         const int64_t i = wave_uniform(u * stride);
         return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };
@@ -571,6 +577,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     uint32_t graw = 0;
     bool issued = false;  // this run's grab is in flight (exactly one grab per run)
     if (dyn && u0 >= u1) {  // no static units (tiny launches): start in the pool
+        in_static = false;
         u = grab_resolve(grab_issue());
         if (u < 0) u = u_end = 0;
         else u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
@@ -582,7 +589,16 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         }
         if (dyn && u + 1 == u_end) pend = grab_resolve(graw);  // this unit's last k-steps prefetch its first unit
         const int64_t t = wave_uniform(tile_at(u));
-        const int64_t tn = wave_uniform((u + 1 < u_end) ? tile_at(u + 1) : (pend >= 0 ? tile_at(pend) : t));
+        int64_t tn = t;
+        if (u + 1 < u_end) {
+            tn = tile_at(u + 1);
+        } else if (pend >= 0) {
+            const bool st = in_static;
+            in_static = false;  // (pend is a dynamic unit)
+            tn = tile_at(pend);
+            in_static = st;
+        }
+        tn = wave_uniform(tn);
         if (t >= part_end) {  // wave-uniform; never taken with one part
             if (MODE != SCAN_COLLECT && a.use_groups) flush();
             const int64_t np_ = t / a.part_tiles;
@@ -730,6 +746,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         if (u + 1 < u_end) {
             ++u;
         } else if (pend >= 0 && done < a.n_units) {  // (done bound: termination even if the counter were corrupt)
+            in_static = false;
             u = pend;
             u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
             pend = -1;

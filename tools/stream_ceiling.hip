@@ -220,6 +220,46 @@ __global__ __launch_bounds__(512) void k_stream_strided(const u32x4* __restrict_
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
 }
 
+// Tile-strided variants: map = 0 wave-major numbering (as the scan), 1 workgroup-major (a workgroup's
+// 8 waves take 8 consecutive tiles); pre = 1 keeps the next burst in flight while one is consumed.
+template <int P>
+__global__ __launch_bounds__(512) void k_stream_strided2(const u32x4* __restrict__ src, long long n_tiles, int tile_chunks,
+                                                         int map, int pre, unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const long long W = (long long)gridDim.x * (blockDim.x >> 6);
+    const long long w = map ? (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)
+                            : (long long)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    if (!pre) {
+        for (long long t = w; t < n_tiles; t += W) {
+            const u32x4* base = src + t * tile_chunks * 64 + lane;
+            for (int c = 0; c < tile_chunks; c += P) {
+                u32x4 ring[P];
+#pragma unroll
+                for (int i = 0; i < P; ++i) ring[i] = __builtin_nontemporal_load(base + (c + i) * 64);
+#pragma unroll
+                for (int i = 0; i < P; ++i) acc ^= ring[i];
+            }
+        }
+    } else {
+        // chunk sequence of this wave: tiles w, w+W, ..., each tile_chunks long; ring of P prefetched
+        const long long nt = w < n_tiles ? (n_tiles - 1 - w) / W + 1 : 0;
+        const long long total = nt * tile_chunks;
+        auto addr = [&](long long k) { return src + ((w + (k / tile_chunks) * W) * tile_chunks + k % tile_chunks) * 64 + lane; };
+        u32x4 ring[P];
+#pragma unroll
+        for (int i = 0; i < P; ++i) ring[i] = i < total ? __builtin_nontemporal_load(addr(i)) : u32x4{0u, 0u, 0u, 0u};
+        for (long long k = 0; k < total; k += P) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                acc ^= ring[i];
+                if (k + P + i < total) ring[i] = __builtin_nontemporal_load(addr(k + P + i));
+            }
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1u;
+}
+
 template <bool NT, int P>
 static double run(const u32x4* buf, long long n_chunks, unsigned* sink, int blocks, int threads, int reps) {
     hipEvent_t a, b;
@@ -367,6 +407,31 @@ int main(int argc, char** argv) {
             const long long by = n_tiles * tc * 1024;
             std::printf("{\"variant\": \"tile-strided, nt, n_cu-32 CUs, 8 waves/CU\", \"tile_KiB\": %d, \"bytes\": %lld, "
                         "\"ms\": %.4f, \"TBps\": %.4f}\n", tc, by, t, by / (t * 1e-3) / 1e12);
+        }
+        CHECK(hipEventDestroy(a));
+        CHECK(hipEventDestroy(b));
+    }
+    if (argc > 2 && atoi(argv[2]) == 6) {  // tile-strided variants
+        hipEvent_t a, b;
+        CHECK(hipEventCreate(&a));
+        CHECK(hipEventCreate(&b));
+        struct SV { int cus, map, pre; };
+        for (SV v : std::vector<SV>{{n_cu - 32, 0, 0}, {n_cu - 32, 1, 0}, {n_cu - 32, 0, 1}, {n_cu, 0, 0}, {n_cu - 32, 0, 0}}) {
+            const int tc = 64;
+            const long long n_tiles = n_chunks / tc;
+            hipLaunchKernelGGL((k_stream_strided2<16>), dim3(v.cus), dim3(512), 0, 0, buf, n_tiles, tc, v.map, v.pre, sink);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(a, 0));
+            for (int r = 0; r < reps; ++r)
+                hipLaunchKernelGGL((k_stream_strided2<16>), dim3(v.cus), dim3(512), 0, 0, buf, n_tiles, tc, v.map, v.pre, sink);
+            CHECK(hipEventRecord(b, 0));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0.f;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            const double t = ms / reps;
+            const long long by = n_tiles * tc * 1024;
+            std::printf("{\"variant\": \"tile-strided\", \"cus\": %d, \"wg_major\": %d, \"prefetch\": %d, \"bytes\": %lld, "
+                        "\"ms\": %.4f, \"TBps\": %.4f}\n", v.cus, v.map, v.pre, by, t, by / (t * 1e-3) / 1e12);
         }
         CHECK(hipEventDestroy(a));
         CHECK(hipEventDestroy(b));

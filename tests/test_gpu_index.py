@@ -235,6 +235,56 @@ def test_early_sample_pipelined_vs_oracle(native, metric):
     _check(s_d.cpu().numpy(), r_d.cpu().numpy(), s_ref, r_ref)
 
 
+@pytest.mark.parametrize("metric", ["cosine", "l2"])
+def test_early_sample_clusters_dups_tombstones_vs_oracle(native, metric):
+    """The early-SAMPLE pipelined path on a shard with tight clusters spread over it (20k rows
+    around each of three rows, so the sampled tiles and the FILTER's row groups are full of near
+    ties), 200 exact duplicates and 5000 tombstones, with planted / cluster / duplicate / isotropic
+    query batches over both workspaces, twice: every batch identical to the oracle, the queries the
+    guard cannot settle answered by the exact fallback."""
+    torch = pytest.importorskip("torch")
+    from hiprag.dist import ShardedSearch
+
+    dim, n, B, k = 64, 1_100_000, 64, 10
+    rng = np.random.default_rng(31)
+    raw = R.gen_rows(29, 0, n, dim)
+    centers = []
+    for j in rng.choice(n, 3, replace=False):  # clusters of 20k rows around three rows
+        c = raw[j] / np.linalg.norm(raw[j])
+        pos = rng.choice(n, 20_000, replace=False)
+        noise = rng.standard_normal((len(pos), dim)).astype(np.float32)
+        raw[pos] = c + 0.02 * noise / np.linalg.norm(noise, axis=1, keepdims=True)
+        centers.append(c)
+    dup = rng.choice(n, 200, replace=False)
+    raw[dup] = raw[dup[0]]
+    idx = native.NativeIndex(dim, "bf16", metric)
+    idx.add(raw)
+    gone = rng.choice(n, 5000, replace=False)
+    idx.remove(gone)
+    live = np.ones(n, bool)
+    live[gone] = False
+    stored = R.process_rows(raw, metric, "bf16")
+    cl = np.stack([centers[i % 3] + 0.01 * rng.standard_normal(dim).astype(np.float32) for i in range(B)])
+    qs = [np.concatenate([_planted_queries(raw, B // 2, rng), rng.standard_normal((B - B // 2, dim)).astype(np.float32)]),
+          cl.astype(np.float32), np.concatenate([raw[dup[:8]], rng.standard_normal((B - 8, dim)).astype(np.float32)]),
+          rng.standard_normal((B, dim)).astype(np.float32)]
+    q_dev = [torch.from_numpy(np.ascontiguousarray(q)).cuda() for q in qs]
+    outs = [(torch.empty((B, k), dtype=torch.float32, device="cuda"), torch.empty((B, k), dtype=torch.int64, device="cuda"))
+            for _ in qs]
+    ready = torch.cuda.Event()
+    ready.record()
+    ss = ShardedSearch(idx, 0, max_batch=B, device=torch.device("cuda", 0))
+    for rep in range(2):  # both workspaces, twice
+        for q, (s_o, r_o) in zip(q_dev, outs):
+            ss.submit(q, k, s_out=s_o, r_out=r_o, q_ready=ready)
+        ss.finalize_all()
+        torch.cuda.synchronize()
+        for q, (s_o, r_o) in zip(qs, outs):
+            s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, metric), k, oracle.mask_from_bool(live),
+                                           metric=metric)
+            _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
+
+
 @pytest.mark.parametrize("dtype,metric,k", [("bf16", "cosine", 10), ("bf16", "cosine", 100), ("f32", "cosine", 32),
                                             ("f16", "cosine", 45), ("bf16", "ip", 45), ("bf16", "l2", 10)])
 def test_selective_filter_tile_list_vs_oracle(native, dtype, metric, k):

@@ -689,7 +689,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     }
     // HIPRAG_SCAN_DEBUG (timing experiments only; results are wrong with bits 1/4 set):
     // 1 = no candidate appends, 2 = no threshold refresh, 4 = no sample pass, 8 = refresh never publishes,
-    // 16 = publish with relaxed stores instead of atomicMax, 32 = the SAMPLE pass publishes nothing
+    // 16 = publish with relaxed stores instead of atomicMax, 32 = the SAMPLE pass publishes nothing,
+    // 64 = FILTER appends compute their slots but store nothing
     if (!fl) {
         if (dbg & 1)
             for (auto& f : h->floor_host) f = INFINITY;
@@ -719,6 +720,13 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     static const int strided_env = getenv("HIPRAG_STRIDED") ? atoi(getenv("HIPRAG_STRIDED")) : 1;  // A/B: 0 = ranges
     a.strided = strided_env;
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
+    // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
+    // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->
+    // 3.05-3.07 ms (two alternating repeats on one box, tools/ab_env.sh), so big shards keep the
+    // epilogue loads.  HIPRAG_EARLY_REFRESH=0/1 forces either (A/B)
+    static const int early_refresh_env = getenv("HIPRAG_EARLY_REFRESH") ? atoi(getenv("HIPRAG_EARLY_REFRESH")) : -1;
+    a.diag_nostore = (dbg & 64) ? 1 : 0;
+    a.early_refresh = early_refresh_env >= 0 ? early_refresh_env : (dual ? 1 : 0);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;

@@ -274,6 +274,8 @@ struct ScanArgs {
     // query groups (more than QB*32 queries per corpus pass): ng workgroups stream the same tile range,
     // each with its own QB*32 queries in LDS; per-query tables hold ng consecutive groups
     int ng;
+    int diag_nostore;        // timing diagnostics only (HIPRAG_SCAN_DEBUG & 64): appends skip their stores (wrong results)
+    int early_refresh;       // FILTER: a refresh's loads go out before the tile's k-loop (0: in its epilogue; A/B)
     int wide_dbg;            // k_scan_wide timing experiments: 1 = no MFMAs, 2 = no LDS reads either (wrong results)
 };
 
@@ -425,6 +427,10 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     const int64_t u1 = strided ? (wr < n_static ? (n_static - 1 - wr) / W + 1 : 0) : u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
     const int S = a.S;
+    // the plan picks P dividing S (make_plan): every k-loop runs at least once, so its ring waits retire
+    // whatever was issued before it (the early refresh loads) -- without this the compiler keeps the
+    // zero-trip path and waits for the ring again where those loads are used
+    __builtin_assume(S >= P);
     bool in_static = true;  // u indexes this wave's static units (else a dynamic unit itself)
     // tile of unit u (wave-uniform: a scalar load when a tile list is given)
     auto tile_at = [&](int64_t u) -> int64_t {
@@ -487,24 +493,20 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     // measured 0.6 ms of a 1.0 ms scan at 1.25M rows), then this wave's group max is published
     // only where it beats the global value (a blind atomicMax from every wave piles ~#waves
     // atomics onto each of the 32*B addresses).
-    auto refresh = [&](bool publish) {
-        if (!a.use_groups) {
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    gmax[qb][i] = -__builtin_inff();
-                    th[qb][i] = fmaxf(th[qb][i], a.floor_q[acc_query(qb, i, half)]);
-                }
-            return;
-        }
-        uint32_t key[QB][16];
+    // The loads (refresh_load) and their use (refresh_apply) are split so that the main loop issues a
+    // refresh's loads BEFORE a tile's k-loop and applies them in its epilogue: the k-loop's own ring
+    // waits retire them, whereas loads issued in the epilogue and used at once made the wave wait for
+    // everything issued before them -- the next tile's ring refills included (a drain per refresh).
+    auto refresh_load = [&](uint32_t (&key)[QB][16]) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 key[qb][i] = __hip_atomic_load(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // floor: also take the per-query floor (the first refresh; th never drops below it afterwards)
+    auto refresh_apply = [&](uint32_t (&key)[QB][16], bool publish, bool floor) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
@@ -537,13 +539,28 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int q = acc_query(qb, i, half);
                 float f = key2f(key[qb][i]);
 #pragma unroll
                 for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
                 gmax[qb][i] = -__builtin_inff();
-                th[qb][i] = fmaxf(th[qb][i], fmaxf(f, a.floor_q[q]));
+                if (floor) f = fmaxf(f, a.floor_q[acc_query(qb, i, half)]);
+                th[qb][i] = fmaxf(th[qb][i], f);
             }
+    };
+    auto refresh = [&](bool publish) {
+        if (!a.use_groups) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    gmax[qb][i] = -__builtin_inff();
+                    th[qb][i] = fmaxf(th[qb][i], a.floor_q[acc_query(qb, i, half)]);
+                }
+            return;
+        }
+        uint32_t key[QB][16];
+        refresh_load(key);
+        refresh_apply(key, publish, true);
     };
     // publish the group maxima of the part being left (or at the end of a SAMPLE range)
     auto flush = [&]() {
@@ -573,6 +590,8 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         const int64_t u = a.dyn_start + (int64_t)v * a.dyn_chunk;
         return u < a.n_units ? u : -1;
     };
+    uint32_t rkey[QB][16];  // group-max keys of the refresh due in the current tile's epilogue
+    const bool early_refresh = a.early_refresh != 0;
     int64_t u = u0, u_end = u1, pend = -1, done = 0;
     uint32_t graw = 0;
     bool issued = false;  // this run's grab is in flight (exactly one grab per run)
@@ -606,6 +625,12 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
             for (int qb = 0; qb < QB; ++qb) gkq[qb] += (np_ - part) * a.pstride;
             part = np_;
             part_end = (part + 1) * a.part_tiles;
+        }
+        // a refresh applied in this tile's epilogue: its loads go out now (see refresh_load)
+        const bool rdue = MODE == SCAN_FILTER && a.use_groups && early_refresh && ((done + 1) % a.refresh_every) == 0;
+        if (rdue) {
+            refresh_load(rkey);
+            asm volatile("" ::: "memory");  // keeps the loads here (the compiler would sink them to their use)
         }
         f32x16 acc[QB];
 #pragma unroll
@@ -695,20 +720,25 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         }
         const bool ok = (allow >> rg) & 1u;
         const uint32_t row = (uint32_t)(t * 32 + rg);
-        uint64_t any = 0;
+        // regs: the accumulator registers (bit qb*16+i, wave-uniform) holding a passing score; the
+        // append pass below visits only those (a scalar bit test per register instead of a compare +
+        // ballot for all 16*QB of them: early in a scan, while the threshold is still loose, most
+        // tiles append something)
+        uint32_t regs = 0;
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float v = ok ? acc[qb][i] : -__builtin_inff();
                 gmax[qb][i] = fmaxf(gmax[qb][i], v);
-                if (FILTER) any |= __ballot(ok && v >= th[qb][i]);
+                if (FILTER) regs |= (__ballot(ok && v >= th[qb][i]) != 0 ? 1u : 0u) << (qb * 16 + i);
             }
-        if (FILTER && any) {
+        if (FILTER && regs) {
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
+                    if (!((regs >> (qb * 16 + i)) & 1u)) continue;
                     const float v = acc[qb][i];
                     const bool pass = ok && v >= th[qb][i];
                     const uint64_t m = __ballot(pass);
@@ -721,7 +751,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
                                 const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)mycnt, q);
                                 if (pass && half == h) {
                                     const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                                    if (pos < (uint32_t)a.capw)
+                                    if (pos < (uint32_t)a.capw && !a.diag_nostore)
                                         wave_buf[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
                                 }
                                 mycnt += (lane == q) ? (uint32_t)__builtin_popcount(mh) : 0u;
@@ -742,7 +772,10 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
                 }
         }
         ++done;
-        if (MODE == SCAN_FILTER && (done % a.refresh_every) == 0) refresh(true);
+        if (MODE == SCAN_FILTER && (done % a.refresh_every) == 0) {
+            if (rdue) refresh_apply(rkey, true, false);
+            else refresh(true);
+        }
         if (u + 1 < u_end) {
             ++u;
         } else if (pend >= 0 && done < a.n_units) {  // (done bound: termination even if the counter were corrupt)

@@ -58,16 +58,24 @@ def main():
                 _native.gen_rows_device(11, i0, i1 - i0, D, x.data_ptr(), st())
                 return x
         t0 = time.time()
+        say = lambda m: print(f"[{dist}] {m} ({time.time() - t0:.1f}s)", file=sys.stderr, flush=True)  # noqa: E731
         ivf = IvfIndex(D, args.nlist, dtype=args.dtype, metric="cosine")
         ivf.train(rows(0, min(N, args.nlist * 32)), iters=10, seed=0)
+        torch.cuda.synchronize()
+        say("coarse quantizer trained")
         ivf.build(N, rows)
+        torch.cuda.synchronize()
+        say(f"IVF lists built ({N} rows)")
+        build_s = time.time() - t0
         flat = _native.NativeIndex(D, args.dtype, "cosine")
         flat.reserve(N)
         for i in range(0, N, 1 << 18):
             x = rows(i, min(N, i + (1 << 18))).contiguous()
             flat.add_device(x.data_ptr(), x.shape[0], st())
+            if (i >> 18) % 64 == 63:
+                say(f"exact index {i + x.shape[0]} rows")
         torch.cuda.synchronize()
-        build_s = time.time() - t0
+        say("exact index built")
         g = torch.Generator(device=dev)
         g.manual_seed(5)
         nb = args.steps + 2
@@ -88,6 +96,7 @@ def main():
             ivf.search_candidates(qs[i], K, args.nprobe, cand, bound)
         torch.cuda.synchronize()
         ivf_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        print(f"[{dist}] IVF {ivf_ms:.3f} ms/batch", file=sys.stderr, flush=True)
         probes = torch.empty((B, args.nprobe, 2), dtype=torch.float64, device=dev)
         ivf.search_candidates(qs[2], K, args.nprobe, cand, bound, probes=probes)
         pl = probes.view(torch.int64)[..., 1]

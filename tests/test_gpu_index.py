@@ -285,6 +285,31 @@ def test_early_sample_clusters_dups_tombstones_vs_oracle(native, metric):
             _check(s_o.cpu().numpy(), r_o.cpu().numpy(), s_ref, r_ref)
 
 
+def test_periodic_clusters_spread_over_waves(native):
+    """Rows whose cluster repeats with a period of 4096 rows (128 tiles, a factor of the scan's wave
+    count): the FILTER's round-robin dealing rotates each round's positions, so a cluster's rows (a
+    query's candidates) reach every wave instead of the few waves whose tiles share its residue -- their
+    32-slot private regions stayed below capacity and the guard held for k = 10 (and the row parts of
+    k = 100 keep contiguous ranges).  Results identical to the oracle either way."""
+    dim, n, B, C = 64, 6_250_000, 64, 4096
+    rng = np.random.default_rng(17)
+    centers = rng.standard_normal((C, dim)).astype(np.float32)
+    centers /= np.linalg.norm(centers, axis=1, keepdims=True)
+    noise = R.gen_rows(41, 0, n, dim)
+    noise /= np.linalg.norm(noise, axis=1, keepdims=True)
+    raw = centers[(np.arange(n, dtype=np.int64) * 2654435761) % C] + 0.7 * noise
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    stored = R.process_rows(raw, "cosine", "bf16")
+    q = (raw[rng.choice(n, B, replace=False)] + 0.1 * rng.standard_normal((B, dim))).astype(np.float32)
+    for k in (10, 100):
+        before = idx.stats()["guard_failures"]
+        s, r = idx.search(q, k)
+        _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k))
+        failed = idx.stats()["guard_failures"] - before
+        assert failed <= B // 8, (k, failed)
+
+
 @pytest.mark.parametrize("dtype,metric,k", [("bf16", "cosine", 10), ("bf16", "cosine", 100), ("f32", "cosine", 32),
                                             ("f16", "cosine", 45), ("bf16", "ip", 45), ("bf16", "l2", 10)])
 def test_selective_filter_tile_list_vs_oracle(native, dtype, metric, k):

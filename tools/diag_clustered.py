@@ -36,6 +36,8 @@ g = torch.Generator(device=dev)
 g.manual_seed(5)
 j = torch.randint(0, N, (B,), generator=g, device=dev)
 q = (torch.cat([rows(int(r), int(r) + 1) for r in j.tolist()]) + 0.1 * torch.randn((B, D), generator=g, device=dev)).contiguous()
+if os.environ.get("DIAG_QUERIES") == "mixed":  # bench_ivf's batches: half planted, half isotropic
+    q = torch.cat([q[: B // 2], torch.randn((B - B // 2, D), generator=g, device=dev)]).contiguous()
 for k in (10, 100):
     kc = _native.kc_for_k(k)
     cand = torch.empty((B, kc, 2), dtype=torch.float64, device=dev)
@@ -62,3 +64,4 @@ for k in (10, 100):
     print(f"k={k} kc={kc}: main pass {t_main * 1e3:.2f} ms, full search {t_full * 1e3:.2f} ms, guard failures {nf}/{B}, "
           f"kth-bound gap median {np.median(gap):.2e} min {gap.min():.2e}, candidates/query {tot / B:.0f} max {mx}",
           flush=True)
+    print(f"  index stats after k={k}: {flat.stats()}", flush=True)

@@ -718,7 +718,12 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     static const int wm_env = getenv("HIPRAG_WAVE_MAJOR") ? atoi(getenv("HIPRAG_WAVE_MAJOR")) : 1;
     a.wave_major = wm_env;
     static const int strided_env = getenv("HIPRAG_STRIDED") ? atoi(getenv("HIPRAG_STRIDED")) : 1;  // A/B: 0 = ranges
-    a.strided = strided_env;
+    // round-robin units make the chip sweep the tiles in order, so with row parts (k > 32) the last part
+    // would keep its SAMPLE-level group maxima until the sweep reaches it, and the threshold (min over all
+    // parts) with them: 50M rows at k = 100 then appended 78k candidates per query, overflowed every
+    // private region and sent every query to the collect pass (33.8 ms/batch).  Parts keep contiguous
+    // per-wave ranges, which visit every part from the start.
+    a.strided = strided_env && np == 1;
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
     // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->

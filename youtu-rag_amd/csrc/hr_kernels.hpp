@@ -311,6 +311,11 @@ struct XFrag;
 #ifndef HR_RING_SCHED
 #define HR_RING_SCHED 0
 #endif
+// HR_ROTATE_ROUNDS=0 builds the unrotated round-robin dealing (A/B and the regression check of
+// test_periodic_clusters_spread_over_waves only)
+#ifndef HR_ROTATE_ROUNDS
+#define HR_ROTATE_ROUNDS 1
+#endif
 // a wave-uniform 64-bit value in scalar registers (the compiler cannot prove threadIdx.x >> 6 uniform)
 __device__ inline int64_t wave_uniform(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -432,9 +437,23 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     // zero-trip path and waits for the ring again where those loads are used
     __builtin_assume(S >= P);
     bool in_static = true;  // u indexes this wave's static units (else a dynamic unit itself)
-    // tile of unit u (wave-uniform: a scalar load when a tile list is given)
+    // Round-robin dealing: round j covers units [jW, (j+1)W) and wave wr takes one of them.  The position
+    // is rotated by a hash of j (full rounds only; the last, partial round keeps wr): with a fixed
+    // position, wave wr would see only tiles = wr (mod W), so any period in the rows that shares factors
+    // with W -- every 4096th row in one cluster, a document's k-th chunks -- lands in the same few waves
+    // (clustered 6.25M rows: 14 waves held a cluster's candidates, their 32-slot regions overflowed and
+    // 45 of 64 queries took the collect pass)
+    const int64_t full_rounds = n_static / W;
     auto tile_at = [&](int64_t u) -> int64_t {
-        if (strided && in_static) u = u * W + wr;
+        if (strided && in_static) {
+            int64_t pos = wr;
+            if (HR_ROTATE_ROUNDS && u < full_rounds) {
+                const uint32_t rot = (uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W;
+                pos += rot;
+                if (pos >= W) pos -= W;
+            }
+            u = u * W + pos;
+        }
         const int64_t i = wave_uniform(u * stride);
         return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };

@@ -63,7 +63,7 @@ enum {
 };
 
 #define HR_MAX_K 128           /* largest top-k (kb_file_search recall 15 x 3, rerank top-100) */
-#define HR_MAX_KC 160          /* largest per-shard candidate count kc */
+#define HR_MAX_KC 192          /* largest per-shard candidate count kc (k = HR_MAX_K with its k/2 margin) */
 
 int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);
 int hr_index_reserve(hr_index* h, int64_t capacity_rows);
@@ -102,8 +102,8 @@ void hr_index_destroy(hr_index* h);
  * Candidate record = {double exact_score; int64 global_row} (16 bytes).
  * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_KC); the scan keeps
  * ceil(kc/32) row parts of group maxima.  hr_kc_for_k gives the kc the single-GPU search
- * uses: 32 for k <= 32, else k + max(16, k/2) rounded up to a multiple of 32, at most
- * HR_MAX_KC (margin for the guard). */
+ * uses: k + max(16, k/2) rounded up to a multiple of 32, at most HR_MAX_KC (margin for the
+ * guard; 32 for k <= 16). */
 int hr_kc_for_k(int k);
 int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                           int64_t row_offset, void* cand_out_dev /* B*kc records */,

@@ -43,6 +43,7 @@ def test_library_loads_and_reports_errors():
     assert [L.hr_kc_for_k(k) for k in range(1, _native.HR_MAX_K + 1)] == \
         [_native.kc_for_k(k) for k in range(1, _native.HR_MAX_K + 1)]
     assert _native.kc_for_k(_native.HR_MAX_K) <= _native.HR_MAX_KC and _native.kc_for_k(45) == 96 and _native.kc_for_k(100) == 160
+    assert _native.kc_for_k(10) == 32 and _native.kc_for_k(32) == 64 and _native.kc_for_k(128) == 192
     with pytest.raises(ValueError):  # argument validation happens before any device call
         _native.NativeIndex(0, "bf16", "cosine")
     with pytest.raises(ValueError):

@@ -1679,9 +1679,11 @@ extern "C" const char* hr_last_error(void) { return g_err.c_str(); }
 extern "C" int hr_abi_version(void) { return 2; }
 
 extern "C" int hr_kc_for_k(int k) {
-    // margin beyond k: max(16, k/2).  Dense clusters put many rows within the guard's E of the
-    // k-th score; at k = 100 a 16-row margin sent half the queries of a clustered corpus to the
-    // collect fallback (5.3 ms/batch at 6.25M rows), k/2 sends almost none (2.8 ms)
+    // margin beyond k: max(16, k/2), for every k.  Dense clusters put many rows within the guard's E of
+    // the k-th score; at k = 100 a 16-row margin sent half the queries of a clustered corpus to the
+    // collect fallback (5.3 ms/batch at 6.25M rows), k/2 sends almost none (2.8 ms).  kc = 32 for every
+    // k <= 32 left no margin at k = 32 (every query of a 10M batch failed the guard: 7.2 vs 3.3 ms) and
+    // HR_MAX_KC = 160 only 32 rows at k = 128 (83 % failures, 8.2 ms; tools/diag_k.py)
     const int margin = std::max(16, k / 2);
-    return k <= 32 ? 32 : std::min(HR_MAX_KC, (k + margin + 31) / 32 * 32);
+    return std::min(HR_MAX_KC, (k + margin + 31) / 32 * 32);
 }

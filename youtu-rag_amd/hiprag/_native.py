@@ -19,13 +19,13 @@ LIB_PATH = os.path.join(_HERE, "libhiprag.so")
 DTYPES = {"f32": 0, "float32": 0, "fp32": 0, "bf16": 1, "bfloat16": 1, "f16": 2, "float16": 2, "fp16": 2}
 METRICS = {"cosine": 0, "ip": 1, "dot": 1, "euclidean": 2, "l2": 2}
 HR_MAX_K = 128   # include/hiprag.h
-HR_MAX_KC = 160
+HR_MAX_KC = 192
 
 
 def kc_for_k(k: int) -> int:
-    """Per-shard candidate count for top-k (hr_kc_for_k): 32 for k <= 32, else k + max(16, k // 2)
-    rounded up to 32, at most HR_MAX_KC (tests/test_native_abi.py checks it against the library)."""
-    return 32 if k <= 32 else min(HR_MAX_KC, (k + max(16, k // 2) + 31) // 32 * 32)
+    """Per-shard candidate count for top-k (hr_kc_for_k): k + max(16, k // 2) rounded up to 32 (32 for
+    k <= 16), at most HR_MAX_KC (tests/test_native_abi.py checks it against the library)."""
+    return min(HR_MAX_KC, (k + max(16, k // 2) + 31) // 32 * 32)
 
 
 CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand

@@ -92,7 +92,7 @@ class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
     def __init__(self, index, row_offset: int, max_batch: int, kc: int | None = None, group=None,
-                 device=None, depth: int = 2, max_k: int = 32, overlap: bool = True):
+                 device=None, depth: int = 2, max_k: int = 16, overlap: bool = True):
         import torch
         import torch.distributed as dist
 
@@ -101,7 +101,9 @@ class ShardedSearch:
         self.row_offset = int(row_offset)
         self.group = group
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k)  # candidates per shard per query
+        # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
+        # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
+        self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k)
         self.max_batch = int(max_batch)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         pinned = self.device.type == "cuda"

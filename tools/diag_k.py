@@ -1,6 +1,6 @@
 """Diagnostics: exact search time and guard failures across top-k on the bench corpus (synthetic,
 counter-based), planted and isotropic query batches, synchronous path.
-Usage: python tools/diag_k.py [rows] [dim]"""
+Usage: python tools/diag_k.py [rows] [dim] [dtype] [metric]"""
 import os
 import sys
 import time
@@ -14,10 +14,12 @@ from hiprag import _native, synth  # noqa: E402
 
 N = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10_000_000
 D = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+DT = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+MET = sys.argv[4] if len(sys.argv) > 4 else "cosine"
 B = 64
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream(dev).cuda_stream
-idx = _native.NativeIndex(D, "bf16", "cosine")
+idx = _native.NativeIndex(D, DT, MET)
 idx.reserve(N)
 idx.add_synthetic(0, 0, N)
 torch.cuda.synchronize()
@@ -37,7 +39,7 @@ for name, q in (("planted", planted), ("isotropic", iso)):
         ms = (time.perf_counter() - t0) * 1e3 / 3
         after = idx.stats()
         tot, mx = idx.last_candidates()
-        print(f"{name:9s} k={k:3d} kc={_native.kc_for_k(k):3d}: {ms:7.2f} ms/batch, guard failures "
+        print(f"{DT} {MET} {name:9s} k={k:3d} kc={_native.kc_for_k(k):3d}: {ms:7.2f} ms/batch, guard failures "
               f"{(after['guard_failures'] - before['guard_failures']) / 3:.1f}/{B}, exhaustive "
               f"{(after['exhaustive'] - before['exhaustive']) / 3:.1f}, candidates/query {tot / B:.0f} max {mx}",
               flush=True)

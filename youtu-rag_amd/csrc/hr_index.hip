@@ -504,10 +504,18 @@ static int launch_scan(hr_index* h, Scratch& sc, int cus, const Plan& pl, const 
                        hipStream_t st) {
     return dispatch_dt(h->dtype, [&](auto dt) -> int {
         constexpr int DT = decltype(dt)::value;
-        constexpr int MT = DT == F16 ? F16 : BF16;
-        if (mode == SCAN_SAMPLE) return launch_scan_p<MT, DT, SCAN_SAMPLE>(h, sc, cus, pl, a, st);
-        if (mode == SCAN_FILTER) return launch_scan_p<MT, DT, SCAN_FILTER>(h, sc, cus, pl, a, st);
-        return launch_scan_p<MT, DT, SCAN_COLLECT>(h, sc, cus, pl, a, st);
+        auto go = [&](auto mt) -> int {
+            constexpr int MT = decltype(mt)::value;
+            if (mode == SCAN_SAMPLE) return launch_scan_p<MT, DT, SCAN_SAMPLE>(h, sc, cus, pl, a, st);
+            if (mode == SCAN_FILTER) return launch_scan_p<MT, DT, SCAN_FILTER>(h, sc, cus, pl, a, st);
+            return launch_scan_p<MT, DT, SCAN_COLLECT>(h, sc, cus, pl, a, st);
+        };
+        if constexpr (DT == F32) {  // fp32 rows: the MFMA type follows the metric (mfma_type)
+            if (mfma_type(h) == F16) return go(std::integral_constant<int, F16>{});
+            return go(std::integral_constant<int, BF16>{});
+        } else {
+            return go(std::integral_constant<int, DT == F16 ? F16 : BF16>{});
+        }
     });
 }
 
@@ -524,7 +532,12 @@ static int tail_cus(const hr_index* h) {
 static double acc_gamma(const hr_index* h) { return (double)(h->dpad + 64) * std::ldexp(1.0, -23); }
 static double storage_u(const hr_index* h) {
     if (h->dtype != F32) return 0.0;
-    return mfma_type(h->dtype) == BF16 ? std::ldexp(1.0, -8) : std::ldexp(1.0, -11);
+    if (mfma_type(h) == BF16) return std::ldexp(1.0, -8);
+    // f16: relative 2^-11 for normal values; an element below 2^-14 rounds to a subnormal with an absolute
+    // error up to 2^-25, which sum_i |q_i| 2^-25 <= sqrt(dpad) |q| 2^-25 bounds -- folded in relative to
+    // the largest row norm, as guard_e scales u_x by it
+    const double mn = std::sqrt(h->max_norm2);
+    return std::ldexp(1.0, -11) + (mn > 0.0 ? std::sqrt((double)h->dpad) * std::ldexp(1.0, -25) / mn : 0.0);
 }
 
 // One chunk of <= Bp queries on this shard.  mode 0: top-kc via SAMPLE+FILTER(groups);
@@ -650,7 +663,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(sc.overflow.ensure((size_t)Bp * 4));
     HIP_TRY(sc.dyn_q.ensure((size_t)std::max(4, pl.NG) * 64));
 
-    const int MT = mfma_type(h->dtype);
+    const int MT = mfma_type(h);
     float* fl = (mode == 0 && !(dbg & 1)) ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, sp, q_dev, B, Bp, h->dim, h->dpad,
@@ -1123,7 +1136,7 @@ int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)h->S * QB * 1024));
     HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
-    if (mfma_type(h->dtype) == BF16)
+    if (mfma_type(h) == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, q_dev, B, Bp, h->dim, h->dpad, h->S,
                            QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(), nullptr, 1,
                            nullptr, nullptr, nullptr);
@@ -1363,7 +1376,7 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
     HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
     HIP_TRY(h->stage.ensure((size_t)Bp * n_tiles * 32 * 4 + 16));
     HIP_TRY(hipMemcpyAsync(h->q_in.p, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice, st));
-    const int MT = mfma_type(h->dtype);
+    const int MT = mfma_type(h);
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, h->q_in.as<float>(), B, Bp, h->dim,
                            h->dpad, h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
@@ -1380,6 +1393,9 @@ extern "C" int hr_index_debug_approx(hr_index* h, const float* q, int B, float* 
         auto k1 = k_debug_approx<MTc, DT, 1>;
         auto k2 = k_debug_approx<MTc, DT, 2>;
         auto kern = pl.QB == 1 ? k1 : k2;
+        if constexpr (DT == F32) {  // the scan's MFMA type for fp32 rows (mfma_type)
+            if (mfma_type(h) == F16) kern = pl.QB == 1 ? k_debug_approx<F16, DT, 1> : k_debug_approx<F16, DT, 2>;
+        }
         HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         hipLaunchKernelGGL(kern, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), lds, st, h->rows,
                            sc.qfrag.as<uint16_t>(), h->S, n_tiles, h->metric == L2 ? h->xnorm : nullptr,

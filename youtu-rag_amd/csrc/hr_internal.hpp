@@ -246,6 +246,11 @@ inline int dispatch_dt(int dt, F&& f) {
     return set_err(HR_E_INVALID, "unknown dtype");
 }
 
-// MFMA operand type: f16 corpora use the f16 MFMA, bf16 and fp32 corpora the bf16 one
-inline int mfma_type(int dtype) { return dtype == F16 ? F16 : BF16; }
+// MFMA operand type: f16 corpora use the f16 MFMA and bf16 corpora the bf16 one.  fp32 corpora are
+// rounded to one of them on the fly: f16 (unit roundoff 2^-11, 8x finer than bf16, so the guard's window
+// and the collect fallbacks shrink with it) when the rows are normalised (cosine: every element in
+// [-1, 1], far inside f16's range), bf16 (fp32's range) for raw inner-product / euclidean rows
+inline int mfma_type(const hr_index* h) {
+    return (h->dtype == F16 || (h->dtype == F32 && h->metric == COSINE)) ? F16 : BF16;
+}
 

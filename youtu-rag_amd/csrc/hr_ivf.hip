@@ -518,7 +518,7 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         HIP_TRY(h->ivf_uoff.ensure((size_t)(bc + 1) * 8));
         HIP_TRY(h->ivf_out.ensure((size_t)cap * 32 * sizeof(Cand)));
         const float* qb = q_dev + (int64_t)b0 * h->dim;
-        if (mfma_type(h->dtype) == BF16)
+        if (mfma_type(h) == BF16)
             hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, st, qb, bc, Bp, h->dim, dpad, h->S,
                                QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
                                nullptr, 1, nullptr, nullptr, nullptr);

@@ -351,6 +351,10 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     static const int mg_env = getenv("HIPRAG_MAX_GROUPS") ? atoi(getenv("HIPRAG_MAX_GROUPS")) : 4;
     const int max_groups = std::max(1, std::min(8, mg_env));
     p->NG = (QB == 2 && h->dtype != F32) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
+    // D > 1280 (Youtu-Embedding's 2048 / 2304 dims) leaves LDS for one 32-query block only: a 64-query
+    // batch was two corpus passes; 32-query groups share one (HIPRAG_QB1_GROUPS=0: separate passes, A/B)
+    static const int qb1_env = getenv("HIPRAG_QB1_GROUPS") ? atoi(getenv("HIPRAG_QB1_GROUPS")) : 1;
+    if (QB == 1 && B > 32 && h->dtype != F32 && qb1_env) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
     if (p->NG > 1 && (p->NG & 1) && wide_capable(h)) p->NG = std::min(max_groups + (max_groups & 1), p->NG + 1);
     p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)

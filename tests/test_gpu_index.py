@@ -130,7 +130,8 @@ def test_random_vs_oracle(native, dim, dtype, n, B, k):
 
 # top-k beyond 32 (kb_file_search recall 15 x 3, rerank top-100): ceil(kc/32) row parts of group maxima
 LARGE_K = [(768, "bf16", 40000, 64, 45), (1024, "bf16", 30000, 64, 100), (256, "f16", 9000, 33, 128),
-           (384, "f32", 20000, 20, 64), (128, "bf16", 3000, 5, 128), (64, "bf16", 150, 3, 100)]
+           (384, "f32", 20000, 20, 64), (128, "bf16", 3000, 5, 128), (64, "bf16", 150, 3, 100),
+           (2304, "bf16", 20000, 64, 100), (2048, "f16", 12000, 96, 32)]
 
 
 @pytest.mark.parametrize("dim,dtype,n,B,k", LARGE_K)

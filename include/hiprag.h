@@ -63,7 +63,7 @@ enum {
 };
 
 #define HR_MAX_K 128           /* largest top-k (kb_file_search recall 15 x 3, rerank top-100) */
-#define HR_MAX_KC 192          /* largest per-shard candidate count kc (k = HR_MAX_K with its k/2 margin) */
+#define HR_MAX_KC 256          /* largest per-shard candidate count kc (k = HR_MAX_K with its margin) */
 
 int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);
 int hr_index_reserve(hr_index* h, int64_t capacity_rows);
@@ -102,9 +102,11 @@ void hr_index_destroy(hr_index* h);
  * Candidate record = {double exact_score; int64 global_row} (16 bytes).
  * kc = candidates per query kept by a shard (k <= kc <= HR_MAX_KC); the scan keeps
  * ceil(kc/32) row parts of group maxima.  hr_kc_for_k gives the kc the single-GPU search
- * uses: k + max(16, k/2) rounded up to a multiple of 32, at most HR_MAX_KC (margin for the
- * guard; 32 for k <= 16). */
+ * uses below 2048 dims: k + max(16, k/2) rounded up to a multiple of 32, at most HR_MAX_KC (margin
+ * for the guard; 32 for k <= 16).  hr_kc_for_k_dim(k, dim) is the kc for a given dim (the margin
+ * grows to max(20, k) from 2048 dims on); hr_kc_for_k(k) = hr_kc_for_k_dim(k, 0). */
 int hr_kc_for_k(int k);
+int hr_kc_for_k_dim(int k, int dim);
 int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int k, int kc, const uint64_t* row_mask_dev,
                           int64_t row_offset, void* cand_out_dev /* B*kc records */,
                           double* bound_out_dev /* B */, void* stream);

@@ -44,6 +44,10 @@ def test_library_loads_and_reports_errors():
         [_native.kc_for_k(k) for k in range(1, _native.HR_MAX_K + 1)]
     assert _native.kc_for_k(_native.HR_MAX_K) <= _native.HR_MAX_KC and _native.kc_for_k(45) == 96 and _native.kc_for_k(100) == 160
     assert _native.kc_for_k(10) == 32 and _native.kc_for_k(32) == 64 and _native.kc_for_k(128) == 192
+    for dim in (64, 1024, 1100, 2000, 2048, 2304):
+        assert [L.hr_kc_for_k_dim(k, dim) for k in range(1, _native.HR_MAX_K + 1)] == \
+            [_native.kc_for_k(k, dim) for k in range(1, _native.HR_MAX_K + 1)]
+    assert _native.kc_for_k(10, 2304) == 32 and _native.kc_for_k(16, 2304) == 64 and _native.kc_for_k(64, 2304) == 128 and _native.kc_for_k(128, 2304) == 256
     with pytest.raises(ValueError):  # argument validation happens before any device call
         _native.NativeIndex(0, "bf16", "cosine")
     with pytest.raises(ValueError):

@@ -53,7 +53,7 @@ for name, q in (("planted", planted), ("isotropic", iso)):
         ms = (time.perf_counter() - t0) * 1e3 / 3
         after = idx.stats()
         tot, mx = idx.last_candidates()
-        print(f"{DT} {MET} allowed {ALLOWED:g} deleted {DELETED:g} {name:9s} k={k:3d} kc={_native.kc_for_k(k):3d}: {ms:7.2f} ms/batch, guard failures "
+        print(f"{DT} {MET} allowed {ALLOWED:g} deleted {DELETED:g} {name:9s} k={k:3d} kc={_native.kc_for_k(k, D):3d}: {ms:7.2f} ms/batch, guard failures "
               f"{(after['guard_failures'] - before['guard_failures']) / 3:.1f}/{B}, exhaustive "
               f"{(after['exhaustive'] - before['exhaustive']) / 3:.1f}, candidates/query {tot / B:.0f} max {mx}",
               flush=True)

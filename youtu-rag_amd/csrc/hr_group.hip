@@ -293,7 +293,7 @@ static int gather(hr_index* g, int B, int kc, DevBuf hr_index::*cand, DevBuf hr_
 // (primary device), k <= HR_MAX_K; mask_host: the handle's row bitmap or null
 static int group_search_impl(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_host, float* s_out,
                              int64_t* r_out, hipStream_t st) {
-    const int kc = hr_kc_for_k(k);
+    const int kc = hr_kc_for_k_dim(k, g->dim);
     TileListReset reset{g};
     std::vector<const uint64_t*> mdev;
     if (int rc = shard_masks(g, mask_host, mdev)) return rc;

@@ -931,7 +931,7 @@ int launch_merge(int device, const Cand* cand, const double* bounds, int G, int 
 // main pass of a single-shard search on device-resident queries: candidates, merge, guard flags
 static int search_main(hr_index* h, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
                        int64_t* r_out, hipStream_t st) {
-    const int kc = hr_kc_for_k(k);
+    const int kc = hr_kc_for_k_dim(k, h->dim);
     HIP_TRY(h->cand.ensure((size_t)B * kc * sizeof(Cand)));
     HIP_TRY(h->bound.ensure((size_t)B * 8));
     HIP_TRY(h->kth.ensure((size_t)B * 8));
@@ -1698,12 +1698,17 @@ extern "C" int hr_device_count(int* n_out) {
 extern "C" const char* hr_last_error(void) { return g_err.c_str(); }
 extern "C" int hr_abi_version(void) { return 2; }
 
-extern "C" int hr_kc_for_k(int k) {
-    // margin beyond k: max(16, k/2), for every k.  Dense clusters put many rows within the guard's E of
+extern "C" int hr_kc_for_k(int k) { return hr_kc_for_k_dim(k, 0); }
+
+extern "C" int hr_kc_for_k_dim(int k, int dim) {
+    // margin beyond k: max(16, k/2), for every k; max(20, k) from 2048 dims on (Youtu-Embedding's
+    // 2048 / 2304): the guard's window widens against the score spread (sigma ~ 1/sqrt(D)), and at
+    // 2M x 2304 rows k = 64 / 128 with a k/2 margin sent 27 / 20 of 64 queries to the collect pass.  Dense clusters put many rows within the guard's E of
     // the k-th score; at k = 100 a 16-row margin sent half the queries of a clustered corpus to the
     // collect fallback (5.3 ms/batch at 6.25M rows), k/2 sends almost none (2.8 ms).  kc = 32 for every
     // k <= 32 left no margin at k = 32 (every query of a 10M batch failed the guard: 7.2 vs 3.3 ms) and
     // HR_MAX_KC = 160 only 32 rows at k = 128 (83 % failures, 8.2 ms; tools/diag_k.py)
-    const int margin = std::max(16, k / 2);
+    const int wide = (dim + 63) / 64 * 64 >= 2048 ? 2 : 1;
+    const int margin = std::max(wide == 2 ? 20 : 16, wide * k / 2);  // (20: k = 16 lacked margin at 2304 dims)
     return std::min(HR_MAX_KC, (k + margin + 31) / 32 * 32);
 }

@@ -19,13 +19,15 @@ LIB_PATH = os.path.join(_HERE, "libhiprag.so")
 DTYPES = {"f32": 0, "float32": 0, "fp32": 0, "bf16": 1, "bfloat16": 1, "f16": 2, "float16": 2, "fp16": 2}
 METRICS = {"cosine": 0, "ip": 1, "dot": 1, "euclidean": 2, "l2": 2}
 HR_MAX_K = 128   # include/hiprag.h
-HR_MAX_KC = 192
+HR_MAX_KC = 256
 
 
-def kc_for_k(k: int) -> int:
-    """Per-shard candidate count for top-k (hr_kc_for_k): k + max(16, k // 2) rounded up to 32 (32 for
-    k <= 16), at most HR_MAX_KC (tests/test_native_abi.py checks it against the library)."""
-    return min(HR_MAX_KC, (k + max(16, k // 2) + 31) // 32 * 32)
+def kc_for_k(k: int, dim: int = 0) -> int:
+    """Per-shard candidate count for top-k (hr_kc_for_k_dim): k + max(16, k // 2) rounded up to 32 (32
+    for k <= 16), the margin max(20, k) from 2048 dims on, at most HR_MAX_KC (tests/test_native_abi.py
+    checks it against the library)."""
+    wide = 2 if (dim + 63) // 64 * 64 >= 2048 else 1
+    return min(HR_MAX_KC, (k + max(20 if wide == 2 else 16, wide * k // 2) + 31) // 32 * 32)
 
 
 CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand
@@ -41,7 +43,7 @@ EXPORTS = [
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
-    "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays",
+    "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_kc_for_k_dim",
 ]
 
 _lib = None
@@ -119,6 +121,8 @@ def load_library(path: str | None = None):
         L.hr_abi_version.restype = i32
         L.hr_kc_for_k.argtypes = [i32]
         L.hr_kc_for_k.restype = i32
+        L.hr_kc_for_k_dim.argtypes = [i32, i32]
+        L.hr_kc_for_k_dim.restype = i32
         _lib = L
         return L
 

@@ -103,7 +103,7 @@ class ShardedSearch:
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
         # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
-        self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k)
+        self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k, int(getattr(index, "dim", 0)))
         self.max_batch = int(max_batch)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         pinned = self.device.type == "cuda"

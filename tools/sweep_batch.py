@@ -47,7 +47,7 @@ def main():
                                        for i in range(nb)])).to(dev)
         ready = torch.cuda.Event()
         ready.record()
-        ss = ShardedSearch(idx, 0, max_batch=B, device=dev)
+        ss = ShardedSearch(idx, 0, max_batch=B, device=dev, max_k=max(16, args.k))
         s = torch.empty((nb, B, args.k), dtype=torch.float32, device=dev)
         r = torch.empty((nb, B, args.k), dtype=torch.int64, device=dev)
         for i in range(5):

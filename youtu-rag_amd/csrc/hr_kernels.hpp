@@ -540,18 +540,25 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
                     key[qb][i] = f2key(gmax[qb][i]);
                 }
             }
-        // the other parts' groups of this lane (keys order like floats: min of keys = min of scores)
+        // the other parts' groups of this lane (keys order like floats: min of keys = min of scores).
+        // A part's 16*QB keys are loaded back to back before any is used -- one memory round trip per
+        // part (a load -> min chain waited for every load in turn: (np - 1) * 32 round trips per refresh)
         for (int p = 0; p < a.np; ++p) {
             if (p == part) continue;
             const int64_t off = (p - part) * a.pstride;
+            uint32_t k2[QB][16];
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    k2[qb][i] = __hip_atomic_load(gkq[qb] + off + 32 * ((i & 3) + 8 * (i >> 2)), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    uint32_t k2 = __hip_atomic_load(gkq[qb] + off + 32 * ((i & 3) + 8 * (i >> 2)), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-                    k2 = k2 > HR_KEY_NEG_INF ? k2 : HR_KEY_NEG_INF;
-                    key[qb][i] = key[qb][i] < k2 ? key[qb][i] : k2;
+                    const uint32_t v = k2[qb][i] > HR_KEY_NEG_INF ? k2[qb][i] : HR_KEY_NEG_INF;
+                    key[qb][i] = key[qb][i] < v ? key[qb][i] : v;
                 }
         }
 #pragma unroll

@@ -56,8 +56,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU search time the cpu_baseline accumulates")
     p.add_argument("--cpu-ref-rows", type=int, default=1_000_000, help="row sample of the reference-path CPU baseline")
     p.add_argument("--cpu-embed-preset", default="bge-large")
-    p.add_argument("--recall-queries", type=int, default=4)
+    p.add_argument("--recall-queries", type=int, default=8, help="planted and isotropic queries of the recall checks")
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
+    p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
     p.add_argument("--single-process", action="store_true",
                    help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()
@@ -183,6 +184,50 @@ def cpu_reference_baseline(args, qbatches, N, D, K, B):
     return out
 
 
+def isotropic_queries(B: int, D: int, seed: int = 7) -> np.ndarray:
+    """B isotropic Gaussian queries: no planted neighbour, so every top-k score sits in the dense upper
+    tail of the corpus' score distribution -- the smallest gaps between ranks, the hardest case for a
+    quantised store's ranking."""
+    return np.random.default_rng(seed).standard_normal((B, D)).astype(np.float32)
+
+
+def recall_checks(args, N, D, K, q_pl, got_pl, s_pl, q_iso, got_iso, s_iso) -> dict:
+    """The GPU's top-k against the CPU oracle over ALL N rows, for planted and isotropic queries:
+    (i) ``ids_identical`` / ``recall_at_10`` / ``max_score_err`` -- against the exact answer over the rows
+    as the GPU stores them (args.dtype): the parity claim (bit-exact ids, scores within 0);
+    (ii) ``recall_at_10_vs_fp32`` -- against the exact answer over the UNQUANTISED fp32 rows, which is
+    what the reference's store holds (faiss_store.py:98, normalize_L2 + IndexFlatIP over float32): how far
+    a bf16 store's ranking departs from the reference's answers."""
+    import oracle
+    from oracle import ref_numpy as R
+
+    out = {}
+    t1 = time.time()
+    qn = R.process_queries(np.concatenate([q_pl, q_iso]), "cosine")
+    got = np.concatenate([got_pl, got_iso])
+    s_gpu = np.concatenate([s_pl, s_iso])
+    n_pl = len(q_pl)
+
+    def rec(a, b):
+        return float(np.mean([len(set(a[i]) & set(b[i])) / K for i in range(len(a))]))
+
+    s_ref, r_ref = oracle.c_search_synthetic(args.seed, 0, N, D, args.dtype, "cosine", qn, K)
+    out["recall_at_10"] = rec(got[:n_pl], r_ref[:n_pl])
+    out["ids_identical"] = bool(np.array_equal(got, r_ref))
+    out["max_score_err"] = float(np.max(np.abs(s_gpu - s_ref.astype(np.float32))))
+    out["recall_check"] = (f"{n_pl} planted + {len(q_iso)} isotropic queries (first timed batch / one extra batch) "
+                           f"vs the CPU oracle over all {N} rows as stored ({args.dtype})")
+    if args.dtype != "f32":
+        _, r32 = oracle.c_search_synthetic(args.seed, 0, N, D, "f32", "cosine", qn, K)
+        out["recall_at_10_vs_fp32"] = {
+            "planted": rec(got[:n_pl], r32[:n_pl]), "isotropic": rec(got[n_pl:], r32[n_pl:]),
+            "top1_agree": float(np.mean(got[:, 0] == r32[:, 0])),
+            "reference": f"exact top-{K} over the unquantised fp32 rows (the reference store's dtype), "
+                         f"{n_pl} planted + {len(q_iso)} isotropic queries"}
+    log(f"recall checks {time.time() - t1:.1f}s")
+    return out
+
+
 def main_single_process(args):
     """--single-process: ONE process, ONE index handle over --gpus devices (hr_index_create with
     n_dev > 1: rows striped over the GPUs by tile, per-shard scans on every device at once, the
@@ -229,46 +274,104 @@ def main_single_process(args):
                                      f"striped over {len(devs)} shards", "rows": N, "dim": D, "batch": B, "k": K,
                          "parallelism": f"onehandle{len(devs)}", "devices": devs}}
     if not args.no_cpu:
-        import oracle
-        from oracle import ref_numpy as R
-
+        q_iso = isotropic_queries(B, D)
+        qi_dev = torch.from_numpy(q_iso).to(dev)
+        s_iso = torch.empty((B, K), dtype=torch.float32, device=dev)
+        r_iso = torch.empty((B, K), dtype=torch.int64, device=dev)
+        index.search_device(qi_dev.data_ptr(), B, K, s_iso.data_ptr(), r_iso.data_ptr(), stream=st)
+        torch.cuda.synchronize(dev)
         nq = min(args.recall_queries, B)
-        s_ref, r_ref = oracle.c_search_synthetic(args.seed, 0, N, D, args.dtype, "cosine",
-                                                 R.process_queries(q_dev[args.warmup, :nq].cpu().numpy(), "cosine"), K)
-        got = r_dev[args.warmup, :nq].cpu().numpy()
-        result["ids_identical"] = bool(np.array_equal(got, r_ref))
-        result["recall_at_10"] = float(np.mean([len(set(got[i]) & set(r_ref[i])) / K for i in range(nq)]))
+        result.update(recall_checks(args, N, D, K, q_dev[args.warmup, :nq].cpu().numpy(),
+                                    r_dev[args.warmup, :nq].cpu().numpy(), s_dev[args.warmup, :nq].cpu().numpy(),
+                                    q_iso[:nq], r_iso[:nq].cpu().numpy(), s_iso[:nq].cpu().numpy()))
     print(json.dumps(result), flush=True)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """``python bench.py --gpus N`` (N > 1) started without a torch.distributed launcher: start the N
+    rank processes (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) as CHILDREN of
+    this process and return their exit code.  This process never touches the GPU (no HIP call, no
+    exec), so the ranks own the devices; rank 0's JSON line reaches stdout through the child."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env={**os.environ, "HIPRAG_BENCH_LAUNCHED": "1"}).returncode
+
+
+def rank_env(args) -> tuple[int, int, int]:
+    """(world, rank, local_rank) of this process; exits non-zero when the launcher's world size is
+    not --gpus (a mismatch would otherwise print a line for the wrong number of GPUs)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
+    return world, rank, local
+
+
+def launch_probe(args) -> None:
+    """--launch-probe (tests): the rank flow up to the process group, no GPU -- every rank joins a gloo
+    group, rank 0 prints the world size the collective library sees and the ranks that answered."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank, _ = rank_env(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": dist.get_world_size() if world > 1 else 1, "ranks_answered": int(t.item()),
+                          "launched_by_bench": os.environ.get("HIPRAG_BENCH_LAUNCHED") == "1"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
     if args.single_process:
         return main_single_process(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.launch_probe:
+        return launch_probe(args)
     import torch
     import torch.distributed as dist
 
     from hiprag import _native, synth
     from hiprag.dist import ShardedSearch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    G = world
+    world, rank, local = rank_env(args)
     # rehearsal of the N > 1 flow on a one-GPU box (never the measured configuration): every rank on
     # GPU 0 and the gloo backend, as HIPRAG_BENCH_REHEARSE=1 (the exchange then takes the host path)
     rehearse = os.environ.get("HIPRAG_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
+    n_vis = torch.cuda.device_count()
+    if local >= n_vis:
+        log(f"error: rank {rank} needs GPU {local} but {n_vis} are visible (--gpus {args.gpus})")
+        sys.exit(3)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if G > 1:
+    if world > 1:
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    # the rank count the collective library actually sees goes into the JSON line
+    G = dist.get_world_size() if world > 1 else 1
 
     N, D, B, K = args.rows, args.dim, args.batch, args.k
     start = N * rank // G
@@ -320,6 +423,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     sample_ms, scan_ms = index.take_scan_times()
+    # one untimed batch of isotropic queries (the worst case for ranking: no planted neighbour), for the
+    # recall checks; every rank takes part (the merge is collective)
+    q_iso = isotropic_queries(B, D)
+    s_iso, r_iso = searcher.search(torch.from_numpy(q_iso).to(dev), K)
+    torch.cuda.synchronize()
     if G > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -396,26 +504,10 @@ def main():
 
     # recall@10 against the oracle's exact answer over the full corpus (rank 0)
     if rank == 0 and not args.no_cpu:
-        try:
-            import oracle
-            from oracle import ref_numpy as R
-
-            nq = min(args.recall_queries, B)
-            qb = qs[args.warmup][:nq]
-            t1 = time.time()
-            s_ref, r_ref = oracle.c_search_synthetic(args.seed, 0, N, D, args.dtype, "cosine",
-                                                     R.process_queries(qb, "cosine"), K)
-            got = r_dev[args.warmup, :nq].cpu().numpy()
-            rec = float(np.mean([len(set(got[i]) & set(r_ref[i])) / K for i in range(nq)]))
-            result["recall_at_10"] = rec
-            result["ids_identical"] = bool(np.array_equal(got, r_ref))
-            s_gpu = s_dev[args.warmup, :nq].cpu().numpy()
-            result["max_score_err"] = float(np.max(np.abs(s_gpu - s_ref.astype(np.float32))))
-            result["recall_check"] = f"{nq} queries of the first timed batch vs CPU oracle over all {N} rows"
-            log(f"recall check {time.time() - t1:.1f}s")
-        except Exception as e:  # report, never hide
-            result["recall_at_10"] = None
-            result["recall_error"] = repr(e)
+        nq = min(args.recall_queries, B)
+        result.update(recall_checks(args, N, D, K, qs[args.warmup][:nq], r_dev[args.warmup, :nq].cpu().numpy(),
+                                    s_dev[args.warmup, :nq].cpu().numpy(), q_iso[:nq],
+                                    r_iso[:nq].cpu().numpy(), s_iso[:nq].cpu().numpy()))
 
     # CPU baselines, rank 0, N=1 only: the reference's search path on the host cores (cpu_baseline),
     # the reference's per-query loop and the CPU query embedding beside it, and the exact fp64 oracle

@@ -41,6 +41,8 @@ class OracleIndex:
         if q.ndim == 1:
             q = q[None]
         allowed = self.live.copy()
+        if mask is not None and len(np.asarray(mask).reshape(-1)) * 64 < len(self.rows):
+            raise ValueError("row mask shorter than the index")  # as hiprag._native.NativeIndex.search
         if mask is not None:
             bits = np.unpackbits(np.asarray(mask, np.uint64).view(np.uint8), bitorder="little")[: len(allowed)]
             allowed &= bits.astype(bool)

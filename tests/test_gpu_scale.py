@@ -6,7 +6,8 @@
   top-k gaps shrink with N), so this is where the exactness guard and its collect / exhaustive
   fallbacks must hold; the guard counters (hr_index_stats) are printed.  Also: the pipelined
   two-stream path the bench times, and tombstones + a where-clause bitmap at 10M.
-* C2: 1M x 768, f32 and bf16 stores, B = 64, k = 10.
+* C2: 1M x 768, f32 and bf16 stores, B = 64, k = 10; the bf16 store's recall@10 against the exact
+  answer over the unquantised fp32 rows (the reference's store dtype).
 * C5: one 6.25M-row f16 IVF shard (50M / 8), nlist 8192, nprobe 32, k = 100, against the IVF
   restatement (FAISS IndexIVFFlat's algorithm, oracle/ref_numpy.ivf_search) evaluated on the rows
   of the probed lists only.
@@ -141,6 +142,32 @@ def test_c2_1M_768_vs_oracle(native, dtype):
         s_ref, r_ref = oracle.c_search_synthetic(seed, 0, n, dim, dtype, "cosine", R.process_queries(q, "cosine"), 10)
         print(f"\nC2 1Mx768 {dtype}: stats {idx.stats()}")
         _check(s, r, s_ref, r_ref)
+    finally:
+        idx.close()
+
+
+def test_c2_bf16_store_recall_vs_fp32(native):
+    """How far the bf16 store departs from the reference's answers: the reference stores fp32
+    (faiss_store.py:98 normalize_L2 + IndexFlatIP over float32; Chroma float32), so its exact answer
+    is the top-10 over the UNQUANTISED rows.  The bf16 store is exact over its stored values (the
+    test above); against the fp32 answer it differs where two rows' scores lie closer than the bf16
+    rounding of their dot products.  Measured recall@10 is printed and bounded (planted queries: one
+    clear neighbour + background ranks; isotropic: every rank in the dense tail).  The f32 store is
+    identical to the fp32 answer (test_c2_1M_768_vs_oracle[f32])."""
+    n, dim, seed = 1_000_000, 768, 11
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    try:
+        idx.add_synthetic(seed, 0, n)
+        planted, iso = _queries(seed, n, dim, 64, qseed=99)
+        q = np.concatenate([planted, iso])
+        _, r = idx.search(q, 10)
+        _, r32 = oracle.c_search_synthetic(seed, 0, n, dim, "f32", "cosine", R.process_queries(q, "cosine"), 10)
+        rec = [np.mean([len(set(r[i]) & set(r32[i])) / 10 for i in sl]) for sl in (range(64), range(64, 128))]
+        top1 = float(np.mean(r[:, 0] == r32[:, 0]))
+        print(f"\nC2 1Mx768 bf16 store vs exact fp32: recall@10 planted {rec[0]:.4f} isotropic {rec[1]:.4f}, "
+              f"top-1 agreement {top1:.4f}")
+        assert top1 == 1.0
+        assert rec[0] >= 0.95 and rec[1] >= 0.95
     finally:
         idx.close()
 

@@ -29,14 +29,19 @@ def _chunks(d, meta):
                   metadata={"group": m["group"]}, embedding=d["corpus"][r].tolist()) for r, m in enumerate(meta["metas"])]
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [None, "f32", "bf16"])
 def test_store_retriever_golden(tmp_path, golden_dir, dtype):
+    """dtype None: no index_params dtype -- the store's default must be fp32, what the reference stores
+    (faiss_store.py:98; Chroma float32), so the golden ranks and scores are reproduced exactly."""
     d = dict(np.load(os.path.join(golden_dir, "c1_retrieval.npz")))
     meta = json.load(open(os.path.join(golden_dir, "c1_retrieval.json")))
     cfg = VectorStoreConfig(backend="hip", collection_name="c1", persist_directory=str(tmp_path),
-                            index_params={"dtype": dtype})
+                            index_params={} if dtype is None else {"dtype": dtype})
     store = VectorStoreFactory.create(cfg)
     assert isinstance(store, HipVectorStore)
+    if dtype is None:
+        assert store.dtype == "f32"
+        dtype = "f32"
     asyncio.run(store.add_chunks(_chunks(d, meta)))
     emb = TableEmbedder(dict(zip(meta["query_names"], d["queries"])))
     for tag, rc, kw in [("thr0", RetrieverConfig(top_k=5, similarity_threshold=0.0), {}),

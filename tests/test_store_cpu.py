@@ -195,3 +195,102 @@ def test_journal_format_roundtrip(tmp_path):
     assert ops[0][0] == "add" and ops[0][1] == [{"id": "a"}, None, {"id": "c"}]
     np.testing.assert_array_equal(ops[0][2], v)
     assert ops[1][0] == "del" and ops[1][1].tolist() == [5, 7]
+
+
+# ---------------------------------------------------------------- concurrency fixes (round-2 advisor)
+def test_rows_added_between_prep_and_run_of_filtered_search(tmp_path):
+    """The filter bitmap is built when the search runs (under the store lock), not when it was queued:
+    rows added in between cannot make it too short, and rows outside the filter are never returned."""
+    s = make_store(tmp_path, persist=False)
+    s.add_chunks_sync(chunks("a", 100))
+    q = np.random.default_rng(3).standard_normal((4, 16)).astype(np.float32)
+    prep = s._prep_search(q, 5, {"source": "src_a"})
+    s.add_chunks_sync(chunks("b", 5000, seed=1))      # 100 -> 5100 rows: 2 -> 80 bitmap words
+    res = s._assemble(prep, s._run_search(prep))
+    assert all(len(r) == 5 and all(c.document_id == "a" for c, _ in r) for r in res)
+    prep = s._prep_search(q, 5, {"source": "src_b"})
+    res = s._assemble(prep, s._run_search(prep))
+    assert all(len(r) == 5 and all(c.document_id == "b" for c, _ in r) for r in res)
+
+
+def test_bad_query_dim_fails_alone(tmp_path):
+    """A query of the wrong length is refused before it is queued; the other concurrent searches of the
+    same filter group complete (before: np.stack raised inside the drain task and every waiter hung)."""
+    s = make_store(tmp_path, persist=False)
+    s.add_chunks_sync(chunks("a", 50))
+    good = np.random.default_rng(4).standard_normal((8, 16)).astype(np.float32)
+
+    async def main():
+        tasks = [asyncio.ensure_future(s.search(query_embedding=g.tolist(), top_k=3)) for g in good]
+        bad = asyncio.ensure_future(s.search(query_embedding=[0.5] * 15, top_k=3))
+        done = await asyncio.wait_for(asyncio.gather(*tasks, bad, return_exceptions=True), 30)
+        return done
+
+    out = run(main())
+    assert isinstance(out[-1], ValueError)
+    assert all(isinstance(r, list) and len(r) == 3 for r in out[:-1])
+
+
+def test_clear_while_search_in_flight_drops_stale_rows(tmp_path):
+    s = make_store(tmp_path, persist=False)
+    s.add_chunks_sync(chunks("a", 50))
+    q = np.random.default_rng(5).standard_normal((2, 16)).astype(np.float32)
+    prep = s._prep_search(q, 5, None)
+    ran = s._run_search(prep)
+    s._clear_sync()
+    s.add_chunks_sync(chunks("b", 3000, seed=2))      # new rows reuse the old row numbers
+    assert s._assemble(prep, ran) == [[], []]
+
+
+def test_mutators_do_not_block_the_event_loop(tmp_path):
+    """add_chunks / delete / get_by_id wait for the store lock in a worker thread: while a search holds
+    the lock (here: another thread), the event loop keeps running other tasks."""
+    import threading
+
+    s = make_store(tmp_path, persist=False)
+    s.add_chunks_sync(chunks("a", 20))
+    held, release = threading.Event(), threading.Event()
+
+    def holder():
+        with s._lock:
+            held.set()
+            release.wait(10)
+
+    th = threading.Thread(target=holder)
+    th.start()
+    held.wait(10)
+
+    async def main():
+        ticks = 0
+        add = asyncio.ensure_future(s.add_chunks(chunks("b", 3, seed=1)))
+        get = asyncio.ensure_future(s.get_by_id("a_chunk_1"))
+        for _ in range(20):
+            await asyncio.sleep(0.005)
+            ticks += 1
+        assert not add.done() and not get.done()   # still waiting for the lock ...
+        release.set()                               # ... while the loop ran 20 ticks
+        await add
+        assert (await get).id == "a_chunk_1"
+        return ticks
+
+    assert run(main()) == 20
+    th.join()
+    assert run(s.count()) == 23
+
+
+def test_sibling_collection_files_survive_clear(tmp_path):
+    def store(name):
+        cfg = VectorStoreConfig(backend="hip", collection_name=name, persist_directory=str(tmp_path),
+                                index_params={"dtype": "f32", "persist": True, "fsync": False})
+        return HipVectorStore(cfg, index_factory=lambda dim: OracleIndex(dim, "f32"),
+                              index_loader=lambda path, dim, dt, metric: OracleIndex.load(path))
+
+    a, b = store("docs"), store("docs.gov")
+    run(a.add_chunks(chunks("x", 10)))
+    run(b.add_chunks(chunks("y", 10, seed=1)))
+    before = set(os.listdir(tmp_path))
+    run(a.clear())
+    left = set(os.listdir(tmp_path))
+    assert {f for f in before if f.startswith("docs.gov.")} <= left
+    assert not any(f.startswith("docs.") and not f.startswith("docs.gov.") for f in left)
+    assert run(store("docs.gov").count()) == 10

@@ -53,6 +53,24 @@ def main(src, tag, alg_bytes=None):
            "k_scan_filter_ms_avg": statistics.mean(filt) if filt else None, "k_scan_filter_launches": len(filt),
            "k_scan_filter_busy_ms_per_launch": busy / 1e6 / len(filt) if filt else None,
            "k_scan_sample_ms_avg": statistics.mean(samp) if samp else None}
+    # launch PERIOD (start to start of consecutive FILTER launches): what one step costs the scan stream;
+    # with overlapping launches (dual FILTER streams) it is shorter than a launch's duration
+    starts = sorted(int(r["Start_Timestamp"]) for r in filt_rows)
+    if len(starts) > 2:
+        per = [(b - a) / 1e6 for a, b in zip(starts, starts[1:])]
+        out["k_scan_filter_period_ms_median"] = statistics.median(per)
+    # the bench's own JSON line from the profiled run (tools/profile.sh keeps its stdout): its ms_per_step
+    # is the step the profiled kernels belong to, so the two are compared within one run
+    log = os.path.join(src, "bench_kt.log")
+    if os.path.exists(log):
+        lines = [ln for ln in open(log, errors="replace") if ln.startswith("{")]
+        if lines:
+            b = json.loads(lines[-1])
+            out["profiled_run"] = {"ms_per_step": b.get("ms_per_step"), "value": b.get("value"),
+                                   "steps": b.get("steps"), "warmup": b.get("warmup"),
+                                   "event_avg_launch_ms": (b.get("roofline") or {}).get("avg_launch_ms")}
+            if b.get("ms_per_step") and filt:
+                out["profiled_run"]["filter_avg_over_ms_per_step"] = statistics.mean(filt) / b["ms_per_step"]
     p = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
     if os.path.exists(p):  # MFMA pipe busy fraction of the FILTER launches
         shutil.copy(p, f"profiles/{tag}_pmc_mfma.csv")

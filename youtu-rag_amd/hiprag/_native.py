@@ -248,7 +248,13 @@ class NativeIndex:
         B = q.shape[0]
         s = np.empty((B, k), np.float32)
         r = np.empty((B, k), np.int64)
-        m = None if mask is None else np.ascontiguousarray(mask, np.uint64)
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, np.uint64).reshape(-1)
+            n_rows = self.size()[0]
+            if len(m) * 64 < n_rows:  # the library reads one bit per index row
+                raise ValueError(f"row mask has {len(m)} words, the index {n_rows} rows "
+                                 f"(needs {(n_rows + 63) // 64})")
         _check(self.lib.hr_index_search(self._h, _ptr(q), B, int(k), _ptr(m), _ptr(s), _ptr(r)))
         return s, r
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 import io
 import json
 import os
+import re
 import struct
 import zlib
 
@@ -86,9 +87,11 @@ class Paths:
         d = self.dir
         if not os.path.isdir(d):
             return []
-        name = os.path.basename(self.base)
-        return [os.path.join(d, f) for f in os.listdir(d)
-                if f == name + ".manifest.json" or f.startswith(name + ".g") or f in (name + ".hri", name + ".rows.jsonl")]
+        # exactly this collection's names: a prefix match would also take a sibling collection's files
+        # ("docs" vs "docs.gov")
+        pat = re.compile(re.escape(os.path.basename(self.base))
+                         + r"\.(manifest\.json|g\d+\.(hri|rows\.jsonl|emb\.npy|journal)|hri|rows\.jsonl)(\.tmp)?")
+        return [os.path.join(d, f) for f in os.listdir(d) if pat.fullmatch(f)]
 
 
 class Journal:

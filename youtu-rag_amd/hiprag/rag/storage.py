@@ -26,9 +26,12 @@ arrive while a launch is in flight form the next batch (no timer: the batch size
 the load).  Results are identical to sequential calls (top-k of a smaller k is the prefix of
 the larger k's, order score desc / row asc).
 
-Embeddings: the index keeps the normalised vectors in ``dtype`` (bf16 by default, 2 B per
-element -- search is exact over the stored values, ranking ties at the bf16 resolution can
-differ from an fp32 store); ``dtype: f32`` keeps fp32 rows.  Chroma returns the raw fp32
+Embeddings: the index keeps the normalised vectors in ``dtype``: fp32 by default, what the
+reference stores (faiss_store.py:98; Chroma float32), so rankings and scores are the reference's.
+``dtype: bf16`` (opt-in) halves the bytes per row and doubles the scan rate; search is then exact
+over the stored bf16 values, whose ranking departs from the fp32 answer where two rows' scores lie
+within the bf16 rounding of their dot products: recall@10 against the exact fp32 top-10 measured
+0.99 at 1M-10M rows (bench.py ``recall_at_10_vs_fp32``, tests/test_gpu_scale.py).  Chroma returns the raw fp32
 embedding it stored (chroma_store.py:233-244): ``keep_embeddings: true`` keeps a host fp32
 copy for ``get_by_id`` / ``include_embeddings``; without it they return the stored
 (normalised, quantised) row.
@@ -112,6 +115,9 @@ class _SearchBatcher:
         self.launches = 0  # diagnostics
 
     async def search(self, q: np.ndarray, top_k: int, filters):
+        dim = self.store.dim
+        if dim is not None and q.shape[0] != dim:  # checked before queueing: a bad query fails alone
+            raise ValueError(f"query dim {q.shape[0]} != collection dim {dim}")
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         self.pending.append((q, int(top_k), filters, _filter_key(filters), fut))
@@ -129,24 +135,30 @@ class _SearchBatcher:
         self.pending = rest
         return batch
 
+    @staticmethod
+    def _fail(batch, exc):
+        for e in batch:
+            if not e[4].done():
+                e[4].set_exception(exc)
+
     async def _drain(self):
         inflight: dict = {}  # task -> batch
+        batch: list = []
         try:
             while self.pending or inflight:
                 while self.pending and len(inflight) < self.depth:
                     batch = self._take()
-                    qs = np.stack([e[0] for e in batch])
-                    k = max(e[1] for e in batch)
-                    self.launches += 1
                     try:
+                        qs = np.stack([e[0] for e in batch])
+                        k = max(e[1] for e in batch)
+                        self.launches += 1
                         prep = self.store._prep_search(qs, k, batch[0][2])
-                    except Exception as exc:  # noqa: BLE001
-                        for e in batch:
-                            if not e[4].done():
-                                e[4].set_exception(exc)
+                    except Exception as exc:  # noqa: BLE001 -- this batch's waiters see the failure
+                        self._fail(batch, exc)
                         continue
                     task = asyncio.ensure_future(asyncio.to_thread(self.store._run_search, prep))
                     inflight[task] = (batch, prep)
+                batch = []
                 if not inflight:
                     continue
                 done, _ = await asyncio.wait(list(inflight), return_when=asyncio.FIRST_COMPLETED)
@@ -155,13 +167,18 @@ class _SearchBatcher:
                     try:
                         res = self.store._assemble(prep, task.result())
                     except Exception as exc:  # noqa: BLE001 -- every waiter sees the failure
-                        for e in batch:
-                            if not e[4].done():
-                                e[4].set_exception(exc)
+                        self._fail(batch, exc)
                         continue
                     for e, r in zip(batch, res):
                         if not e[4].done():
                             e[4].set_result(r[: e[1]])
+                batch = []
+        except BaseException as exc:  # never leave a waiter hanging: fail what this drain holds
+            err = exc if isinstance(exc, Exception) else RuntimeError(f"search batcher stopped: {exc!r}")
+            self._fail(batch, err)
+            for b, _ in inflight.values():
+                self._fail(b, err)
+            raise
         finally:
             self.running = False
 
@@ -176,7 +193,7 @@ class HipVectorStore(BaseVectorStore):
     def __init__(self, config: VectorStoreConfig, *, index_factory=None, index_loader=None):
         self.config = config
         params = dict(config.index_params or {})
-        self.dtype = params.get("dtype", "bf16")
+        self.dtype = params.get("dtype", "f32")  # the reference's store dtype; bf16 is an opt-in
         devs = params.get("devices")
         self.devices = [int(d) for d in devs] if devs else [int(params.get("device", 0))]
         self.device = self.devices[0]
@@ -204,6 +221,9 @@ class HipVectorStore(BaseVectorStore):
             self._load_if_present()
 
     def _reset_tables(self):
+        # bumped on every reset (clear / delete_collection): a search that ran against the previous
+        # tables must not resolve its rows through the new ones
+        self._epoch = getattr(self, "_epoch", 0) + 1
         self._index = None
         self.dim: int | None = None
         # host tables, one entry per index row (None = deleted): a tuple of atoms (id, document_id, content,
@@ -412,7 +432,14 @@ class HipVectorStore(BaseVectorStore):
         self._log("add", records=records, vectors=vectors)
         logger.info("added %d chunks to %s", len(fresh), self.config.collection_name)
 
+    # The async mutators and get_by_id take the store lock in a worker thread: a search launch holds it
+    # for a whole GPU pass, and the event loop (where the batcher assembles results) must never wait on it.
     async def add_chunks(self, chunks: list[Chunk]) -> None:
+        if not chunks:
+            return
+        await asyncio.to_thread(self.add_chunks_sync, chunks)
+
+    def add_chunks_sync(self, chunks: list[Chunk]) -> None:
         if not chunks:
             return
         with self._lock:
@@ -472,27 +499,41 @@ class HipVectorStore(BaseVectorStore):
             self._log("del", rows=rows)
         return len(rows)
 
+    def _delete_sync(self, chunk_ids: list[str]) -> None:
+        with self._lock:
+            if self._index is not None:
+                self._remove_tables([self._id_to_row[c] for c in chunk_ids if c in self._id_to_row])
+
     async def delete(self, chunk_ids: list[str]) -> None:
         if not chunk_ids or self._index is None:
             return
+        await asyncio.to_thread(self._delete_sync, chunk_ids)
+
+    def _delete_document_sync(self, document_id: str) -> int:
         with self._lock:
-            self._remove_tables([self._id_to_row[c] for c in chunk_ids if c in self._id_to_row])
+            if self._index is None:
+                return 0
+            return self._remove_tables(list(self._doc_rows.get(document_id, ())))
 
     async def delete_by_document_id(self, document_id: str) -> int:
         if self._index is None:
             return 0
-        with self._lock:
-            n = self._remove_tables(list(self._doc_rows.get(document_id, ())))
+        n = await asyncio.to_thread(self._delete_document_sync, document_id)
         logger.info("deleted %d chunks for document_id %s", n, document_id)
         return n
+
+    def _delete_by_metadata_sync(self, metadata_filter: dict[str, Any]) -> int:
+        with self._lock:
+            if self._index is None:
+                return 0
+            n = len(self._records)
+            hit = F.evaluate(metadata_filter, self._cols) & self._live[:n]
+            return self._remove_tables(np.nonzero(hit)[0].tolist())
 
     async def delete_by_metadata(self, metadata_filter: dict[str, Any]) -> int:
         if self._index is None or not metadata_filter:
             return 0
-        with self._lock:
-            n = len(self._records)
-            hit = F.evaluate(metadata_filter, self._cols) & self._live[:n]
-            return self._remove_tables(np.nonzero(hit)[0].tolist())
+        return await asyncio.to_thread(self._delete_by_metadata_sync, metadata_filter)
 
     def _clear_sync(self):
         with self._lock:
@@ -507,7 +548,7 @@ class HipVectorStore(BaseVectorStore):
                     os.remove(p)
 
     async def clear(self) -> None:
-        self._clear_sync()
+        await asyncio.to_thread(self._clear_sync)
 
     def delete_collection(self) -> None:
         """Drop the collection and its files (chroma_store.py:331, synchronous there too)."""
@@ -526,9 +567,10 @@ class HipVectorStore(BaseVectorStore):
                 self._index = None
 
     # ---------------------------------------------------------------- reads
-    def _chunk(self, row: int, embedding=None) -> Chunk:
-        rec = self._records[row]
-        meta = self._metas[row]
+    def _chunk(self, row: int, embedding=None, tables=None) -> Chunk:
+        recs, metas = tables or (self._records, self._metas)
+        rec = recs[row]
+        meta = metas[row]
         # a fresh metadata dict per result, as Chroma returns (callers may mutate it)
         return Chunk(rec[0], meta.get("document_id", ""), rec[2], meta.get("chunk_index", 0), dict(meta),
                      embedding)
@@ -551,44 +593,51 @@ class HipVectorStore(BaseVectorStore):
         return self._assemble(prep, self._run_search(prep))
 
     # search_batch in three steps, so the micro-batcher can run only the middle one in a worker thread
-    # (it holds the GIL for nothing but the ctypes call; a worker doing the Python parts was starved by
+    # (it holds the GIL for little but the ctypes call; a worker doing the Python parts was starved by
     # a busy event loop) and assemble on the event-loop thread while the next launch runs
     def _prep_search(self, query_embeddings, top_k: int, filters):
         q = np.asarray(query_embeddings, dtype=np.float32)
         if q.ndim == 1:
             q = q[None, :]
-        if self._index is None or self.count_sync() == 0 or int(top_k) <= 0:
-            return (q, 0, None)
-        if q.shape[1] != self.dim:
-            raise ValueError(f"query dim {q.shape[1]} != collection dim {self.dim}")
-        # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
-        # search takes its exhaustive exact path (same results, one corpus pass per query)
-        return (q, min(int(top_k), self.count_sync()), self.filter_bitmap(filters))
+        dim = self.dim
+        if dim is not None and q.shape[1] != dim:
+            raise ValueError(f"query dim {q.shape[1]} != collection dim {dim}")
+        return (q, int(top_k), filters)
 
     def _run_search(self, prep):
-        q, k, bitmap = prep
-        if k == 0:
-            return None
+        """The native search, under the store lock.  Everything that depends on the collection's
+        current state -- the live row count, the filter bitmap (sized to the index's rows NOW, not when
+        the query was queued: rows added in between would otherwise make the bitmap too short), the
+        tables the rows resolve through -- is taken here, under the same lock as the search."""
+        q, top_k, filters = prep
         with self._lock:  # ordered against mutations
-            if self._index is None:
-                return None
-            return self._index.search(q, k, bitmap)
+            tables = (self._records, self._metas, self._epoch)
+            n_live = self.count_sync()
+            if self._index is None or n_live == 0 or top_k <= 0:
+                return None, tables
+            # top_k beyond the live rows returns them all (Chroma/FAISS); beyond HR_MAX_K the native
+            # search takes its exhaustive exact path (same results, one corpus pass per query)
+            return self._index.search(q, min(top_k, n_live), self.filter_bitmap(filters)), tables
 
-    def _assemble(self, prep, raw) -> list[list[tuple[Chunk, float]]]:
+    def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
+        raw, (recs, metas, epoch) = ran
         n = len(prep[0])
-        if raw is None:
+        if raw is None or epoch != self._epoch:  # cleared since the search ran: its rows are gone
             return [[] for _ in range(n)]
         scores, rows = raw
         rows_l, scores_l = rows.tolist(), scores.tolist()  # Python ints / floats once, not per element
-        recs = self._records  # append-only list; a row deleted since the search reads None and is dropped
+        # the tables the search ran against (append-only; a row deleted since then reads None, dropped)
+        tables = (recs, metas)
         out = []
         for b in range(n):
             valid = [(r, sc) for r, sc in zip(rows_l[b], scores_l[b]) if r >= 0 and recs[r] is not None]
             embs = None
             if self.include_embeddings and valid:
                 with self._lock:
+                    if epoch != self._epoch:
+                        return [[] for _ in range(n)]
                     embs = self._embeddings([r for r, _ in valid])
-            out.append([(self._chunk(r, None if embs is None else embs[i].tolist()), s)
+            out.append([(self._chunk(r, None if embs is None else embs[i].tolist(), tables), s)
                         for i, (r, s) in enumerate(valid)])
         return out
 
@@ -599,12 +648,15 @@ class HipVectorStore(BaseVectorStore):
         q = np.asarray(query_embedding, dtype=np.float32).reshape(-1)
         return await self._batcher.search(q, top_k, filters)
 
-    async def get_by_id(self, chunk_id: str) -> Chunk | None:
+    def get_by_id_sync(self, chunk_id: str) -> Chunk | None:
         with self._lock:
             row = self._id_to_row.get(chunk_id)
             if row is None:
                 return None
             return self._chunk(row, self._embeddings([row])[0].tolist())
+
+    async def get_by_id(self, chunk_id: str) -> Chunk | None:
+        return await asyncio.to_thread(self.get_by_id_sync, chunk_id)
 
     def count_sync(self) -> int:
         return len(self._id_to_row)

@@ -37,7 +37,10 @@ import numpy as np  # noqa: E402
 
 METRIC = "retrieval QPS + recall@10 vs CPU ref, 10M×1024 corpus, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
-HBM_COPY_GBS = 6290.0
+# the practical read ceiling: a read-only kernel with the scan's access shape and launch (n_cu - 32 CUs,
+# 8 waves/CU, non-temporal 16 B lane loads) over 20.48 GB, tools/stream_ceiling.hip ->
+# profiles/r02_stream_ceiling.jsonl ("nt, n_cu-32 CUs, 8 waves/CU (the scan's launch)")
+HBM_READ_CEILING_GBS = 7076.6
 MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (no sparsity), MI355X_MICROARCH.md
 
 
@@ -232,8 +235,9 @@ def main_single_process(args):
     """--single-process: ONE process, ONE index handle over --gpus devices (hr_index_create with
     n_dev > 1: rows striped over the GPUs by tile, per-shard scans on every device at once, the
     candidates peer-copied to device 0 and merged there) -- the reference's deployment shape (one
-    FastAPI process, one store per collection).  Batches run synchronously through
-    hr_index_search_device; same JSON line as the multi-process path."""
+    FastAPI process, one store per collection).  Batches are pipelined through hr_index_search_submit /
+    _finalize (one host thread per shard, two batches in flight); same JSON line as the multi-process
+    path, plus the host time per batch of the caller and of the busiest shard thread."""
     import torch
 
     from hiprag import _native, synth
@@ -255,16 +259,30 @@ def main_single_process(args):
     s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
     r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
-    for i in range(args.warmup):
-        index.search_device(q_dev[i].data_ptr(), B, K, s_dev[i].data_ptr(), r_dev[i].data_ptr(), stream=st)
+
+    # pipelined: submit enqueues batch i on every shard (one host thread per shard) and returns; the
+    # handle keeps two batches in flight and finalizes the older one (guard flags, rare fallback) when a
+    # third arrives; every batch is final before the clock stops
+    def run(lo, hi):
+        tickets = [index.search_submit(q_dev[i].data_ptr(), B, K, s_dev[i].data_ptr(), r_dev[i].data_ptr(), stream=st)
+                   for i in range(lo, hi)]
+        for t in tickets:
+            index.search_finalize(t)
+
+    run(0, args.warmup)
     for d in set(devs):
         torch.cuda.synchronize(d)
+    h0 = index.host_us()
     t_start = time.perf_counter()
-    for i in range(args.warmup, n_batches):
-        index.search_device(q_dev[i].data_ptr(), B, K, s_dev[i].data_ptr(), r_dev[i].data_ptr(), stream=st)
+    run(args.warmup, n_batches)
     for d in set(devs):
         torch.cuda.synchronize(d)
     elapsed = time.perf_counter() - t_start
+    h1 = index.host_us()
+    nb = max(1, h1["batches"] - h0["batches"])
+    host = {"caller_submit_us": round((h1["submit_us"] * h1["batches"] - h0["submit_us"] * h0["batches"]) / nb, 1),
+            "busiest_shard_thread_us": round((h1["shard_thread_us"] * h1["batches"]
+                                              - h0["shard_thread_us"] * h0["batches"]) / nb, 1)} if len(devs) > 1 else None
     result = {"metric": METRIC, "value": round(args.steps * B / elapsed, 2), "unit": "queries/s",
               "n_gpus": len(set(devs)), "steps": args.steps, "warmup": args.warmup,
               "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "strong",
@@ -272,7 +290,8 @@ def main_single_process(args):
               "data": "synthetic: counter-based corpus generator (hiprag.synth), planted queries",
               "config": {"workload": f"{N / 1e6:g}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, one handle "
                                      f"striped over {len(devs)} shards", "rows": N, "dim": D, "batch": B, "k": K,
-                         "parallelism": f"onehandle{len(devs)}", "devices": devs}}
+                         "parallelism": f"onehandle{len(devs)}", "devices": devs},
+              "host_us_per_batch": host}
     if not args.no_cpu:
         q_iso = isotropic_queries(B, D)
         qi_dev = torch.from_numpy(q_iso).to(dev)
@@ -464,7 +483,8 @@ def main():
                    "rows": N, "dim": D, "batch": B, "k": K, "parallelism": f"rowshard{G}"},
         "roofline": {"bound": "hbm", "kernel": "k_scan (FILTER pass)", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "frac_of_copy_peak": round(achieved / HBM_COPY_GBS, 4), "traffic": None,
+                     "frac_of_measured_read_ceiling": round(achieved / HBM_READ_CEILING_GBS, 4),
+                     "read_ceiling_source": "profiles/r02_stream_ceiling.jsonl", "traffic": None,
                      "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg, 4),
                      "sample_pass_ms": round(sample_avg, 4)},
         # the Q·Xᵀ contraction of the same launch on the MFMA pipe (bf16 dense peak, MI355X_MICROARCH.md)
@@ -497,6 +517,10 @@ def main():
             result["roofline"]["traffic_unit"] = "GB per launch (HBM read, PMC)"
             result["roofline"]["traffic_source"] = os.path.relpath(summaries[-1], REPO)
             result["roofline"]["profiled_avg_launch_ms"] = round(prof["k_scan_filter_ms_avg"], 4)
+            if prof.get("k_scan_filter_period_ms_median"):  # start-to-start of consecutive FILTER launches
+                result["roofline"]["profiled_launch_period_ms"] = round(prof["k_scan_filter_period_ms_median"], 4)
+            if (prof.get("profiled_run") or {}).get("ms_per_step"):  # the bench line of that profiled run
+                result["roofline"]["profiled_run_ms_per_step"] = prof["profiled_run"]["ms_per_step"]
             if prof.get("k_scan_sample_fetch_bytes"):  # the SAMPLE pass beside it (L3 hits included)
                 result["roofline"]["sample_traffic"] = round(prof["k_scan_sample_fetch_bytes"] / 1e9, 3)
             if prof.get("k_scan_filter_busy_ms_per_launch"):  # overlapping launches (dual FILTER streams)

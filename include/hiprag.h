@@ -90,6 +90,21 @@ int hr_index_search(hr_index* h, const float* q, int B, int k, const uint64_t* r
                     int64_t* rows_out);
 int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const uint64_t* row_mask_dev,
                            float* scores_out_dev, int64_t* rows_out_dev, void* stream);
+/* Pipelined form of hr_index_search_device (no mask, k <= HR_MAX_K): enqueue a batch and return a
+ * ticket; hr_index_search_finalize(ticket) waits for that batch's exactness-guard flags, runs the exact
+ * fallback for queries that need it and returns once scores_out/rows_out hold the final results.  A
+ * multi-device handle keeps two batches in flight, every shard submitted by a host thread of its own
+ * (so host time per batch does not grow with the number of devices); submitting a third finalizes the
+ * oldest.  q_dev and the outputs must stay valid until the batch is finalized; other calls on the handle
+ * finalize every batch in flight first.  A single-device handle completes the batch inside submit
+ * (ticket 0).  Replaces VectorRetriever.batch_retrieve's sequential search loop (base_retriever.py:82-99)
+ * for a store spanning the node's GPUs (one cached store per collection, base_toolkit.py:79-91). */
+int hr_index_search_submit(hr_index* h, const float* q_dev, int B, int k, float* scores_out_dev, int64_t* rows_out_dev,
+                           void* stream, int64_t* ticket_out);
+int hr_index_search_finalize(hr_index* h, int64_t ticket);
+/* Diagnostics of the pipelined search: out[0] = caller host time per submit (us), out[1] = host time
+ * per batch of the busiest shard thread (us), out[2] = batches submitted. */
+int hr_index_host_us(hr_index* h, double* out);
 int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out);
 /* Shape of a handle (e.g. one returned by hr_index_load): dim, storage dtype, metric, devices. */
 int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* metric_out, int* n_dev_out);

@@ -198,3 +198,57 @@ def test_group_device_queries_and_store(native, tmp_path):
     ra = a2.search_batch(q[:8], 7)
     rb = b.search_batch(q[:8], 7)
     assert [[c.id for c, _ in x] for x in ra] == [[c.id for c, _ in x] for x in rb]
+
+
+def test_group_pipelined_submit_finalize(native):
+    """hr_index_search_submit / _finalize on a group handle: batches of different sizes in flight two at a
+    time (one host thread per shard), one of them forcing the guard's collect fallback (planted duplicates
+    on every shard), finalized in and out of order, a synchronous search and an add between submits
+    (they finalize what is in flight) -- every batch identical to the oracle."""
+    import torch
+
+    dim, n, G = 128, 30_000, 3
+    raw = R.gen_rows(41, 0, n, dim)
+    dups = np.sort(np.random.default_rng(4).choice(n, 150, replace=False))
+    raw[dups] = raw[dups[0]]
+    grp = native.NativeIndex(dim, "bf16", "cosine", devices=_devs(G))
+    grp.add(raw[:20_000])
+    rng = np.random.default_rng(8)
+    dev = torch.device("cuda", _devs(1)[0])
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def ref(rows_n, q, k):
+        return oracle.c_search(R.process_rows(raw[:rows_n], "cosine", "bf16"), "bf16", R.process_queries(q, "cosine"), k)
+
+    batches = []
+    for i, (B, k) in enumerate([(64, 10), (17, 10), (33, 100), (64, 10), (5, 3)]):
+        q = _queries(raw[:20_000], B, rng)
+        if i == 2:
+            q[0] = raw[dups[0]]  # a duplicated row: exact ties across shards -> collect fallback
+        qd = torch.from_numpy(q).to(dev)
+        s = torch.full((B, k), 7.0, dtype=torch.float32, device=dev)
+        r = torch.full((B, k), 7, dtype=torch.int64, device=dev)
+        t = grp.search_submit(qd.data_ptr(), B, k, s.data_ptr(), r.data_ptr(), stream=st)
+        assert t > 0
+        batches.append((t, q, qd, s, r, k))
+    before = grp.stats()["guard_failures"]
+    grp.search_finalize(batches[4][0])   # newest first: the older ones were finalized by later submits
+    grp.search_finalize(batches[3][0])
+    grp.search_finalize(batches[3][0])   # twice: no-op
+    torch.cuda.synchronize(dev)
+    for t, q, qd, s, r, k in batches:
+        _check(s.cpu().numpy(), r.cpu().numpy(), *ref(20_000, q, k))
+    assert grp.stats()["guard_failures"] >= before
+    # a submit, then an add and a synchronous search before its finalize
+    q = _queries(raw[:20_000], 40, rng)
+    qd = torch.from_numpy(q).to(dev)
+    s = torch.empty((40, 10), dtype=torch.float32, device=dev)
+    r = torch.empty((40, 10), dtype=torch.int64, device=dev)
+    t = grp.search_submit(qd.data_ptr(), 40, 10, s.data_ptr(), r.data_ptr(), stream=st)
+    grp.add(raw[20_000:])
+    _check(s.cpu().numpy(), r.cpu().numpy(), *ref(20_000, q, 10))   # final before the add ran
+    _check(*grp.search(q, 10), *ref(n, q, 10))
+    grp.search_finalize(t)
+    h = grp.host_us()
+    assert h["batches"] == 6 and h["submit_us"] > 0 and h["shard_thread_us"] > 0
+    grp.close()

@@ -102,6 +102,40 @@ def test_c3_pipelined_path_vs_oracle(c3):
                r_ref[64 * h:64 * (h + 1), :k])
 
 
+def test_c3_group_8_shards_pipelined_vs_oracle(c3, native):
+    """The single-process multi-GPU handle at C3: one handle striped over 8 shards (on a one-GPU box the
+    8 shards share the GPU: dev_ids = [0]*8 -- 8 x 1.25M rows, the per-GPU rows of the 8-GPU node), rows
+    generated in place (generator row = handle row, so the corpus is C3's), batches pipelined through
+    hr_index_search_submit / _finalize with one host thread per shard: planted and isotropic batches,
+    k = 10 and 100, identical to the oracle over all 10M rows."""
+    import torch
+
+    _, q, s_ref, r_ref = c3
+    n_vis = native.device_count()
+    devs = [i % n_vis for i in range(8)]
+    grp = native.NativeIndex(D3, "bf16", "cosine", devices=devs)
+    try:
+        grp.reserve(N3)
+        grp.add_synthetic(SEED3, 0, N3)
+        dev = torch.device("cuda", devs[0])
+        st = torch.cuda.current_stream(dev).cuda_stream
+        qd = torch.from_numpy(q).to(dev).view(2, 64, D3)
+        outs = []
+        for i, k in enumerate([10, 10, 100, 100, 10, 10]):
+            h = i % 2
+            s = torch.empty((64, k), dtype=torch.float32, device=dev)
+            r = torch.empty((64, k), dtype=torch.int64, device=dev)
+            outs.append((grp.search_submit(qd[h].data_ptr(), 64, k, s.data_ptr(), r.data_ptr(), stream=st), h, k, s, r))
+        for t, *_ in outs:
+            grp.search_finalize(t)
+        torch.cuda.synchronize(dev)
+        for _, h, k, s, r in outs:
+            _check(s.cpu().numpy(), r.cpu().numpy(), s_ref[64 * h:64 * (h + 1), :k], r_ref[64 * h:64 * (h + 1), :k])
+        print(f"\nC3 one handle x 8 shards: stats {grp.stats()}, host us {grp.host_us()}")
+    finally:
+        grp.close()
+
+
 def test_c3_tombstones_and_filter_vs_oracle(c3):
     """Deleted rows (tombstones) and a where-clause bitmap at 10M: a dense random filter (full scan
     with the mask fused into the scan) and a few documents' contiguous row ranges (tile list)."""

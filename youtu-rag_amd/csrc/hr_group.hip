@@ -16,6 +16,11 @@
 // shard and a second merge.  Results are identical to a single-device index holding the same rows.
 // The on-disk format is the single-index layout (tile t = handle tile t, slot swizzle of t), so a
 // file loads into any number of devices.
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <thread>
+
 #include "hr_internal.hpp"
 
 namespace {
@@ -73,6 +78,8 @@ struct TileListReset {  // the host tile lists are valid for one group search on
 
 }  // namespace
 
+static void pipe_stop(hr_index* g);
+
 int group_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
     hr_index* g = new hr_index();
     g->G = n_dev;
@@ -108,11 +115,46 @@ int group_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, 
         return set_err(HR_E_HIP, std::string("group_create: ") + hipGetErrorString(e));
     }
     g->n_cu = g->shards[0]->n_cu;
+    // peer access between the primary and every other device, once per pair (the candidate and query
+    // copies then go straight over xGMI; where it is refused hipMemcpyPeerAsync stages, still correct)
+    g->g_peer.assign((size_t)n_dev, 1);
+    for (int s = 0; s < n_dev; ++s) {
+        const int d = dev_ids[s];
+        if (d == g->device) continue;
+        bool seen = false;
+        for (int j = 0; j < s; ++j) seen |= dev_ids[j] == d;
+        if (seen) {
+            for (int j = 0; j < s; ++j)
+                if (dev_ids[j] == d) g->g_peer[(size_t)s] = g->g_peer[(size_t)j];
+            continue;
+        }
+        int a = 0, b = 0;
+        bool ok = hipDeviceCanAccessPeer(&a, g->device, d) == hipSuccess &&
+                  hipDeviceCanAccessPeer(&b, d, g->device) == hipSuccess && a && b;
+        if (ok) {
+            hipError_t e1 = hipSetDevice(g->device);
+            if (e1 == hipSuccess) e1 = hipDeviceEnablePeerAccess(d, 0);
+            hipError_t e2 = hipSetDevice(d);
+            if (e2 == hipSuccess) e2 = hipDeviceEnablePeerAccess(g->device, 0);
+            ok = (e1 == hipSuccess || e1 == hipErrorPeerAccessAlreadyEnabled) &&
+                 (e2 == hipSuccess || e2 == hipErrorPeerAccessAlreadyEnabled);
+            (void)hipGetLastError();  // an "already enabled" answer is not an error here
+        }
+        g->g_peer[(size_t)s] = ok ? 1 : 0;
+    }
+    if (hipSetDevice(g->device) != hipSuccess) {
+        group_destroy(g);
+        return set_err(HR_E_HIP, "group_create: hipSetDevice");
+    }
     *out = g;
     return HR_OK;
 }
 
 void group_destroy(hr_index* g) {
+    if (g->pipe) {
+        (void)group_drain(g);
+        pipe_stop(g);
+    }
     for (hr_index* s : g->shards) hr_index_destroy(s);
     for (size_t i = 0; i < g->g_ev.size(); ++i)
         if (g->g_ev[i]) (void)hipEventDestroy(g->g_ev[i]);
@@ -127,6 +169,7 @@ void group_destroy(hr_index* g) {
 }
 
 int group_reserve(hr_index* g, int64_t rows) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     const int64_t nt = (rows + 31) / 32;
     for (int s = 0; s < g->G; ++s) {
         hr_index* sh = g->shards[(size_t)s];
@@ -147,6 +190,7 @@ static void refresh_group_totals(hr_index* g) {
 }
 
 int group_add_host(hr_index* g, const float* rows, int64_t n, int64_t* first) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     const int G = g->G;
     const int64_t H0 = g->n;
     // blocks of whole handle tiles per shard (bounded host staging)
@@ -177,6 +221,7 @@ int group_add_host(hr_index* g, const float* rows, int64_t n, int64_t* first) {
 }
 
 int group_add_synthetic(hr_index* g, uint64_t seed, int64_t global_row0, int64_t n, int64_t* first) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     const int64_t H0 = g->n;
     const std::vector<int64_t> cnt = split_counts(H0, n, g->G);
     for (int s = 0; s < g->G; ++s) {
@@ -191,6 +236,7 @@ int group_add_synthetic(hr_index* g, uint64_t seed, int64_t global_row0, int64_t
 }
 
 int group_add_device(hr_index* g, const float* rows_dev, int64_t n, int64_t* first, hipStream_t st) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     // rows produced on the caller's device/stream: one D2H, then striped host adds per shard
     std::vector<float> h((size_t)n * g->dim);
     HIP_TRY(hipMemcpyAsync(h.data(), rows_dev, h.size() * 4, hipMemcpyDeviceToHost, st));
@@ -199,6 +245,7 @@ int group_add_device(hr_index* g, const float* rows_dev, int64_t n, int64_t* fir
 }
 
 int group_remove(hr_index* g, const int64_t* rows, int64_t n) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     for (int64_t i = 0; i < n; ++i)
         if (rows[i] < 0 || rows[i] >= g->n) return set_err(HR_E_INVALID, "row out of range");
     std::vector<std::vector<int64_t>> loc((size_t)g->G);
@@ -212,6 +259,7 @@ int group_remove(hr_index* g, const int64_t* rows, int64_t n) {
 }
 
 int group_get_rows(hr_index* g, const int64_t* rows, int64_t n, float* out) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     std::vector<std::vector<int64_t>> loc((size_t)g->G), pos((size_t)g->G);
     for (int64_t i = 0; i < n; ++i) {
         const int s = shard_of(rows[i], g->G);
@@ -253,19 +301,21 @@ static int shard_queries(hr_index* g, hr_index* sh, const float* q_dev, int B, D
 }
 
 // per-shard masks (device) + host tile lists from a host row mask of the handle
-static int shard_masks(hr_index* g, const uint64_t* mask_host, std::vector<const uint64_t*>& mdev) {
+// (words: per-shard host staging that must outlive the search -- the copies are asynchronous)
+static int shard_masks(hr_index* g, const uint64_t* mask_host, std::vector<const uint64_t*>& mdev,
+                       std::vector<std::vector<uint32_t>>& words) {
     mdev.assign((size_t)g->G, nullptr);
     if (!mask_host) return HR_OK;
-    std::vector<uint32_t> w;
+    words.resize((size_t)g->G);
     for (int s = 0; s < g->G; ++s) {
         hr_index* sh = g->shards[(size_t)s];
         if (sh->n == 0) continue;
+        std::vector<uint32_t>& w = words[(size_t)s];
         shard_mask_words((const uint32_t*)mask_host, g->n, g->G, s, sh->n, w);
         if (int rc = set_device(sh)) return rc;
         HIP_TRY(sh->s_mask.ensure(w.size() * 4));
         HIP_TRY(hipMemcpyAsync(sh->s_mask.p, w.data(), w.size() * 4, hipMemcpyHostToDevice, sh->stream));
         if (int rc = index_host_tile_list(sh, w.data(), sh->stream)) return rc;
-        HIP_TRY(hipStreamSynchronize(sh->stream));  // w is reused for the next shard
         mdev[(size_t)s] = (const uint64_t*)sh->s_mask.p;
     }
     return HR_OK;
@@ -289,54 +339,12 @@ static int gather(hr_index* g, int B, int kc, DevBuf hr_index::*cand, DevBuf hr_
     return HR_OK;
 }
 
-// exact top-k of B queries (q_dev on the primary, ordered on st) over all shards -> s_out / r_out
-// (primary device), k <= HR_MAX_K; mask_host: the handle's row bitmap or null
-static int group_search_impl(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_host, float* s_out,
-                             int64_t* r_out, hipStream_t st) {
-    const int kc = hr_kc_for_k_dim(k, g->dim);
-    TileListReset reset{g};
-    std::vector<const uint64_t*> mdev;
-    if (int rc = shard_masks(g, mask_host, mdev)) return rc;
-    HIP_TRY(hipSetDevice(g->device));
-    HIP_TRY(hipEventRecord(g->g_ev_q, st));
-    for (int s = 0; s < g->G; ++s) {  // every shard's scan + select + rescore, all devices at once
-        hr_index* sh = g->shards[(size_t)s];
-        if (int rc = set_device(sh)) return rc;
-        HIP_TRY(hipStreamWaitEvent(sh->stream, g->g_ev_q, 0));
-        HIP_TRY(sh->cand.ensure((size_t)B * kc * sizeof(Cand)));
-        HIP_TRY(sh->bound.ensure((size_t)B * 8));
-        const float* qs = nullptr;
-        if (int rc = shard_queries(g, sh, q_dev, B, sh->g_q, &qs)) return rc;
-        if (sh->n_live == 0) {  // nothing here: no candidates, bound -inf
-            std::vector<Cand> c((size_t)B * kc, Cand{-INFINITY, -1});
-            std::vector<double> b((size_t)B, -INFINITY);
-            HIP_TRY(hipMemcpyAsync(sh->cand.p, c.data(), c.size() * sizeof(Cand), hipMemcpyHostToDevice, sh->stream));
-            HIP_TRY(hipMemcpyAsync(sh->bound.p, b.data(), b.size() * 8, hipMemcpyHostToDevice, sh->stream));
-            HIP_TRY(hipStreamSynchronize(sh->stream));
-        } else if (int rc = index_shard_search(sh, qs, B, kc, mdev[(size_t)s], sh->cand.as<Cand>(),
-                                               sh->bound.as<double>(), sh->stream)) {
-            return rc;
-        }
-        HIP_TRY(hipEventRecord(g->g_ev[(size_t)s], sh->stream));
-    }
-    if (int rc = gather(g, B, kc, &hr_index::cand, &hr_index::bound, g->g_cand, g->g_bound, st)) return rc;
-    HIP_TRY(g->g_kth.ensure((size_t)B * 8));
-    HIP_TRY(g->g_fail.ensure((size_t)B * 4));
-    if (int rc = launch_merge(g->device, g->g_cand.as<Cand>(), g->g_bound.as<double>(), g->G, B, kc, k, s_out, r_out,
-                              g->g_kth.as<double>(), g->g_fail.as<int32_t>(), st))
-        return rc;
-    std::vector<int32_t> fail((size_t)B);
-    std::vector<double> kth((size_t)B);
-    HIP_TRY(hipMemcpyAsync(fail.data(), g->g_fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(kth.data(), g->g_kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    std::vector<int> failed;
-    for (int b = 0; b < B; ++b)
-        if (fail[(size_t)b]) failed.push_back(b);
-    if (failed.empty()) return HR_OK;
+// exact fallback of the queries whose guard failed: every shard re-scans them in collect mode (every
+// row whose approximate score can still reach the k-th exact score), then one more gather + merge;
+// the merged rows overwrite the failed queries' rows of s_out / r_out (primary device, on st)
+static int group_fallback(hr_index* g, const float* q_dev, int k, const std::vector<int>& failed, const double* kth,
+                          const std::vector<const uint64_t*>& mdev, float* s_out, int64_t* r_out, hipStream_t st) {
     g->n_guard_fail += (int64_t)failed.size();
-    // exact fallback: every shard re-scans the failing queries in collect mode (every row whose
-    // approximate score can still reach the k-th exact score), then one more gather + merge
     const int nf = (int)failed.size(), cap = fallback_cap(g->G);
     HIP_TRY(g->fb_q.ensure((size_t)nf * g->dim * 4));
     std::vector<double> kf((size_t)nf);
@@ -388,12 +396,63 @@ static int group_search_impl(hr_index* g, const float* q_dev, int B, int k, cons
     return HR_OK;
 }
 
+
+// exact top-k of B queries (q_dev on the primary, ordered on st) over all shards -> s_out / r_out
+// (primary device), k <= HR_MAX_K; mask_host: the handle's row bitmap or null
+static int group_search_impl(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_host, float* s_out,
+                             int64_t* r_out, hipStream_t st) {
+    const int kc = hr_kc_for_k_dim(k, g->dim);
+    TileListReset reset{g};
+    std::vector<const uint64_t*> mdev;
+    std::vector<std::vector<uint32_t>> words;
+    if (int rc = shard_masks(g, mask_host, mdev, words)) return rc;
+    HIP_TRY(hipSetDevice(g->device));
+    HIP_TRY(hipEventRecord(g->g_ev_q, st));
+    for (int s = 0; s < g->G; ++s) {  // every shard's scan + select + rescore, all devices at once
+        hr_index* sh = g->shards[(size_t)s];
+        if (int rc = set_device(sh)) return rc;
+        HIP_TRY(hipStreamWaitEvent(sh->stream, g->g_ev_q, 0));
+        HIP_TRY(sh->cand.ensure((size_t)B * kc * sizeof(Cand)));
+        HIP_TRY(sh->bound.ensure((size_t)B * 8));
+        const float* qs = nullptr;
+        if (int rc = shard_queries(g, sh, q_dev, B, sh->g_q, &qs)) return rc;
+        if (sh->n_live == 0) {  // nothing here: no candidates, bound -inf
+            std::vector<Cand> c((size_t)B * kc, Cand{-INFINITY, -1});
+            std::vector<double> b((size_t)B, -INFINITY);
+            HIP_TRY(hipMemcpyAsync(sh->cand.p, c.data(), c.size() * sizeof(Cand), hipMemcpyHostToDevice, sh->stream));
+            HIP_TRY(hipMemcpyAsync(sh->bound.p, b.data(), b.size() * 8, hipMemcpyHostToDevice, sh->stream));
+            HIP_TRY(hipStreamSynchronize(sh->stream));
+        } else if (int rc = index_shard_search(sh, qs, B, kc, mdev[(size_t)s], sh->cand.as<Cand>(),
+                                               sh->bound.as<double>(), sh->stream)) {
+            return rc;
+        }
+        HIP_TRY(hipEventRecord(g->g_ev[(size_t)s], sh->stream));
+    }
+    if (int rc = gather(g, B, kc, &hr_index::cand, &hr_index::bound, g->g_cand, g->g_bound, st)) return rc;
+    HIP_TRY(g->g_kth.ensure((size_t)B * 8));
+    HIP_TRY(g->g_fail.ensure((size_t)B * 4));
+    if (int rc = launch_merge(g->device, g->g_cand.as<Cand>(), g->g_bound.as<double>(), g->G, B, kc, k, s_out, r_out,
+                              g->g_kth.as<double>(), g->g_fail.as<int32_t>(), st))
+        return rc;
+    std::vector<int32_t> fail((size_t)B);
+    std::vector<double> kth((size_t)B);
+    HIP_TRY(hipMemcpyAsync(fail.data(), g->g_fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(kth.data(), g->g_kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[(size_t)b]) failed.push_back(b);
+    if (failed.empty()) return HR_OK;
+    return group_fallback(g, q_dev, k, failed, kth.data(), mdev, s_out, r_out, st);
+}
+
 // k > HR_MAX_K: every shard's exhaustive exact top-k, merged on the host (score desc, row asc)
 static int group_exact_all(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_host, Cand* out,
                            hipStream_t st) {
     TileListReset reset{g};
     std::vector<const uint64_t*> mdev;
-    if (int rc = shard_masks(g, mask_host, mdev)) return rc;
+    std::vector<std::vector<uint32_t>> words;
+    if (int rc = shard_masks(g, mask_host, mdev, words)) return rc;
     HIP_TRY(hipSetDevice(g->device));
     HIP_TRY(hipEventRecord(g->g_ev_q, st));
     std::vector<Cand> all((size_t)g->G * B * k);
@@ -425,6 +484,7 @@ static int group_exact_all(hr_index* g, const float* q_dev, int B, int k, const 
 
 int group_search_device(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
                         int64_t* r_out, hipStream_t st) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
     if (k <= 0 || k > HR_MAX_K) return set_err(HR_E_INVALID, "k must be in [1, HR_MAX_K]");
     std::vector<uint64_t> mh;
@@ -437,6 +497,7 @@ int group_search_device(hr_index* g, const float* q_dev, int B, int k, const uin
 }
 
 int group_search_host(hr_index* g, const float* q, int B, int k, const uint64_t* mask, float* s_out, int64_t* r_out) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     refresh_group_totals(g);
     if (g->n_live == 0) {  // empty index: reference returns [] (faiss_store.py:143-144)
         for (int64_t i = 0; i < (int64_t)B * k; ++i) {
@@ -469,10 +530,381 @@ int group_search_host(hr_index* g, const float* q, int B, int k, const uint64_t*
     return HR_OK;
 }
 
+// ---------------------------------------------------------------- pipelined search (submit / finalize)
+// The synchronous group search submits the G shards one after another from the caller's thread and then
+// blocks on the guard flags: ~0.1 ms of host work per shard per batch, so a G = 8 handle spent ~0.9 ms
+// of host time per batch against a ~0.42 ms GPU step (1.25M rows per GPU).  The pipelined form gives
+// every shard a host thread of its own and keeps two batches in flight:
+//   submit   (caller)    records "queries ready" on the caller's stream and hands the batch to the G
+//                        shard threads; returns at once with a ticket;
+//   shard s  (thread s)  waits for the queries (peer copy if its GPU is not the primary), runs the
+//                        pipelined shard search (scan stream + tail stream, two workspaces: batch i's
+//                        select/rescore overlaps batch i+1's scan), copies its B*kc candidates + B
+//                        bounds to the primary and records "shard done"; the LAST shard thread of a
+//                        batch enqueues the merge on the primary's merge stream (waits for every
+//                        shard's event), copies the guard flags to pinned host memory, records "merged";
+//   finalize (caller)    waits for "merged" and reads the flags; a failing query takes the exact
+//                        collect fallback (synchronous, rare) after the shard threads have gone idle.
+// Results are identical to the synchronous path (the same kernels on the same data).
+namespace {
+struct Job {
+    int slot;
+};
+
+struct WorkerQ {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<Job> q;
+    bool stop = false;
+};
+}  // namespace
+
+struct GroupPipe {
+    static constexpr int kSlots = 2;
+    struct Slot {
+        DevBuf cand, bound, kth, fail;                 // primary: gathered candidates, merge outputs
+        std::vector<DevBuf> sh_cand, sh_bound, sh_q;   // per shard (shards off the primary device)
+        int32_t* fail_h = nullptr;                     // pinned guard flags / k-th exact scores
+        double* kth_h = nullptr;
+        int cap_B = 0;
+        hipEvent_t q_ready = nullptr, merged = nullptr;
+        std::vector<hipEvent_t> sh_done, sh_q_ready;   // per shard, on the shard's device
+        // the batch in flight
+        bool busy = false;
+        int64_t ticket = 0;
+        const float* q = nullptr;
+        int B = 0, k = 0, kc = 0;
+        float* s_out = nullptr;
+        int64_t* r_out = nullptr;
+        int pending = 0;                               // shard threads still enqueuing this batch
+        int err = HR_OK;
+        std::string errmsg;
+    } slot[kSlots];
+    std::vector<std::thread> workers;
+    std::vector<std::unique_ptr<WorkerQ>> qs;
+    std::vector<hipStream_t> tail;                     // per shard: select + rescore + candidate copy
+    hipStream_t merge = nullptr;                       // primary: merge + flag copy
+    std::mutex m;                                      // slot state (pending / err)
+    std::condition_variable cv;
+    int next = 0;
+    int64_t next_ticket = 1;
+    // host time (diagnostics, hr_index_host_us): caller submit, shard-thread enqueue per batch
+    double submit_us = 0.0, shard_us_max = 0.0;
+    int64_t batches = 0;
+    std::vector<double> shard_us;
+};
+
+static int pipe_merge(hr_index* g, GroupPipe::Slot& sl) {
+    GroupPipe* p = g->pipe;
+    HIP_TRY(hipSetDevice(g->device));
+    for (int s = 0; s < g->G; ++s) HIP_TRY(hipStreamWaitEvent(p->merge, sl.sh_done[(size_t)s], 0));
+    HIP_TRY(hipStreamWaitEvent(p->merge, sl.q_ready, 0));  // s_out / r_out: after the caller's earlier work
+    if (int rc = launch_merge(g->device, sl.cand.as<Cand>(), sl.bound.as<double>(), g->G, sl.B, sl.kc, sl.k, sl.s_out,
+                              sl.r_out, sl.kth.as<double>(), sl.fail.as<int32_t>(), p->merge))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(sl.fail_h, sl.fail.p, (size_t)sl.B * 4, hipMemcpyDeviceToHost, p->merge));
+    HIP_TRY(hipMemcpyAsync(sl.kth_h, sl.kth.p, (size_t)sl.B * 8, hipMemcpyDeviceToHost, p->merge));
+    HIP_TRY(hipEventRecord(sl.merged, p->merge));
+    return HR_OK;
+}
+
+// shard s's part of the batch in slot `si` (runs on shard thread s)
+static int pipe_shard(hr_index* g, int s, GroupPipe::Slot& sl) {
+    GroupPipe* p = g->pipe;
+    hr_index* sh = g->shards[(size_t)s];
+    if (int rc = set_device(sh)) return rc;
+    const bool local = sh->device == g->device;
+    const size_t cb = (size_t)sl.B * sl.kc * sizeof(Cand);
+    Cand* cand = local ? sl.cand.as<Cand>() + (size_t)s * sl.B * sl.kc : nullptr;
+    double* bound = local ? sl.bound.as<double>() + (size_t)s * sl.B : nullptr;
+    if (!local) {
+        HIP_TRY(sl.sh_cand[(size_t)s].ensure(cb));
+        HIP_TRY(sl.sh_bound[(size_t)s].ensure((size_t)sl.B * 8));
+        cand = sl.sh_cand[(size_t)s].as<Cand>();
+        bound = sl.sh_bound[(size_t)s].as<double>();
+    }
+    hipStream_t tail = p->tail[(size_t)s];
+    if (sh->n_live == 0) {  // nothing here: no candidates, bound -inf (tail stream, after the queries)
+        std::vector<Cand> c((size_t)sl.B * sl.kc, Cand{-INFINITY, -1});
+        std::vector<double> b((size_t)sl.B, -INFINITY);
+        HIP_TRY(hipStreamWaitEvent(tail, sl.q_ready, 0));
+        HIP_TRY(hipMemcpyAsync(cand, c.data(), cb, hipMemcpyHostToDevice, tail));
+        HIP_TRY(hipMemcpyAsync(bound, b.data(), (size_t)sl.B * 8, hipMemcpyHostToDevice, tail));
+        HIP_TRY(hipStreamSynchronize(tail));  // (pageable staging; an empty shard is rare)
+    } else {
+        const float* qs = sl.q;
+        hipEvent_t ready = sl.q_ready;
+        if (!local) {  // the queries over xGMI onto this shard's device
+            HIP_TRY(sl.sh_q[(size_t)s].ensure((size_t)sl.B * g->dim * 4));
+            HIP_TRY(hipStreamWaitEvent(sh->stream, sl.q_ready, 0));
+            HIP_TRY(hipMemcpyPeerAsync(sl.sh_q[(size_t)s].p, sh->device, sl.q, g->device, (size_t)sl.B * g->dim * 4,
+                                       sh->stream));
+            HIP_TRY(hipEventRecord(sl.sh_q_ready[(size_t)s], sh->stream));
+            qs = sl.sh_q[(size_t)s].as<float>();
+            ready = sl.sh_q_ready[(size_t)s];
+        } else if (hipEventQuery(ready) != hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(sh->stream, ready, 0));  // the scan stream's prep reads them
+        }
+        if (int rc = index_shard_search_async(sh, qs, sl.B, sl.kc, cand, bound, sh->stream, tail, ready)) return rc;
+        if (!local) {
+            HIP_TRY(hipMemcpyPeerAsync(sl.cand.as<Cand>() + (size_t)s * sl.B * sl.kc, g->device, cand, sh->device, cb,
+                                       tail));
+            HIP_TRY(hipMemcpyPeerAsync(sl.bound.as<double>() + (size_t)s * sl.B, g->device, bound, sh->device,
+                                       (size_t)sl.B * 8, tail));
+        }
+    }
+    HIP_TRY(hipEventRecord(sl.sh_done[(size_t)s], tail));
+    return HR_OK;
+}
+
+static void pipe_worker(hr_index* g, int s) {
+    GroupPipe* p = g->pipe;
+    WorkerQ& wq = *p->qs[(size_t)s];
+    for (;;) {
+        Job job;
+        {
+            std::unique_lock<std::mutex> lk(wq.m);
+            wq.cv.wait(lk, [&] { return wq.stop || !wq.q.empty(); });
+            if (wq.q.empty()) return;  // stop
+            job = wq.q.front();
+            wq.q.pop_front();
+        }
+        GroupPipe::Slot& sl = p->slot[job.slot];
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc = pipe_shard(g, s, sl);
+        std::string msg = rc ? hr_last_error() : std::string();
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        bool last = false;
+        {
+            std::lock_guard<std::mutex> lk(p->m);
+            p->shard_us[(size_t)s] += us;
+            if (rc && sl.err == HR_OK) {
+                sl.err = rc;
+                sl.errmsg = msg;
+            }
+            last = --sl.pending == 0;
+        }
+        if (last) {  // every shard has enqueued its part: the merge goes behind all of them
+            int mrc = HR_OK;
+            std::string mmsg;
+            bool ok;
+            {
+                std::lock_guard<std::mutex> lk(p->m);
+                ok = sl.err == HR_OK;
+            }
+            if (ok && (mrc = pipe_merge(g, sl)) != HR_OK) mmsg = hr_last_error();
+            std::lock_guard<std::mutex> lk(p->m);
+            if (mrc && sl.err == HR_OK) {
+                sl.err = mrc;
+                sl.errmsg = mmsg;
+            }
+            sl.pending = -1;  // merged (or failed): finalize may proceed
+            p->cv.notify_all();
+        }
+    }
+}
+
+static void pipe_stop(hr_index* g) {
+    GroupPipe* p = g->pipe;
+    if (!p) return;
+    for (auto& q : p->qs) {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->stop = true;
+        q->cv.notify_all();
+    }
+    for (auto& t : p->workers)
+        if (t.joinable()) t.join();
+    for (int i = 0; i < GroupPipe::kSlots; ++i) {
+        GroupPipe::Slot& sl = p->slot[i];
+        (void)hipSetDevice(g->device);
+        if (sl.merged) (void)hipEventSynchronize(sl.merged);
+        for (DevBuf* b : {&sl.cand, &sl.bound, &sl.kth, &sl.fail}) b->release();
+        if (sl.fail_h) (void)hipHostFree(sl.fail_h);
+        if (sl.kth_h) (void)hipHostFree(sl.kth_h);
+        if (sl.q_ready) (void)hipEventDestroy(sl.q_ready);
+        if (sl.merged) (void)hipEventDestroy(sl.merged);
+        for (int s = 0; s < g->G; ++s) {
+            (void)hipSetDevice(g->shards[(size_t)s]->device);
+            if (sl.sh_done[(size_t)s]) (void)hipEventSynchronize(sl.sh_done[(size_t)s]);
+            sl.sh_cand[(size_t)s].release();
+            sl.sh_bound[(size_t)s].release();
+            sl.sh_q[(size_t)s].release();
+            if (sl.sh_done[(size_t)s]) (void)hipEventDestroy(sl.sh_done[(size_t)s]);
+            if (sl.sh_q_ready[(size_t)s]) (void)hipEventDestroy(sl.sh_q_ready[(size_t)s]);
+        }
+    }
+    for (int s = 0; s < g->G; ++s) {
+        (void)hipSetDevice(g->shards[(size_t)s]->device);
+        if (p->tail[(size_t)s]) (void)hipStreamDestroy(p->tail[(size_t)s]);
+    }
+    (void)hipSetDevice(g->device);
+    if (p->merge) (void)hipStreamDestroy(p->merge);
+    delete p;
+    g->pipe = nullptr;
+}
+
+static int pipe_start(hr_index* g) {
+    if (g->pipe) return HR_OK;
+    GroupPipe* p = new GroupPipe();
+    g->pipe = p;
+    const int G = g->G;
+    p->tail.assign((size_t)G, nullptr);
+    p->shard_us.assign((size_t)G, 0.0);
+    for (int i = 0; i < GroupPipe::kSlots; ++i) {
+        GroupPipe::Slot& sl = p->slot[i];
+        sl.sh_cand.resize((size_t)G);
+        sl.sh_bound.resize((size_t)G);
+        sl.sh_q.resize((size_t)G);
+        sl.sh_done.assign((size_t)G, nullptr);
+        sl.sh_q_ready.assign((size_t)G, nullptr);
+    }
+    auto fail = [&](hipError_t e) {
+        pipe_stop(g);
+        return set_err(HR_E_HIP, std::string("group pipeline: ") + hipGetErrorString(e));
+    };
+    hipError_t e = hipSuccess;
+    for (int s = 0; s < G && e == hipSuccess; ++s) {
+        e = hipSetDevice(g->shards[(size_t)s]->device);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->tail[(size_t)s], hipStreamNonBlocking);
+        for (int i = 0; i < GroupPipe::kSlots && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&p->slot[i].sh_done[(size_t)s], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&p->slot[i].sh_q_ready[(size_t)s], hipEventDisableTiming);
+        }
+    }
+    if (e == hipSuccess) e = hipSetDevice(g->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->merge, hipStreamNonBlocking);
+    for (int i = 0; i < GroupPipe::kSlots && e == hipSuccess; ++i) {
+        e = hipEventCreateWithFlags(&p->slot[i].q_ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->slot[i].merged, hipEventDisableTiming);
+    }
+    if (e != hipSuccess) return fail(e);
+    for (int s = 0; s < G; ++s) p->qs.emplace_back(new WorkerQ());
+    for (int s = 0; s < G; ++s) p->workers.emplace_back(pipe_worker, g, s);
+    return HR_OK;
+}
+
+// wait until slot si's shard threads have enqueued everything (merge included); returns its error
+static int pipe_wait_enqueued(GroupPipe* p, GroupPipe::Slot& sl) {
+    std::unique_lock<std::mutex> lk(p->m);
+    p->cv.wait(lk, [&] { return sl.pending < 0; });
+    if (sl.err != HR_OK) return set_err(sl.err, sl.errmsg);
+    return HR_OK;
+}
+
+static int pipe_finalize_slot(hr_index* g, GroupPipe::Slot& sl) {
+    GroupPipe* p = g->pipe;
+    struct Done {
+        GroupPipe::Slot& sl;
+        ~Done() { sl.busy = false; }
+    } done{sl};
+    if (int rc = pipe_wait_enqueued(p, sl)) return rc;
+    HIP_TRY(hipSetDevice(g->device));
+    HIP_TRY(hipEventSynchronize(sl.merged));
+    std::vector<int> failed;
+    for (int b = 0; b < sl.B; ++b)
+        if (sl.fail_h[b]) failed.push_back(b);
+    if (failed.empty()) return HR_OK;
+    // the fallback drives the shards from this thread: every shard thread must be idle first
+    for (auto& o : p->slot)
+        if (o.busy && &o != &sl)
+            if (int rc = pipe_wait_enqueued(p, o)) return rc;
+    std::vector<const uint64_t*> mdev((size_t)g->G, nullptr);
+    const int rc = group_fallback(g, sl.q, sl.k, failed, sl.kth_h, mdev, sl.s_out, sl.r_out, p->merge);
+    return rc;
+}
+
+int group_drain(hr_index* g) {
+    GroupPipe* p = g->pipe;
+    if (!p) return HR_OK;
+    int first_rc = HR_OK;
+    for (int i = 0; i < GroupPipe::kSlots; ++i) {  // oldest first
+        GroupPipe::Slot& sl = p->slot[(p->next + i) % GroupPipe::kSlots];
+        if (!sl.busy) continue;
+        const int rc = pipe_finalize_slot(g, sl);
+        if (rc && first_rc == HR_OK) first_rc = rc;
+    }
+    return first_rc;
+}
+
+int group_search_submit(hr_index* g, const float* q_dev, int B, int k, float* s_out, int64_t* r_out, hipStream_t st,
+                        int64_t* ticket) {
+    if (int rc = pipe_start(g)) return rc;
+    GroupPipe* p = g->pipe;
+    GroupPipe::Slot& sl = p->slot[p->next];
+    if (sl.busy)  // the slot's previous batch (two submits ago) is finalized first
+        if (int rc = pipe_finalize_slot(g, sl)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();  // host work of this submit (not the wait above)
+    p->next = (p->next + 1) % GroupPipe::kSlots;
+    refresh_group_totals(g);
+    const int kc = hr_kc_for_k_dim(k, g->dim);
+    HIP_TRY(hipSetDevice(g->device));
+    if (B > sl.cap_B) {
+        if (sl.fail_h) HIP_TRY(hipHostFree(sl.fail_h));
+        if (sl.kth_h) HIP_TRY(hipHostFree(sl.kth_h));
+        sl.fail_h = nullptr;
+        sl.kth_h = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&sl.fail_h, (size_t)B * 4));
+        HIP_TRY(hipHostMalloc((void**)&sl.kth_h, (size_t)B * 8));
+        sl.cap_B = B;
+    }
+    HIP_TRY(sl.cand.ensure((size_t)g->G * B * kc * sizeof(Cand)));
+    HIP_TRY(sl.bound.ensure((size_t)g->G * B * 8));
+    HIP_TRY(sl.kth.ensure((size_t)B * 8));
+    HIP_TRY(sl.fail.ensure((size_t)B * 4));
+    HIP_TRY(hipEventRecord(sl.q_ready, st));
+    sl.q = q_dev;
+    sl.B = B;
+    sl.k = k;
+    sl.kc = kc;
+    sl.s_out = s_out;
+    sl.r_out = r_out;
+    sl.err = HR_OK;
+    sl.errmsg.clear();
+    sl.ticket = p->next_ticket++;
+    {
+        std::lock_guard<std::mutex> lk(p->m);
+        sl.pending = g->G;
+    }
+    sl.busy = true;
+    const int si = (int)(&sl - p->slot);
+    for (int s = 0; s < g->G; ++s) {
+        WorkerQ& wq = *p->qs[(size_t)s];
+        std::lock_guard<std::mutex> lk(wq.m);
+        wq.q.push_back(Job{si});
+        wq.cv.notify_one();
+    }
+    *ticket = sl.ticket;
+    p->batches++;
+    p->submit_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    return HR_OK;
+}
+
+int group_search_finalize(hr_index* g, int64_t ticket) {
+    GroupPipe* p = g->pipe;
+    if (!p || ticket <= 0) return HR_OK;
+    for (auto& sl : p->slot)
+        if (sl.busy && sl.ticket == ticket) return pipe_finalize_slot(g, sl);
+    return HR_OK;  // finalized already (by a later submit or a drain)
+}
+
+int group_host_us(hr_index* g, double out[3]) {
+    GroupPipe* p = g->pipe;
+    out[0] = out[1] = out[2] = 0.0;
+    if (!p || !p->batches) return HR_OK;
+    std::lock_guard<std::mutex> lk(p->m);
+    out[0] = p->submit_us / (double)p->batches;
+    double mx = 0.0;
+    for (double u : p->shard_us) mx = std::max(mx, u);
+    out[1] = mx / (double)p->batches;
+    out[2] = (double)p->batches;
+    return HR_OK;
+}
+
 // ---------------------------------------------------------------- persistence
 // The file is the single-index layout (header, handle tiles in order with the slot swizzle of the
 // handle tile, live words): written / read in blocks of handle tiles, re-swizzled on the host.
 int group_save(hr_index* g, const char* path) {
+    if (int rc = group_drain(g)) return rc;  // batches in flight first (they read the rows)
     refresh_group_totals(g);
     const std::string tmp_path = std::string(path) + ".tmp";
     FILE* f = std::fopen(tmp_path.c_str(), "wb");

@@ -1128,6 +1128,36 @@ extern "C" int hr_index_search_device(hr_index* h, const float* q_dev, int B, in
     return search_device_impl(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
 }
 
+// Pipelined search (include/hiprag.h): a group handle keeps two batches in flight, every shard
+// submitted by its own host thread (hr_group.hip); a single-device handle runs the batch at once
+// (ticket 0; ShardedSearch pipelines single-device shards from Python).
+extern "C" int hr_index_search_submit(hr_index* h, const float* q_dev, int B, int k, float* scores_out_dev,
+                                      int64_t* rows_out_dev, void* stream, int64_t* ticket_out) {
+    if (!h || !q_dev || !scores_out_dev || !rows_out_dev || !ticket_out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = set_device(h)) return rc;
+    if (int rc = validate_search(h, B, k)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    *ticket_out = 0;
+    if (h->G > 1) return group_search_submit(h, q_dev, B, k, scores_out_dev, rows_out_dev, st, ticket_out);
+    return search_device_impl(h, q_dev, B, k, nullptr, scores_out_dev, rows_out_dev, st);
+}
+
+extern "C" int hr_index_search_finalize(hr_index* h, int64_t ticket) {
+    if (!h) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return group_search_finalize(h, ticket);
+    return HR_OK;
+}
+
+extern "C" int hr_index_host_us(hr_index* h, double* out) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return group_host_us(h, out);
+    out[0] = out[1] = out[2] = 0.0;
+    return HR_OK;
+}
+
 // top-k beyond HR_MAX_K (Chroma's n_results has no cap, chroma_store.py:118-120): the exhaustive
 // exact pass per query -- canonical fp64 score of every live, allowed row + stable radix sort,
 // the same arithmetic and (score desc, row asc) order as the scan path -- into host records
@@ -1261,6 +1291,11 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
 int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
                        double* bound_out, hipStream_t st) {
     return shard_search(h, q_dev, B, kc, mask_dev, 0, cand_out, bound_out, st, st);
+}
+
+int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, Cand* cand_out, double* bound_out,
+                             hipStream_t st, hipStream_t st_tail, hipEvent_t q_ready) {
+    return shard_search(h, q_dev, B, kc, nullptr, 0, cand_out, bound_out, st, st_tail, q_ready);
 }
 
 int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,

@@ -180,6 +180,8 @@ struct hr_index {
     DevBuf s_mask;                    // shard of a group: this shard's words of the caller's row mask
     std::vector<hipEvent_t> g_ev;     // group: one per shard (shard stream -> primary stream)
     hipEvent_t g_ev_q = nullptr;      // group: queries ready on the primary stream
+    std::vector<char> g_peer;         // group: shard s's device has peer access with the primary
+    struct GroupPipe* pipe = nullptr; // group: pipelined search (submit / finalize, hr_group.hip)
 };
 
 // group-handle entry points (hr_group.hip); each public hr_index_* call forwards here when h->G > 1
@@ -194,6 +196,13 @@ int group_search_host(hr_index* g, const float* q, int B, int k, const uint64_t*
 int group_search_device(hr_index* g, const float* q_dev, int B, int k, const uint64_t* mask_dev, float* s_out,
                         int64_t* r_out, hipStream_t st);
 int group_get_rows(hr_index* g, const int64_t* rows, int64_t n, float* out);
+// pipelined group search: enqueue a batch (every shard submitted by its own host thread), finalize =
+// wait for its guard flags and run the exact fallback; group_drain finalizes everything in flight
+int group_search_submit(hr_index* g, const float* q_dev, int B, int k, float* s_out, int64_t* r_out, hipStream_t st,
+                        int64_t* ticket);
+int group_search_finalize(hr_index* g, int64_t ticket);
+int group_drain(hr_index* g);
+int group_host_us(hr_index* g, double out[3]);
 int group_save(hr_index* g, const char* path);
 int group_load_into(hr_index* g, FILE* f, int64_t n, int64_t n_live, double max_norm2);
 void group_stats(hr_index* g, int64_t out[3]);
@@ -210,6 +219,10 @@ int index_finish_load(hr_index* h);
 // candidates (global rows) + bounds into cand_out / bound_out on `st`
 int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
                        double* bound_out, hipStream_t st);
+// the same, pipelined: scan on st, select + rescore on st_tail (outputs ready in st_tail order), the
+// queries ready once q_ready completes (see hr_index_search_shard_async_ev)
+int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, Cand* cand_out, double* bound_out,
+                             hipStream_t st, hipStream_t st_tail, hipEvent_t q_ready);
 int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,
                         const uint64_t* mask_dev, Cand* cand_out, double* bound_out, hipStream_t st);
 int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, Cand* out_host,

@@ -44,6 +44,7 @@ EXPORTS = [
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_kc_for_k_dim",
+    "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us",
 ]
 
 _lib = None
@@ -84,6 +85,9 @@ def load_library(path: str | None = None):
             "hr_index_remove": [vp, vp, i64],
             "hr_index_search": [vp, vp, i32, i32, vp, vp, vp],
             "hr_index_search_device": [vp, vp, i32, i32, vp, vp, vp, vp],
+            "hr_index_search_submit": [vp, vp, i32, i32, vp, vp, vp, vp],
+            "hr_index_search_finalize": [vp, i64],
+            "hr_index_host_us": [vp, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
@@ -263,6 +267,26 @@ class NativeIndex:
         _check(self.lib.hr_index_search_device(self._h, ctypes.c_void_p(q_ptr), int(B), int(k),
                                                ctypes.c_void_p(mask_ptr or None), ctypes.c_void_p(scores_ptr),
                                                ctypes.c_void_p(rows_ptr), ctypes.c_void_p(stream or None)))
+
+    def search_submit(self, q_ptr: int, B: int, k: int, scores_ptr: int, rows_ptr: int, stream: int = 0) -> int:
+        """Pipelined search_device (no mask): enqueue a batch, return its ticket.  A multi-device handle
+        keeps two batches in flight (one host thread per shard); the outputs are final once
+        search_finalize(ticket) returns.  A single-device handle finishes the batch here (ticket 0)."""
+        t = ctypes.c_int64(0)
+        _check(self.lib.hr_index_search_submit(self._h, ctypes.c_void_p(q_ptr), int(B), int(k),
+                                               ctypes.c_void_p(scores_ptr), ctypes.c_void_p(rows_ptr),
+                                               ctypes.c_void_p(stream or None), ctypes.byref(t)))
+        return t.value
+
+    def search_finalize(self, ticket: int) -> None:
+        """Wait for a submitted batch's guard flags and run its exact fallback (no-op if already final)."""
+        _check(self.lib.hr_index_search_finalize(self._h, int(ticket)))
+
+    def host_us(self) -> dict:
+        """Host time of the pipelined search: caller us per submit, busiest shard thread us per batch."""
+        out = (ctypes.c_double * 3)()
+        _check(self.lib.hr_index_host_us(self._h, out))
+        return {"submit_us": out[0], "shard_thread_us": out[1], "batches": int(out[2])}
 
     def search_shard(self, q_ptr: int, B: int, k: int, kc: int, row_offset: int, cand_ptr: int, bound_ptr: int,
                      mask_ptr: int = 0, stream: int = 0, tail_stream: int | None = None,

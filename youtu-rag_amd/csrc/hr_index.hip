@@ -418,6 +418,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
             // static runs and dynamic runs are >= 2 units (the grab is issued one unit early)
             const int64_t s_per = per_wave - std::max<int64_t>(2, per_wave * pct / 100);
             args.dyn_start = s_per * W;
+            args.dyn_pct = pct;
             args.dyn_chunk = std::max(2, chunk_env > 0 ? chunk_env : 2);
             args.dyn_q = sc.dyn_q.as<uint32_t>();
         }
@@ -738,9 +739,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // round-robin units make the chip sweep the tiles in order, so with row parts (k > 32) the last part
     // would keep its SAMPLE-level group maxima until the sweep reaches it, and the threshold (min over all
     // parts) with them: 50M rows at k = 100 then appended 78k candidates per query, overflowed every
-    // private region and sent every query to the collect pass (33.8 ms/batch).  Parts keep contiguous
-    // per-wave ranges, which visit every part from the start.
-    a.strided = strided_env && np == 1;
+    // private region and sent every query to the collect pass (33.8 ms/batch).  So with parts the FILTER
+    // deals in teams (ScanArgs::teams): team p = every np-th wave, dealing part p's tiles round-robin, so
+    // every part is read from the start and each wave stays in its part; over a tile list (units are list
+    // positions, not tiles) parts keep contiguous per-wave ranges, as does the SAMPLE pass.
+    // HIPRAG_PART_TEAMS=0: contiguous ranges for every row-part FILTER (A/B)
+    static const int teams_env = getenv("HIPRAG_PART_TEAMS") ? atoi(getenv("HIPRAG_PART_TEAMS")) : 1;
+    a.strided = strided_env;
+    a.teams = (teams_env && !tl_ptr) ? 1 : 0;
     a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
     // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
     // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->

@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
     if (mkeys && lane < 32)
         for (int p = 0; p < np; ++p) mkeys[((int64_t)p * Bp + b) * 32 + lane] = HR_KEY_NEG_INF;
     if (lane == 0) {
-        if (dyn_q && (b % (QB * 32)) == 0) dyn_q[(b / (QB * 32)) * 16] = 0;  // one counter per query group
+        if (dyn_q && (b % (QB * 32)) == 0)  // per query group: one counter per row-part team (<= 16)
+            for (int p = 0; p < 16; ++p) dyn_q[(b / (QB * 32)) * 16 + p] = 0;
         if (cnt) cnt[b] = 0;
         if (floor_q) floor_q[b] = real ? -__builtin_inff() : __builtin_inff();
     }
@@ -276,6 +277,12 @@ struct ScanArgs {
     int ng;
     int diag_nostore;        // timing diagnostics only (HIPRAG_SCAN_DEBUG & 64): appends skip their stores (wrong results)
     int early_refresh;       // FILTER: a refresh's loads go out before the tile's k-loop (0: in its epilogue; A/B)
+    // FILTER with row parts (np > 1) and round-robin dealing: the waves form np teams, team p (waves with
+    // wr % np == p) deals part p's tiles round-robin among its members with a dynamic tail of its own
+    // (counter dyn_q[p]) -- every wave stays in one part, every part is read from the start, and the chip
+    // reads np windows of consecutive tiles.  0: parts keep contiguous per-wave ranges (tile lists)
+    int teams;
+    int dyn_pct;             // dynamic-tail percentage the host used (teams recompute their split)
     int wide_dbg;            // k_scan_wide timing experiments: 1 = no MFMAs, 2 = no LDS reads either (wrong results)
 };
 
@@ -415,19 +422,35 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         if (a.buf) a.buf += (int64_t)grp * Bq * a.cap;
         if (a.dyn_q) a.dyn_q += grp * 16;
     }
-    const int64_t W = nrb * (blockDim.x >> 6);  // waves per group
+    const int64_t Wg = nrb * (blockDim.x >> 6);  // waves per group
     const int64_t w = rb * (blockDim.x >> 6) + (tid >> 6);  // slot of this wave's outputs within the group
-    const int64_t wg = (int64_t)grp * W + w;                // ... over all groups
+    const int64_t wg = (int64_t)grp * Wg + w;               // ... over all groups
     // unit range: contiguous per wave, numbered wave-major across workgroups so the waves that
     // get one extra unit sit on different CUs (the tail is then one tile per CU, not a
     // handful of fully loaded CUs finishing a tile after everyone else)
-    const int64_t wr = a.wave_major ? (int64_t)(tid >> 6) * nrb + rb : w;
-    const bool dyn = MODE == SCAN_FILTER && a.dyn_start < a.n_units;  // launch-uniform
-    const int64_t n_static = dyn ? a.dyn_start : a.n_units;
+    const int64_t wrg = a.wave_major ? (int64_t)(tid >> 6) * nrb + rb : w;
+    // teams (FILTER, row parts, round-robin dealing; ScanArgs::teams): this wave deals part tp's tiles
+    // [t_off, t_off + n_units) with the other Wt waves of its team; every index below is team-local
+    const bool teams = MODE == SCAN_FILTER && a.np > 1 && a.teams && a.strided;
+    const int tp = teams ? (int)(wrg % a.np) : 0;
+    const int64_t W = teams ? (Wg - tp + a.np - 1) / a.np : Wg;
+    const int64_t wr = teams ? wrg / a.np : wrg;
+    const int64_t t_off = teams ? (int64_t)tp * a.part_tiles : 0;
+    const int64_t n_units = teams ? std::max<int64_t>(0, std::min<int64_t>(a.n_units - t_off, a.part_tiles)) : a.n_units;
+    int64_t dyn_start = a.dyn_start;
+    if (teams) {  // the host's split recomputed for this team's share (static runs >= 8 units or no tail)
+        const int64_t per_wave = n_units / W;
+        dyn_start = n_units;
+        if (a.dyn_start < a.n_units && per_wave >= 8)
+            dyn_start = (per_wave - std::max<int64_t>(2, per_wave * a.dyn_pct / 100)) * W;
+    }
+    uint32_t* const dyn_ctr = a.dyn_q ? a.dyn_q + tp : nullptr;
+    const bool dyn = MODE == SCAN_FILTER && dyn_start < n_units;  // team-uniform
+    const int64_t n_static = dyn ? dyn_start : n_units;
     // static units: a contiguous range per wave, or (strided) every W-th unit from wr, so that at any
     // moment the chip's waves read one window of consecutive tiles; u then counts the wave's own units
     const int64_t base = n_static / W, rem = n_static % W;
-    const bool strided = a.strided != 0;
+    const bool strided = a.strided != 0 && (a.np == 1 || teams);
     const int64_t u0 = strided ? 0 : wr * base + (wr < rem ? wr : rem);
     const int64_t u1 = strided ? (wr < n_static ? (n_static - 1 - wr) / W + 1 : 0) : u0 + base + (wr < rem ? 1 : 0);
     const int64_t stride = FILTER ? 1 : a.sample_stride;
@@ -454,7 +477,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
             }
             u = u * W + pos;
         }
-        const int64_t i = wave_uniform(u * stride);
+        const int64_t i = wave_uniform(t_off + u * stride);
         return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };
     const unsigned long long t_entry = a.stamps ? wall_clock64() : 0ull;
@@ -608,13 +631,13 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     // (Reading it at once makes the compiler drain every outstanding load: vmcnt(0).)
     auto grab_issue = [&]() -> uint32_t {
         uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(a.dyn_q, 1u);
+        if (lane == 0) v = atomicAdd(dyn_ctr, 1u);
         return v;
     };
     auto grab_resolve = [&](uint32_t v) -> int64_t {
         v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-        const int64_t u = a.dyn_start + (int64_t)v * a.dyn_chunk;
-        return u < a.n_units ? u : -1;
+        const int64_t u = dyn_start + (int64_t)v * a.dyn_chunk;
+        return u < n_units ? u : -1;
     };
     uint32_t rkey[QB][16];  // group-max keys of the refresh due in the current tile's epilogue
     const bool early_refresh = a.early_refresh != 0;
@@ -625,7 +648,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         in_static = false;
         u = grab_resolve(grab_issue());
         if (u < 0) u = u_end = 0;
-        else u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
+        else u_end = std::min<int64_t>(u + a.dyn_chunk, n_units);
     }
     while (u < u_end) {
         if (dyn && !issued && u + 2 >= u_end) {  // a 1-unit run issues and resolves at once
@@ -804,10 +827,10 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         }
         if (u + 1 < u_end) {
             ++u;
-        } else if (pend >= 0 && done < a.n_units) {  // (done bound: termination even if the counter were corrupt)
+        } else if (pend >= 0 && done < n_units) {  // (done bound: termination even if the counter were corrupt)
             in_static = false;
             u = pend;
-            u_end = std::min<int64_t>(u + a.dyn_chunk, a.n_units);
+            u_end = std::min<int64_t>(u + a.dyn_chunk, n_units);
             pend = -1;
             issued = false;
         } else {

@@ -102,6 +102,18 @@ int hr_index_search_device(hr_index* h, const float* q_dev, int B, int k, const 
 int hr_index_search_submit(hr_index* h, const float* q_dev, int B, int k, float* scores_out_dev, int64_t* rows_out_dev,
                            void* stream, int64_t* ticket_out);
 int hr_index_search_finalize(hr_index* h, int64_t ticket);
+/* Asynchronous search of host queries on a single-device handle (the drop-in store's micro-batcher on
+ * an asyncio event loop; VectorRetriever.retrieve's store.search, base_retriever.py:58-63): copies the B
+ * queries to pinned staging, enqueues the whole pass (query copy, prep, SAMPLE, FILTER, select, rescore,
+ * merge, results + guard flags back to pinned memory) and returns a ticket without waiting.  When the
+ * batch's results are in host memory a host function writes an 8-byte 1 to notify_fd (an eventfd the
+ * caller polls; -1: none).  hr_index_search_collect(ticket) then copies the scores / rows out (after
+ * running the exact fallback for queries that need it, synchronously).  At most two batches are in
+ * flight (a third submit fails with HR_E_INVALID until one is collected); adds, removes and reserve wait
+ * for batches in flight first.  No row mask; 1 <= k <= HR_MAX_K; an empty index or a multi-device handle
+ * returns HR_E_UNSUPPORTED (use hr_index_search). */
+int hr_index_search_submit_host(hr_index* h, const float* q, int B, int k, int notify_fd, int64_t* ticket_out);
+int hr_index_search_collect(hr_index* h, int64_t ticket, float* scores_out, int64_t* rows_out);
 /* Diagnostics of the pipelined search: out[0] = caller host time per submit (us), out[1] = host time
  * per batch of the busiest shard thread (us), out[2] = batches submitted. */
 int hr_index_host_us(hr_index* h, double* out);

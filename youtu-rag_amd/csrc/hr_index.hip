@@ -10,6 +10,8 @@ int set_err(int code, const std::string& msg) {
     return code;
 }
 
+static int async_drain(hr_index* h);
+
 // ---------------------------------------------------------------- create / grow
 extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
     if (!out) return set_err(HR_E_INVALID, "out is null");
@@ -87,6 +89,7 @@ int index_grow(hr_index* h, int64_t need_rows) {
 extern "C" int hr_index_reserve(hr_index* h, int64_t capacity_rows) {
     if (!h || capacity_rows < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->G > 1) return group_reserve(h, capacity_rows);
     if (int rc = set_device(h)) return rc;
     return index_grow(h, capacity_rows);
@@ -176,6 +179,7 @@ static int64_t max_rows(const hr_index* h) { return (((int64_t)1 << 32) - 64) * 
 extern "C" int hr_index_add(hr_index* h, const float* rows, int64_t n, int64_t* first_row_out) {
     if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
@@ -189,6 +193,7 @@ extern "C" int hr_index_add_synthetic(hr_index* h, uint64_t seed, int64_t global
                                       int64_t* first_row_out) {
     if (!h || n < 0 || global_row0 < 0) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
@@ -202,6 +207,7 @@ extern "C" int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_
                                       int64_t n_rows_after, void* stream) {
     if (!h || n < 0 || (n > 0 && (!rows_dev || !dest_dev))) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "explicit row placement (IVF lists) needs a single-device index");
     if (n_rows_after < h->n || n_rows_after > ((int64_t)1 << 32) - 64)
         return set_err(HR_E_INVALID, "n_rows_after must be >= the current size and < 2^32");
@@ -251,6 +257,7 @@ extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n
                                    void* stream) {
     if (!h || n < 0 || (n > 0 && !rows_dev)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->n + n > max_rows(h)) return set_err(HR_E_INVALID, "a shard holds at most 2^32 rows");
     if (n == 0) {
         if (first_row_out) *first_row_out = h->n;
@@ -272,6 +279,7 @@ extern "C" int hr_index_add_device(hr_index* h, const float* rows_dev, int64_t n
 extern "C" int hr_index_remove(hr_index* h, const int64_t* rows, int64_t n) {
     if (!h || n < 0 || (n > 0 && !rows)) return set_err(HR_E_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = async_drain(h)) return rc;  // asynchronous batches in flight read the rows
     if (h->G > 1) return group_remove(h, rows, n);
     return index_remove_local(h, rows, n);
 }
@@ -1156,6 +1164,117 @@ extern "C" int hr_index_search_finalize(hr_index* h, int64_t ticket) {
     return HR_OK;
 }
 
+// ---- asynchronous host-query search (the drop-in store's event loop; include/hiprag.h)
+static void notify_fd(void* p) {  // host function on the tail stream: one completion to the caller's eventfd
+    const int fd = (int)(intptr_t)p;
+    const uint64_t one = 1;
+    ssize_t w = write(fd, &one, sizeof one);
+    (void)w;
+}
+
+// wait (host) for every asynchronous batch in flight: mutations must not run under a scan that reads the
+// rows (a growing corpus is reallocated); the results stay in pinned memory for collect
+static int async_drain(hr_index* h) {
+    for (auto& sl : h->aslot)
+        if (sl.busy && sl.done) HIP_TRY(hipEventSynchronize(sl.done));
+    return HR_OK;
+}
+
+extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, int k, int notify, int64_t* ticket_out) {
+    if (!h || !q || !ticket_out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *ticket_out = 0;
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "asynchronous host search: single-device handles");
+    if (int rc = validate_search(h, B, k)) return rc;
+    if (h->n_live == 0) return set_err(HR_E_UNSUPPORTED, "empty index: use hr_index_search");
+    auto& sl = h->aslot[h->anext];
+    if (sl.busy) return set_err(HR_E_INVALID, "two batches in flight: collect one first");
+    if (int rc = set_device(h)) return rc;
+    if (!h->atail) HIP_TRY(hipStreamCreateWithFlags(&h->atail, hipStreamNonBlocking));
+    if (!h->acopy) HIP_TRY(hipStreamCreateWithFlags(&h->acopy, hipStreamNonBlocking));
+    if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    if (!sl.q_ready) HIP_TRY(hipEventCreateWithFlags(&sl.q_ready, hipEventDisableTiming));
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t qb = (size_t)B * h->dim * 4;
+    sl.off_s = up(qb);
+    sl.off_r = sl.off_s + up((size_t)B * k * 4);
+    sl.off_f = sl.off_r + up((size_t)B * k * 8);
+    sl.off_k = sl.off_f + up((size_t)B * 4);
+    const size_t need = sl.off_k + (size_t)B * 8;
+    if (need > sl.pin_bytes) {
+        if (sl.pin) HIP_TRY(hipHostFree(sl.pin));
+        sl.pin = nullptr;
+        sl.pin_bytes = 0;
+        HIP_TRY(hipHostMalloc((void**)&sl.pin, need));
+        sl.pin_bytes = need;
+    }
+    const int kc = hr_kc_for_k_dim(k, h->dim);
+    HIP_TRY(sl.q.ensure(qb));
+    HIP_TRY(sl.cand.ensure((size_t)B * kc * sizeof(Cand)));
+    HIP_TRY(sl.bound.ensure((size_t)B * 8));
+    HIP_TRY(sl.kth.ensure((size_t)B * 8));
+    HIP_TRY(sl.fail.ensure((size_t)B * 4));
+    HIP_TRY(sl.s.ensure((size_t)B * k * 4));
+    HIP_TRY(sl.r.ensure((size_t)B * k * 8));
+    // queries: host -> pinned -> device on a copy stream of their own, so the early query prep + SAMPLE
+    // (ready by event) need not queue behind the previous batch's FILTER
+    std::memcpy(sl.pin, q, qb);
+    HIP_TRY(hipMemcpyAsync(sl.q.p, sl.pin, qb, hipMemcpyHostToDevice, h->acopy));
+    HIP_TRY(hipEventRecord(sl.q_ready, h->acopy));
+    if (hipEventQuery(sl.q_ready) != hipSuccess) HIP_TRY(hipStreamWaitEvent(h->stream, sl.q_ready, 0));
+    if (int rc = shard_search(h, sl.q.as<float>(), B, kc, nullptr, 0, sl.cand.as<Cand>(), sl.bound.as<double>(),
+                              h->stream, h->atail, sl.q_ready))
+        return rc;
+    if (int rc = launch_merge(h->device, sl.cand.as<Cand>(), sl.bound.as<double>(), 1, B, kc, k, sl.s.as<float>(),
+                              sl.r.as<int64_t>(), sl.kth.as<double>(), sl.fail.as<int32_t>(), h->atail))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_s, sl.s.p, (size_t)B * k * 4, hipMemcpyDeviceToHost, h->atail));
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_r, sl.r.p, (size_t)B * k * 8, hipMemcpyDeviceToHost, h->atail));
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_f, sl.fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, h->atail));
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_k, sl.kth.p, (size_t)B * 8, hipMemcpyDeviceToHost, h->atail));
+    HIP_TRY(hipEventRecord(sl.done, h->atail));
+    if (notify >= 0) HIP_TRY(hipLaunchHostFunc(h->atail, notify_fd, (void*)(intptr_t)notify));
+    sl.busy = true;
+    sl.B = B;
+    sl.k = k;
+    sl.ticket = h->aticket++;
+    h->anext ^= 1;
+    *ticket_out = sl.ticket;
+    return HR_OK;
+}
+
+extern "C" int hr_index_search_collect(hr_index* h, int64_t ticket, float* scores_out, int64_t* rows_out) {
+    if (!h || !scores_out || !rows_out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    hr_index::AsyncSlot* sp = nullptr;
+    for (auto& sl : h->aslot)
+        if (sl.busy && sl.ticket == ticket) sp = &sl;
+    if (!sp) return set_err(HR_E_INVALID, "unknown or collected ticket");
+    auto& sl = *sp;
+    struct Free {
+        hr_index::AsyncSlot& s;
+        ~Free() { s.busy = false; }
+    } fr{sl};
+    if (int rc = set_device(h)) return rc;
+    HIP_TRY(hipEventSynchronize(sl.done));
+    const int B = sl.B, k = sl.k;
+    const int32_t* fail = (const int32_t*)(sl.pin + sl.off_f);
+    const double* kth = (const double*)(sl.pin + sl.off_k);
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[b]) failed.push_back(b);
+    if (!failed.empty()) {  // the exact collect fallback (rare), synchronous, into the slot's device results
+        if (int rc = search_fallback(h, sl.q.as<float>(), k, nullptr, sl.s.as<float>(), sl.r.as<int64_t>(), failed, kth,
+                                     h->stream))
+            return rc;
+        HIP_TRY(hipMemcpy(sl.pin + sl.off_s, sl.s.p, (size_t)B * k * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(sl.pin + sl.off_r, sl.r.p, (size_t)B * k * 8, hipMemcpyDeviceToHost));
+    }
+    std::memcpy(scores_out, sl.pin + sl.off_s, (size_t)B * k * 4);
+    std::memcpy(rows_out, sl.pin + sl.off_r, (size_t)B * k * 8);
+    return HR_OK;
+}
+
 extern "C" int hr_index_host_us(hr_index* h, double* out) {
     if (!h || !out) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1627,6 +1746,14 @@ extern "C" void hr_index_destroy(hr_index* h) {
             for (auto& x : ev.e) (void)hipEventDestroy(x);
     for (auto& ev : h->ev_pending)
         for (auto& x : ev.e) (void)hipEventDestroy(x);
+    for (auto& sl : h->aslot) {
+        if (sl.pin) (void)hipHostFree(sl.pin);
+        for (DevBuf* b : {&sl.q, &sl.cand, &sl.bound, &sl.kth, &sl.fail, &sl.s, &sl.r}) b->release();
+        if (sl.done) (void)hipEventDestroy(sl.done);
+        if (sl.q_ready) (void)hipEventDestroy(sl.q_ready);
+    }
+    if (h->atail) (void)hipStreamDestroy(h->atail);
+    if (h->acopy) (void)hipStreamDestroy(h->acopy);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->pre) (void)hipStreamDestroy(h->pre);
     delete h;

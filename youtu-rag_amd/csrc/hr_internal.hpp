@@ -168,6 +168,22 @@ struct hr_index {
     size_t pin_bytes = 0;
     DevBuf sync_out;          // device results of the graph path
     int64_t n_graph_replays = 0;
+    // ---- asynchronous host-query search (hr_index_search_submit_host / _collect, hr_index.hip): up to two
+    // batches in flight; each batch's completion is signalled to a file descriptor (an eventfd the caller's
+    // event loop watches) by a host function queued behind its results' copy to pinned memory
+    struct AsyncSlot {
+        bool busy = false;
+        int64_t ticket = 0;
+        int B = 0, k = 0;
+        uint8_t* pin = nullptr;  // pinned: queries in | scores | rows | guard flags | k-th scores out
+        size_t pin_bytes = 0;
+        size_t off_s = 0, off_r = 0, off_f = 0, off_k = 0;
+        DevBuf q, cand, bound, kth, fail, s, r;
+        hipEvent_t q_ready = nullptr, done = nullptr;
+    } aslot[2];
+    int anext = 0;
+    int64_t aticket = 1;
+    hipStream_t acopy = nullptr, atail = nullptr;
     // ---- multi-device handles (hr_index_create with n_dev > 1, hr_group.hip)
     // A group handle owns G shard handles (one per dev_ids entry, repeats allowed) and stripes its
     // rows over them by 32-row tile (stripe_row, hr_common.hpp); it holds no rows itself.  Its

@@ -44,7 +44,8 @@ EXPORTS = [
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_kc_for_k_dim",
-    "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us",
+    "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
+    "hr_index_search_collect",
 ]
 
 _lib = None
@@ -88,6 +89,8 @@ def load_library(path: str | None = None):
             "hr_index_search_submit": [vp, vp, i32, i32, vp, vp, vp, vp],
             "hr_index_search_finalize": [vp, i64],
             "hr_index_host_us": [vp, vp],
+            "hr_index_search_submit_host": [vp, vp, i32, i32, i32, vp],
+            "hr_index_search_collect": [vp, i64, vp, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
@@ -277,6 +280,26 @@ class NativeIndex:
                                                ctypes.c_void_p(scores_ptr), ctypes.c_void_p(rows_ptr),
                                                ctypes.c_void_p(stream or None), ctypes.byref(t)))
         return t.value
+
+    def search_submit_host(self, q: np.ndarray, k: int, notify_fd: int = -1) -> int:
+        """Asynchronous search of host queries (single-device handle, no mask): returns a ticket at once;
+        when the batch's results reach host memory an 8-byte 1 is written to notify_fd (an eventfd).
+        At most two batches in flight.  Raises NotImplementedError where hr_index_search must serve
+        (empty index, multi-device handle)."""
+        q = np.ascontiguousarray(q, np.float32)
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be (B, {self.dim}) float32")
+        t = ctypes.c_int64(0)
+        _check(self.lib.hr_index_search_submit_host(self._h, _ptr(q), q.shape[0], int(k), int(notify_fd),
+                                                    ctypes.byref(t)))
+        return t.value
+
+    def search_collect(self, ticket: int, B: int, k: int) -> tuple[np.ndarray, np.ndarray]:
+        """(scores, rows) of a submitted asynchronous batch (waits if it is not done yet)."""
+        s = np.empty((B, k), np.float32)
+        r = np.empty((B, k), np.int64)
+        _check(self.lib.hr_index_search_collect(self._h, int(ticket), _ptr(s), _ptr(r)))
+        return s, r
 
     def search_finalize(self, ticket: int) -> None:
         """Wait for a submitted batch's guard flags and run its exact fallback (no-op if already final)."""

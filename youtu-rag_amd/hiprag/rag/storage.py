@@ -620,25 +620,47 @@ class HipVectorStore(BaseVectorStore):
             return self._index.search(q, min(top_k, n_live), self.filter_bitmap(filters)), tables
 
     def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
+        """(Chunk, score) lists of a finished batch.  Runs on the event loop while the next launch is in
+        flight, so it is the host's per-hit cost under load: the hits' host records are gathered for the
+        whole batch at once (object-array fancy indexing instead of a Python lookup per row and field) and
+        each Chunk is built straight into its __dict__ (a fresh metadata dict per hit, as Chroma returns)."""
         raw, (recs, metas, epoch) = ran
         n = len(prep[0])
         if raw is None or epoch != self._epoch:  # cleared since the search ran: its rows are gone
             return [[] for _ in range(n)]
         scores, rows = raw
-        rows_l, scores_l = rows.tolist(), scores.tolist()  # Python ints / floats once, not per element
         # the tables the search ran against (append-only; a row deleted since then reads None, dropped)
-        tables = (recs, metas)
-        out = []
-        for b in range(n):
-            valid = [(r, sc) for r, sc in zip(rows_l[b], scores_l[b]) if r >= 0 and recs[r] is not None]
-            embs = None
-            if self.include_embeddings and valid:
-                with self._lock:
-                    if epoch != self._epoch:
-                        return [[] for _ in range(n)]
-                    embs = self._embeddings([r for r, _ in valid])
-            out.append([(self._chunk(r, None if embs is None else embs[i].tolist(), tables), s)
-                        for i, (r, s) in enumerate(valid)])
+        valid = rows >= 0
+        hit_rows = rows[valid]
+        rec_l = recs.a[hit_rows].tolist()
+        meta_l = metas.a[hit_rows].tolist()
+        score_l = scores[valid].tolist()
+        per_q = valid.sum(axis=1).tolist()
+        embs = None
+        if self.include_embeddings and len(hit_rows):
+            keep = [i for i, r in enumerate(rec_l) if r is not None]
+            with self._lock:
+                if epoch != self._epoch:
+                    return [[] for _ in range(n)]
+                e = self._embeddings(hit_rows[keep].tolist())
+            embs = [None] * len(rec_l)
+            for j, i in enumerate(keep):
+                embs[i] = e[j].tolist()
+        new, C = object.__new__, Chunk
+        hits = []
+        for i, (r, m) in enumerate(zip(rec_l, meta_l)):
+            if r is None:
+                hits.append(None)
+                continue
+            c = new(C)
+            c.__dict__ = {"id": r[0], "document_id": m.get("document_id", ""), "content": r[2],
+                          "chunk_index": m.get("chunk_index", 0), "metadata": dict(m),
+                          "embedding": None if embs is None else embs[i]}
+            hits.append((c, score_l[i]))
+        out, at = [], 0
+        for cnt in per_q:
+            out.append([h for h in hits[at:at + cnt] if h is not None])
+            at += cnt
         return out
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None

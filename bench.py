@@ -415,7 +415,7 @@ def main():
     q_ready.record()
     s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
     r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
-    searcher = ShardedSearch(index, start, max_batch=B, device=dev)
+    searcher = ShardedSearch(index, start, max_batch=B, device=dev, max_k=K)
 
     # One step = one batch through the whole path.  Steps are pipelined two deep: submit()
     # enqueues batch i (scan, gather, merge, async copy of the guard flags) and finalizes the

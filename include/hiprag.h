@@ -59,7 +59,8 @@ enum {
     HR_E_HIP = -2,       /* HIP runtime error -> RuntimeError */
     HR_E_UNSUPPORTED = -3,
     HR_E_OVERFLOW = -4,  /* candidate buffer overflow in the exact fallback */
-    HR_E_IO = -5
+    HR_E_IO = -5,
+    HR_E_BUSY = -6       /* hr_index_search_submit_host: another call holds the handle (never waits) */
 };
 
 #define HR_MAX_K 128           /* largest top-k (kb_file_search recall 15 x 3, rerank top-100) */
@@ -110,7 +111,8 @@ int hr_index_search_finalize(hr_index* h, int64_t ticket);
  * caller polls; -1: none).  hr_index_search_collect(ticket) then copies the scores / rows out (after
  * running the exact fallback for queries that need it, synchronously).  At most two batches are in
  * flight (a third submit fails with HR_E_INVALID until one is collected); adds, removes and reserve wait
- * for batches in flight first.  No row mask; 1 <= k <= HR_MAX_K; an empty index or a multi-device handle
+ * for batches in flight first; submit never blocks on the handle: while another call holds it, it returns
+ * HR_E_BUSY at once.  No row mask; 1 <= k <= HR_MAX_K; an empty index or a multi-device handle
  * returns HR_E_UNSUPPORTED (use hr_index_search). */
 int hr_index_search_submit_host(hr_index* h, const float* q, int B, int k, int notify_fd, int64_t* ticket_out);
 int hr_index_search_collect(hr_index* h, int64_t ticket, float* scores_out, int64_t* rows_out);

@@ -68,3 +68,37 @@ class OracleIndex:
             idx = cls(int(z["dim"]), str(z["dtype"]), str(z["metric"]))
             idx.rows, idx.live = z["rows"].copy(), z["live"].copy()
         return idx
+
+
+class AsyncOracleIndex(OracleIndex):
+    """OracleIndex with the asynchronous host-query entry point of NativeIndex (search_submit_host /
+    search_collect): results are computed at submit, and the completion count is written to the caller's
+    eventfd from a timer thread after `delay` seconds -- the GPU's host function, simulated.  At most two
+    batches in flight, like the library."""
+
+    def __init__(self, *a, delay=0.002, **kw):
+        super().__init__(*a, **kw)
+        self.delay, self.tickets, self.next_ticket, self.busy = delay, {}, 1, False
+        self.devices = [0]
+
+    def search_submit_host(self, q, k, notify_fd=-1):
+        import os
+        import threading
+
+        import hiprag._native as N
+
+        if self.busy:
+            raise N.BusyError(N.E_BUSY, "handle busy")
+        if len(self.tickets) >= 2:
+            raise ValueError("two batches in flight: collect one first")
+        if self.live.sum() == 0:
+            raise NotImplementedError("empty index")
+        t = self.next_ticket
+        self.next_ticket += 1
+        self.tickets[t] = self.search(q, k)
+        if notify_fd >= 0:
+            threading.Timer(self.delay, lambda: os.eventfd_write(notify_fd, 1)).start()
+        return t
+
+    def search_collect(self, ticket, B, k):
+        return self.tickets.pop(ticket)

@@ -84,3 +84,51 @@ def test_euclidean_store_vs_oracle(tmp_path, golden_dir):
         res = asyncio.run(store.search(query_embedding=q.tolist(), top_k=5))
         assert [c.id for c, _ in res] == [f"chunk_{x}" for x in r_ref[b]]
         np.testing.assert_array_equal(np.array([s for _, s in res], np.float32), s_ref[b].astype(np.float32))
+
+
+def test_store_native_async_concurrent_vs_oracle(tmp_path):
+    """The reference's call pattern on the device: many concurrent single-query store.search calls
+    (VectorRetriever.retrieve, base_retriever.py:58-63).  Unfiltered batches are launched from the event
+    loop through hr_index_search_submit_host (completion by eventfd, no worker thread); every answer is
+    the oracle's, filtered ones (worker path) too, and a clear with batches in flight resolves them empty."""
+    import oracle
+    from oracle import ref_numpy as R
+
+    rng = np.random.default_rng(21)
+    n, dim = 20_000, 256
+    raw = R.gen_rows(5, 0, n, dim)
+    cfg = VectorStoreConfig(backend="hip", collection_name="asy", persist_directory=str(tmp_path),
+                            index_params={"dtype": "bf16", "persist": False, "max_batch": 32})
+    store = HipVectorStore(cfg)
+    store.add_chunks_sync([Chunk(id=f"c{i}", document_id=f"d{i // 100}", content=str(i), chunk_index=i % 100,
+                                 metadata={"grp": f"g{i % 3}"}, embedding=raw[i].tolist()) for i in range(n)])
+    q = (raw[rng.choice(n, 200, replace=False)] + 300.0 * rng.standard_normal((200, dim))).astype(np.float32)
+    stored = R.process_rows(raw, "cosine", "bf16")
+    s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10)
+    allowed = np.arange(n) % 3 == 1
+    sf_ref, rf_ref = oracle.c_search(stored, "bf16", R.process_queries(q[:40], "cosine"), 5,
+                                     oracle.mask_from_bool(allowed))
+
+    async def main():
+        un = [store.search(query_embedding=x.tolist(), top_k=10) for x in q]
+        fi = [store.search(query_embedding=x.tolist(), top_k=5, filters={"grp": "g1"}) for x in q[:40]]
+        return await asyncio.gather(*un, *fi)
+
+    out = asyncio.run(main())
+    assert store._batcher.native_launches >= 200 // 32
+    for b in range(200):
+        assert [c.id for c, _ in out[b]] == [f"c{r}" for r in r_ref[b]]
+        np.testing.assert_array_equal(np.array([s for _, s in out[b]], np.float32), s_ref[b].astype(np.float32))
+    for b in range(40):
+        assert [c.id for c, _ in out[200 + b]] == [f"c{r}" for r in rf_ref[b]]
+
+    async def clear_mid_flight():
+        tasks = [asyncio.ensure_future(store.search(query_embedding=x.tolist(), top_k=3)) for x in q[:64]]
+        await asyncio.sleep(0)
+        await asyncio.sleep(0)
+        await store.clear()
+        return await asyncio.gather(*tasks)
+
+    res = asyncio.run(clear_mid_flight())
+    assert all(r == [] or len(r) == 3 for r in res)  # finished before the clear, or emptied by it
+    store.close()

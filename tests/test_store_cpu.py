@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from fake_index import OracleIndex
+from fake_index import AsyncOracleIndex, OracleIndex
 from hiprag.rag import Chunk, HipVectorStore, RetrieverConfig, VectorRetriever, VectorStoreConfig
 from hiprag.rag import filters as F
 from hiprag.rag import persist as P
@@ -294,3 +294,69 @@ def test_sibling_collection_files_survive_clear(tmp_path):
     assert {f for f in before if f.startswith("docs.gov.")} <= left
     assert not any(f.startswith("docs.") and not f.startswith("docs.gov.") for f in left)
     assert run(store("docs.gov").count()) == 10
+
+
+
+# ---------------------------------------------------------------- native asynchronous launches (eventfd)
+def make_async_store(tmp_path, **params):
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
+                            index_params={"dtype": "f32", "persist": False, "fsync": False, **params})
+    holder = {}
+
+    def factory(dim):
+        holder["idx"] = AsyncOracleIndex(dim, "f32")
+        return holder["idx"]
+
+    return HipVectorStore(cfg, index_factory=factory), holder
+
+
+def test_native_async_launches_match_sequential(tmp_path):
+    """Unfiltered concurrent searches go through the asynchronous entry point (launched from the event
+    loop, completion by eventfd) and give exactly the sequential answers; filtered ones take the worker
+    path in the same drain."""
+    s, holder = make_async_store(tmp_path, max_batch=16)
+    s.add_chunks_sync(chunks("a", 300) + chunks("b", 200, seed=1))
+    q = np.random.default_rng(11).standard_normal((80, 16)).astype(np.float32)
+    want = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q, 7)]
+    want_f = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q[:8], 5, {"source": "src_b"})]
+
+    async def main():
+        un = [s.search(query_embedding=x.tolist(), top_k=7) for x in q]
+        fi = [s.search(query_embedding=x.tolist(), top_k=5, filters={"source": "src_b"}) for x in q[:8]]
+        return await asyncio.gather(*un, *fi)
+
+    out = run(main())
+    assert [[(c.id, sc) for c, sc in r] for r in out[:80]] == want
+    assert [[(c.id, sc) for c, sc in r] for r in out[80:]] == want_f
+    assert s._batcher.native_launches >= 5  # 80 queries / max_batch 16
+    assert not holder["idx"].tickets       # every native batch collected
+    s.close()
+
+
+def test_native_async_busy_handle_and_clear(tmp_path):
+    """A busy handle sends the batch to the worker path; a clear while native batches are in flight
+    resolves them with no rows (their rows are gone) instead of resolving through the new tables."""
+    s, holder = make_async_store(tmp_path, max_batch=8)
+    s.add_chunks_sync(chunks("a", 100))
+    q = np.random.default_rng(12).standard_normal((16, 16)).astype(np.float32)
+    holder["idx"].busy = True
+
+    async def searches():
+        return await asyncio.gather(*[s.search(query_embedding=x.tolist(), top_k=3) for x in q])
+
+    out = run(searches())
+    assert all(len(r) == 3 for r in out) and s._batcher.native_launches == 0
+    holder["idx"].busy = False
+    holder["idx"].delay = 0.05
+
+    async def clear_mid_flight():
+        tasks = [asyncio.ensure_future(s.search(query_embedding=x.tolist(), top_k=3)) for x in q]
+        await asyncio.sleep(0.01)          # both native batches are in flight
+        await s.clear()
+        await s.add_chunks(chunks("z", 50, seed=3))
+        return await asyncio.gather(*tasks)
+
+    out = run(clear_mid_flight())
+    assert s._batcher.native_launches == 2
+    assert all(r == [] for r in out)
+    s.close()

@@ -78,6 +78,7 @@ def main():
     p.add_argument("--gc-freeze", default="0", help="0/1 list: gc.freeze() after building the store (A/B)")
     p.add_argument("--seconds", type=float, default=3.0)
     p.add_argument("--k", type=int, default=10)
+    p.add_argument("--native-async", default="1", help="0/1 list: event-loop native launches (1) or worker threads (0)")
     args = p.parse_args()
 
     import gc
@@ -99,21 +100,25 @@ def main():
         if fz:
             gc.collect()
             gc.freeze()
-        for depth in (int(x) for x in args.depth.split(",")):
-            for mb in (int(x) for x in args.max_batch.split(",")):
-                st._batcher.max_batch, st._batcher.depth = mb, depth
-                asyncio.run(run_clients(st, queries, 64, 0.5, args.k))  # warm
-                for C in (int(x) for x in args.clients.split(",")):
-                    gc0 = sum(s["collections"] for s in gc.get_stats())
-                    lat, wall, launches = asyncio.run(run_clients(st, queries, C, args.seconds, args.k))
-                    a = np.asarray(lat) * 1e3
-                    print(json.dumps({"rows": args.rows, "max_batch": mb, "depth": depth, "gc_freeze": fz, "clients": C,
-                                      "queries": len(lat), "qps": round(len(lat) / wall, 1),
-                                      "latency_ms_p50": round(float(np.percentile(a, 50)), 3),
-                                      "latency_ms_p99": round(float(np.percentile(a, 99)), 3),
-                                      "launches": launches, "mean_launch_size": round(len(lat) / max(1, launches), 1),
-                                      "gc_collections": sum(s["collections"] for s in gc.get_stats()) - gc0}),
-                          flush=True)
+        for depth, mb, na in ((d, m, a) for d in (int(x) for x in args.depth.split(","))
+                              for m in (int(x) for x in args.max_batch.split(","))
+                              for a in (int(x) for x in args.native_async.split(","))):
+            st._batcher.max_batch, st._batcher.depth, st.native_async = mb, depth, bool(na)
+            asyncio.run(run_clients(st, queries, 64, 0.5, args.k))  # warm
+            for C in (int(x) for x in args.clients.split(",")):
+                gc0 = sum(s["collections"] for s in gc.get_stats())
+                nat0 = st._batcher.native_launches
+                lat, wall, launches = asyncio.run(run_clients(st, queries, C, args.seconds, args.k))
+                a = np.asarray(lat) * 1e3
+                print(json.dumps({"rows": args.rows, "max_batch": mb, "depth": depth, "gc_freeze": fz,
+                                  "native_async": na, "native_launches": st._batcher.native_launches - nat0,
+                                  "clients": C,
+                                  "queries": len(lat), "qps": round(len(lat) / wall, 1),
+                                  "latency_ms_p50": round(float(np.percentile(a, 50)), 3),
+                                  "latency_ms_p99": round(float(np.percentile(a, 99)), 3),
+                                  "launches": launches, "mean_launch_size": round(len(lat) / max(1, launches), 1),
+                                  "gc_collections": sum(s["collections"] for s in gc.get_stats()) - gc0}),
+                      flush=True)
 
 
 if __name__ == "__main__":

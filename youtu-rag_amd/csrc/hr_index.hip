@@ -1182,7 +1182,10 @@ static int async_drain(hr_index* h) {
 
 extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, int k, int notify, int64_t* ticket_out) {
     if (!h || !q || !ticket_out) return set_err(HR_E_INVALID, "null argument");
-    std::lock_guard<std::mutex> lk(h->mu);
+    // never wait for the handle: the caller is an event loop (another call holding it -- an add waiting
+    // for the GPU -- answers HR_E_BUSY and the caller takes its blocking path in a worker thread)
+    std::unique_lock<std::mutex> lk(h->mu, std::try_to_lock);
+    if (!lk.owns_lock()) return set_err(HR_E_BUSY, "handle busy");
     *ticket_out = 0;
     if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "asynchronous host search: single-device handles");
     if (int rc = validate_search(h, B, k)) return rc;

@@ -32,7 +32,7 @@ def kc_for_k(k: int, dim: int = 0) -> int:
 
 CAND_DTYPE = np.dtype([("score", "<f8"), ("row", "<i8")])  # matches hr::Cand
 
-E_INVALID, E_HIP, E_UNSUPPORTED, E_OVERFLOW, E_IO = -1, -2, -3, -4, -5
+E_INVALID, E_HIP, E_UNSUPPORTED, E_OVERFLOW, E_IO, E_BUSY = -1, -2, -3, -4, -5, -6
 
 # every symbol include/hiprag.h declares (checked by tests/test_native_abi.py)
 EXPORTS = [
@@ -56,6 +56,10 @@ class NativeError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"hiprag error {code}: {msg}")
         self.code = code
+
+
+class BusyError(NativeError):
+    """hr_index_search_submit_host found the handle held by another call (it never waits)."""
 
 
 def load_library(path: str | None = None):
@@ -141,6 +145,8 @@ def _check(rc: int):
             raise ValueError(msg)
         if rc == E_UNSUPPORTED:
             raise NotImplementedError(msg)
+        if rc == E_BUSY:
+            raise BusyError(rc, msg)
         raise NativeError(rc, msg)
 
 

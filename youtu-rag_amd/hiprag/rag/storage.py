@@ -49,6 +49,7 @@ import logging
 import os
 import threading
 from array import array
+from collections import deque
 from typing import Any
 
 import numpy as np
@@ -103,16 +104,24 @@ class _ObjColumn:
 class _SearchBatcher:
     """Coalesces concurrent ``search`` calls into batched launches (one per filter group).
 
-    Up to ``depth`` launches are in flight: a worker thread runs only the native search (ctypes drops
-    the GIL), and the Chunk objects are assembled on the event-loop thread while the next launch already
-    runs -- the GPU does not idle during host work, and a worker holding the GIL cannot be starved by a
-    busy event loop (with 1024 clients that convoy cut throughput 4x)."""
+    Up to ``depth`` launches are in flight, and the Chunk objects of a finished batch are assembled on the
+    event-loop thread while the next launch runs.  An unfiltered batch on a single-device index is launched
+    from the event loop itself through the library's asynchronous entry point
+    (hr_index_search_submit_host: the call only enqueues the GPU work and returns); its completion arrives
+    as a count on an eventfd the loop watches (written by a host function behind the batch's results), so
+    no Python thread takes part -- no GIL hand-off between a worker and the loop per launch.  Filtered
+    batches, multi-device handles, and launches that find the handle or the store busy run the blocking
+    search in a worker thread (``asyncio.to_thread``; ctypes drops the GIL)."""
 
     def __init__(self, store: "HipVectorStore", max_batch: int, depth: int = 2):
         self.store, self.max_batch, self.depth = store, max(1, int(max_batch)), max(1, int(depth))
         self.pending: list = []
         self.running = False
-        self.launches = 0  # diagnostics
+        self.launches = 0         # diagnostics
+        self.native_launches = 0  # ... of which through the asynchronous native entry point
+        self.efd = -1             # eventfd of native completions (one count per finished batch)
+        self._native: deque = deque()  # completion futures of native launches, in submission order
+        self._loop = None         # the loop the eventfd reader is registered with
 
     async def search(self, q: np.ndarray, top_k: int, filters):
         dim = self.store.dim
@@ -141,8 +150,56 @@ class _SearchBatcher:
             if not e[4].done():
                 e[4].set_exception(exc)
 
+    # -- native completions
+    def native_fd(self, loop) -> int:
+        """The eventfd native launches signal, its reader registered with `loop` (-1: unavailable)."""
+        if self.efd < 0:
+            if not hasattr(os, "eventfd"):
+                return -1
+            self.efd = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
+        if self._loop is not loop:
+            loop.add_reader(self.efd, self._on_completions)
+            self._loop = loop
+        return self.efd
+
+    def _on_completions(self):
+        try:
+            n = os.eventfd_read(self.efd)
+        except BlockingIOError:
+            return
+        for _ in range(n):  # batches finish in submission order (one stream)
+            if not self._native:
+                break
+            fut = self._native.popleft()
+            if not fut.done():
+                fut.set_result(None)
+
+    def _release_loop(self):
+        if self._loop is not None and not self._native:
+            with contextlib.suppress(Exception):
+                self._loop.remove_reader(self.efd)
+            self._loop = None
+
+    def close(self):
+        self._release_loop()
+        if self.efd >= 0 and not self._native:
+            os.close(self.efd)
+            self.efd = -1
+
+    def _launch(self, loop, prep):
+        """Start one batch: (awaitable, info).  info is None for a worker-thread launch (the awaitable's
+        result is the search), else the native launch to collect once the awaitable resolves."""
+        info = self.store._submit_native(prep, self, loop)
+        if info is not None:
+            fut = loop.create_future()
+            self._native.append(fut)
+            self.native_launches += 1
+            return fut, info
+        return asyncio.ensure_future(asyncio.to_thread(self.store._run_search, prep)), None
+
     async def _drain(self):
-        inflight: dict = {}  # task -> batch
+        loop = asyncio.get_running_loop()
+        inflight: dict = {}  # awaitable -> (batch, prep, native launch info or None)
         batch: list = []
         try:
             while self.pending or inflight:
@@ -153,19 +210,28 @@ class _SearchBatcher:
                         k = max(e[1] for e in batch)
                         self.launches += 1
                         prep = self.store._prep_search(qs, k, batch[0][2])
+                        aw, info = self._launch(loop, prep)
                     except Exception as exc:  # noqa: BLE001 -- this batch's waiters see the failure
                         self._fail(batch, exc)
                         continue
-                    task = asyncio.ensure_future(asyncio.to_thread(self.store._run_search, prep))
-                    inflight[task] = (batch, prep)
+                    inflight[aw] = (batch, prep, info)
                 batch = []
                 if not inflight:
                     continue
                 done, _ = await asyncio.wait(list(inflight), return_when=asyncio.FIRST_COMPLETED)
-                for task in done:
-                    batch, prep = inflight.pop(task)
+                for aw in done:
+                    batch, prep, info = inflight.pop(aw)
                     try:
-                        res = self.store._assemble(prep, task.result())
+                        if info is None:
+                            ran = aw.result()
+                        else:
+                            ran = self.store._collect_native(info, blocking=False)
+                            if ran is None:  # the store is busy (a mutation holds its lock): collect in a worker
+                                t = asyncio.ensure_future(asyncio.to_thread(self.store._collect_native, info, True))
+                                inflight[t] = (batch, prep, None)
+                                batch = []
+                                continue
+                        res = self.store._assemble(prep, ran)
                     except Exception as exc:  # noqa: BLE001 -- every waiter sees the failure
                         self._fail(batch, exc)
                         continue
@@ -176,11 +242,12 @@ class _SearchBatcher:
         except BaseException as exc:  # never leave a waiter hanging: fail what this drain holds
             err = exc if isinstance(exc, Exception) else RuntimeError(f"search batcher stopped: {exc!r}")
             self._fail(batch, err)
-            for b, _ in inflight.values():
+            for b, _, _ in inflight.values():
                 self._fail(b, err)
             raise
         finally:
             self.running = False
+            self._release_loop()
 
 
 def _filter_key(filters) -> str:
@@ -211,6 +278,8 @@ class HipVectorStore(BaseVectorStore):
         self._loader = index_loader or (lambda path, dim, dtype, metric: _native.NativeIndex.load(
             path, devices=self.devices, dim=dim, dtype=dtype, metric=metric))
         self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)), int(params.get("search_depth", 2)))
+        # unfiltered batches launched from the event loop through the asynchronous native entry point
+        self.native_async = bool(params.get("native_async", True))
         self._lock = threading.RLock()
         self._paths = P.Paths(config.persist_directory, config.collection_name)
         self._gen = 0
@@ -556,6 +625,7 @@ class HipVectorStore(BaseVectorStore):
 
     def close(self) -> None:
         """Fold the journal into a snapshot and release the device index."""
+        self._batcher.close()
         with self._lock:
             if self._journal is not None and self._journal.size:
                 self.flush()
@@ -619,6 +689,46 @@ class HipVectorStore(BaseVectorStore):
             # search takes its exhaustive exact path (same results, one corpus pass per query)
             return self._index.search(q, min(top_k, n_live), self.filter_bitmap(filters)), tables
 
+    def _submit_native(self, prep, batcher: _SearchBatcher, loop):
+        """Launch an unfiltered batch through the asynchronous native entry point from the event loop
+        (None: this batch takes the worker-thread path -- a filter, no async-capable index, k beyond
+        HR_MAX_K, an empty collection, or the store / handle busy: nothing here ever waits)."""
+        q, top_k, filters = prep
+        idx = self._index
+        if (filters or idx is None or not self.native_async or top_k <= 0 or top_k > _native.HR_MAX_K
+                or not hasattr(idx, "search_submit_host") or len(getattr(idx, "devices", (0,))) > 1):
+            return None
+        if not self._lock.acquire(blocking=False):  # a mutation (in a worker thread) holds the store
+            return None
+        try:
+            n_live = self.count_sync()
+            if n_live == 0 or self._index is not idx:
+                return None
+            fd = batcher.native_fd(loop)
+            if fd < 0:
+                return None
+            k = min(top_k, n_live)
+            try:
+                ticket = idx.search_submit_host(q, k, fd)
+            except (NotImplementedError, _native.BusyError):
+                return None
+            return idx, ticket, q.shape[0], k, (self._records, self._metas, self._epoch)
+        finally:
+            self._lock.release()
+
+    def _collect_native(self, info, blocking: bool):
+        """(raw, tables) of a finished native launch, as _run_search returns them; None when not blocking
+        and the store lock is held (the caller then collects in a worker thread)."""
+        idx, ticket, B, k, tables = info
+        if not self._lock.acquire(blocking=blocking):
+            return None
+        try:
+            if idx is not self._index or tables[2] != self._epoch:  # cleared / closed since: rows are gone
+                return None, tables
+            return idx.search_collect(ticket, B, k), tables
+        finally:
+            self._lock.release()
+
     def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
         """(Chunk, score) lists of a finished batch.  Runs on the event loop while the next launch is in
         flight, so it is the host's per-hit cost under load: the hits' host records are gathered for the
@@ -630,7 +740,9 @@ class HipVectorStore(BaseVectorStore):
             return [[] for _ in range(n)]
         scores, rows = raw
         # the tables the search ran against (append-only; a row deleted since then reads None, dropped)
-        valid = rows >= 0
+        # rows the index returned but the tables do not hold yet (an add racing a native launch) are
+        # treated like rows added after the search
+        valid = (rows >= 0) & (rows < min(len(recs), len(metas)))
         hit_rows = rows[valid]
         rec_l = recs.a[hit_rows].tolist()
         meta_l = metas.a[hit_rows].tolist()

@@ -65,7 +65,7 @@ def cpu_embed_rate(preset: str, texts: list[str], max_length: int, batch: int = 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", type=int, default=100_000)
-    ap.add_argument("--preset", default="bge-large")
+    ap.add_argument("--preset", default="bge-base", help="bge-base (SURVEY §8(d) C4: 12 layers, H = 768) or bge-large")
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--max-length", type=int, default=512)
@@ -84,6 +84,10 @@ def main():
     splitter_cfg = ChunkingConfig(chunk_size=500, chunk_overlap=50)
     t_gen = time.perf_counter() - t0
     emb = TorchRocmEmbedder(preset=args.preset, dtype=args.dtype, batch_size=args.batch, max_length=args.max_length)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from flops import EncoderFlops, mfma_block
+
+    counter = EncoderFlops(emb.model)
     store = HipVectorStore(VectorStoreConfig(backend="hip", collection_name="bench", persist_directory="/tmp/unused",
                                              index_params={"dtype": "bf16", "persist": False,
                                                            "capacity": int(args.chunks * 1.2)}))
@@ -127,6 +131,7 @@ def main():
     asyncio.run(store.clear())
     for k in stage:
         stage[k] = 0.0
+    counter.reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = t0
@@ -139,6 +144,7 @@ def main():
             print(f"[ingest] {n_chunks} chunks, {last - t0:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t_ing = time.perf_counter() - t0
+    flops = counter.totals()
     # queries: embed + one batched search
     ret = BatchedVectorRetriever(store, emb, RetrieverConfig(top_k=10, similarity_threshold=0.0))
     qs = [" ".join(d.content.split()[5:15]) for d in docs[:args.queries]]
@@ -162,6 +168,9 @@ def main():
         "dtype": args.dtype, "data": "synthetic text, random-init weights",
         "config": {"workload": "C4 ingest", "preset": args.preset, "batch": args.batch, "max_length": args.max_length,
                    "chunk_size": 500, "chunk_overlap": 50, "docgen_s": round(t_gen, 2)},
+        # the embed stage against the MFMA roof: encoder FLOPs over the embed stage's wall time
+        "mfma": mfma_block(flops, stage["embed_s"], what="embedder forward over the ingest (tools/flops.py), "
+                           "per second of the embed stage"),
         "cpu_baseline": {"value": round(cpu_rate, 2), "unit": "chunks/s (embed only)", "cores": threads,
                          "kind": "port", "sample": f"{len(texts)} chunks, same model fp32 on host torch"},
     }), flush=True)

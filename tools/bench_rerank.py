@@ -159,6 +159,10 @@ def main():
     rr = TorchRocmReranker(preset="bge-reranker-base", dtype="bfloat16", batch_size=args.rerank_batch,
                            max_length=512)
     vocab = [f"tok{i}" for i in range(20000)]
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from flops import EncoderFlops, mfma_block
+
+    counter = EncoderFlops(rr.model)
 
     def passage(row: int) -> str:  # stored chunk text of a row (deterministic synthetic words)
         r = np.random.default_rng(row)
@@ -184,6 +188,7 @@ def main():
     for i in range(args.warmup, nb):
         rr.warm([r.chunk.content for rs in work[i][1] for r in rs])
     tok_ms = (time.perf_counter() - t_tok) * 1e3 / args.steps
+    counter.reset()
     t1 = time.perf_counter()
     pairs = 0
     for i in range(args.warmup, nb):
@@ -191,6 +196,8 @@ def main():
         pairs += sum(len(r) for r in work[i][1])
     torch.cuda.synchronize()
     rr_ms = (time.perf_counter() - t1) * 1e3 / args.steps
+    out["stage2_mfma"] = mfma_block(counter.totals(), rr_ms * args.steps / 1e3,
+                                    what="cross-encoder forward of the timed steps (tools/flops.py)")
     assert all(len(r) == args.final_k for r in res)
     out.update({"stage2_passage_tokenise_ms_per_step_cold": round(tok_ms, 2),
                 "stage2_rerank_queries_per_step": rq, "stage2_pairs_per_step": pairs // args.steps,

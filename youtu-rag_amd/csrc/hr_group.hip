@@ -97,6 +97,7 @@ int group_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, 
         }
         sh->stripe_G = n_dev;
         sh->stripe_s = s;
+        for (int j = 0; j < n_dev; ++j) sh->shared_dev |= j != s && dev_ids[j] == dev_ids[s];
         g->shards.push_back(sh);
         hipEvent_t ev = nullptr;
         hipError_t e = hipSetDevice(sh->device);

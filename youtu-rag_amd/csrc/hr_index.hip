@@ -590,8 +590,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // FILTER (A/B at 16: 1M x 768 0.355 vs 0.325 ms/step; at 4, 300k-row shards lose 10 %).
     static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
     static const int early_min = getenv("HIPRAG_EARLY_MIN") ? atoi(getenv("HIPRAG_EARLY_MIN")) : 8;  // A/B
+    // Not for a group shard sharing its GPU with other shards (dev_ids repeated): their early SAMPLEs on
+    // high-priority streams then cut into each other's FILTERs -- 8 shards of 1.25M rows on one GPU
+    // 4.87 ms/batch with, 3.76 without (profiles/r03_group_shared_gpu.log)
     const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && tail_cus(h) > 0 &&
-                       n_tiles >= early_min * sample_target(n_tiles);
+                       !h->shared_dev && n_tiles >= early_min * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {

@@ -192,6 +192,7 @@ struct hr_index {
     int G = 1;                        // > 1: group handle
     std::vector<hr_index*> shards;
     int stripe_G = 1, stripe_s = 0;   // shard of a group: global row of local row L = stripe_row(L, G, s)
+    bool shared_dev = false;          // shard of a group whose GPU also holds another shard of the group
     DevBuf g_cand, g_bound, g_kth, g_fail, g_out, g_q;  // group: gathered candidates / merge outputs (primary)
     DevBuf s_mask;                    // shard of a group: this shard's words of the caller's row mask
     std::vector<hipEvent_t> g_ev;     // group: one per shard (shard stream -> primary stream)

@@ -759,20 +759,21 @@ class HipVectorStore(BaseVectorStore):
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
         new, C = object.__new__, Chunk
-        hits = []
-        for i, (r, m) in enumerate(zip(rec_l, meta_l)):
-            if r is None:
-                hits.append(None)
-                continue
-            c = new(C)
-            c.__dict__ = {"id": r[0], "document_id": m.get("document_id", ""), "content": r[2],
-                          "chunk_index": m.get("chunk_index", 0), "metadata": dict(m),
-                          "embedding": None if embs is None else embs[i]}
-            hits.append((c, score_l[i]))
-        out, at = [], 0
-        for cnt in per_q:
-            out.append([h for h in hits[at:at + cnt] if h is not None])
-            at += cnt
+        out, i = [], 0
+        for cnt in per_q:  # one pass: each query's hits straight into its list
+            res = []
+            for j in range(i, i + cnt):
+                r = rec_l[j]
+                if r is None:
+                    continue
+                m = meta_l[j]
+                c = new(C)
+                c.__dict__ = {"id": r[0], "document_id": m.get("document_id", ""), "content": r[2],
+                              "chunk_index": m.get("chunk_index", 0), "metadata": dict(m),
+                              "embedding": None if embs is None else embs[j]}
+                res.append((c, score_l[j]))
+            out.append(res)
+            i += cnt
         return out
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None

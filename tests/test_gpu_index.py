@@ -868,11 +868,11 @@ def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
 
 
 @pytest.mark.parametrize("dim,dtype,metric", [(1024, "bf16", "cosine"), (768, "f16", "cosine"), (1024, "bf16", "ip")])
-def test_wide_filter_edges_vs_oracle(native, dim, dtype, metric):
-    """The wide FILTER (k_scan_wide: 128 queries per workgroup, LDS-DMA corpus ring; 65..256 queries,
-    k <= 32, D = 768 / 1024): fewer tiles than workgroups, ragged ranges, a selective filter (tile
-    list), a removed stretch, and massive ties that overflow a region's 256 candidate slots (the
-    guard then sends the query to the exact fallback) -- identical to the oracle every time."""
+def test_query_group_edges_vs_oracle(native, dim, dtype, metric):
+    """Query groups (65..256 queries per corpus pass, k <= 32, D = 768 / 1024): fewer tiles than
+    workgroups, ragged ranges, a selective filter (tile list), a removed stretch, and massive ties that
+    overflow the private candidate regions (the guard then sends the query to the exact fallback) --
+    identical to the oracle every time."""
     rng = np.random.default_rng(dim + 3)
     for n, B, k in ((500, 65, 10), (9_001, 128, 32), (70_000, 256, 1), (40_000, 130, 16)):
         raw = R.gen_rows(31, 0, n, dim)

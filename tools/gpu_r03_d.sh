@@ -4,6 +4,8 @@ set -o pipefail
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r03d
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_index.py -x -q --timeout 200 --timeout-method thread > $O/index_tests.log 2>&1
+rc=$?; echo "index tests rc=$rc"; tail -2 $O/index_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u tools/bench_ingest.py --chunks 100000 --preset bge-base --dtype bfloat16 > $O/ingest_100k_base.json 2> $O/ingest_100k_base.err
 rc=$?; echo "ingest rc=$rc"; cat $O/ingest_100k_base.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $O/prof_ingest -o run --output-format csv -- python3 tools/bench_ingest.py --chunks 20000 --preset bge-base --dtype bfloat16 --cpu-sample 8 > $O/ingest_prof.json 2> $O/ingest_prof.err

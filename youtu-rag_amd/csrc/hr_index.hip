@@ -339,15 +339,6 @@ struct Plan {
 
 static int scan_lds_bytes(const hr_index* h, int QB) { return h->S * QB * 1024; }
 
-// the wide FILTER (k_scan_wide) serves pairs of 64-query groups: bf16 / f16 corpora at D = 768 or 1024,
-// cosine / inner product.  OFF by default (HIPRAG_WIDE=1 turns it on): measured slower than the query
-// groups of k_scan -- B = 128 at 10M rows 5.52 vs 4.40 ms, B = 256 10.9 vs 7.56 ms (tools/ab_wide.sh,
-// DESIGN.md "Query groups")
-static bool wide_capable(const hr_index* h) {
-    static const int wide_env = getenv("HIPRAG_WIDE") ? atoi(getenv("HIPRAG_WIDE")) : 0;
-    return wide_env && h->dtype != F32 && h->metric != L2 && (h->S == 64 || h->S == 48);
-}
-
 static int make_plan(const hr_index* h, int B, Plan* p) {
     const int QB = (B > 32 && scan_lds_bytes(h, 2) <= 160 * 1024) ? 2 : 1;
     if (scan_lds_bytes(h, QB) > 160 * 1024)
@@ -363,7 +354,6 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     // batch was two corpus passes; 32-query groups share one (HIPRAG_QB1_GROUPS=0: separate passes, A/B)
     static const int qb1_env = getenv("HIPRAG_QB1_GROUPS") ? atoi(getenv("HIPRAG_QB1_GROUPS")) : 1;
     if (QB == 1 && B > 32 && h->dtype != F32 && qb1_env) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
-    if (p->NG > 1 && (p->NG & 1) && wide_capable(h)) p->NG = std::min(max_groups + (max_groups & 1), p->NG + 1);
     p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
     const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
@@ -436,52 +426,6 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
     return HR_OK;
 }
 
-// wide FILTER: one workgroup (4 waves) per CU serves two 64-query groups; NG / 2 sets of workgroups
-template <int MT, int DT, int S_, int R>
-static int launch_scan_wide_r(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, hipStream_t st) {
-    const int nset = pl.NG / 2;
-    const bool nt = nset == 1;  // sets share tiles through L2: default-policy loads then
-    auto kern = nt ? k_scan_wide<MT, DT, S_, R, true> : k_scan_wide<MT, DT, S_, R, false>;
-    const int lds = R * 16 * 1024 + 16 * 1024;
-    static std::mutex attr_mu;
-    static bool attr[64][2] = {};
-    {
-        std::lock_guard<std::mutex> lk(attr_mu);
-        if (!attr[h->device & 63][nt]) {
-            HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            attr[h->device & 63][nt] = true;
-        }
-    }
-    int64_t per_set = std::max<int64_t>(1, std::min<int64_t>(cus / nset, a.n_units));
-    if (nset > 1) per_set = std::max<int64_t>(8, per_set / 8 * 8);
-    ScanArgs args = a;
-    args.ng = nset;
-    static const int wdbg = getenv("HIPRAG_WIDE_DEBUG") ? atoi(getenv("HIPRAG_WIDE_DEBUG")) : 0;
-    args.wide_dbg = wdbg;
-    const int Bq = 64;
-    HIP_TRY(sc.pbuf.ensure((size_t)pl.NG * Bq * per_set * kCapWide * sizeof(float2)));
-    HIP_TRY(sc.pcnt.ensure((size_t)pl.NG * Bq * per_set * 4));
-    args.pbuf = sc.pbuf.as<float2>();
-    args.pcnt = sc.pcnt.as<uint32_t>();
-    args.capw = kCapWide;
-    sc.last_W = per_set;
-    sc.last_Bp = Bq;
-    sc.last_ng = pl.NG;
-    sc.last_capw = kCapWide;
-    h->last_scr = &sc;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(per_set * nset)), dim3(256), lds, st, args);
-    HIP_TRY(hipGetLastError());
-    return HR_OK;
-}
-
-template <int MT, int DT, int S_>
-static int launch_scan_wide(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, hipStream_t st) {
-    // ring depth (stages of 16 KiB): 9 = 128 KiB in flight per CU (HIPRAG_WIDE_RING=8: 112 KiB, A/B)
-    static const int ring_env = getenv("HIPRAG_WIDE_RING") ? atoi(getenv("HIPRAG_WIDE_RING")) : 9;
-    if (ring_env == 8) return launch_scan_wide_r<MT, DT, S_, 8>(h, sc, cus, pl, a, st);
-    return launch_scan_wide_r<MT, DT, S_, 9>(h, sc, cus, pl, a, st);
-}
-
 template <int MT, int DT, int MODE>
 static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, hipStream_t st) {
     int lds = scan_lds_bytes(h, pl.QB);
@@ -494,11 +438,6 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // (HIPRAG_SAMPLE_NT=1: non-temporal SAMPLE loads, for A/B)
     static const bool sample_nt = getenv("HIPRAG_SAMPLE_NT") && atoi(getenv("HIPRAG_SAMPLE_NT")) != 0;
     const bool dflt = pl.NG > 1 || (MODE == SCAN_SAMPLE && !sample_nt);
-    if constexpr (MODE == SCAN_FILTER && DT != F32) {
-        if (pl.NG >= 2 && pl.NG % 2 == 0 && wide_capable(h) && a.np == 1 && !a.xnorm && a.use_groups && !a.stamps)
-            return h->S == 64 ? launch_scan_wide<MT, DT, 64>(h, sc, cus, pl, a, st)
-                              : launch_scan_wide<MT, DT, 48>(h, sc, cus, pl, a, st);
-    }
 #define HR_SCAN_CASE(QBv, Pv)                                                                     \
     if (pl.QB == QBv && pl.P == Pv)                                                               \
         return dflt ? launch_scan_t<MT, DT, QBv, Pv, MODE, false>(h, sc, cus, a, st, lds)         \

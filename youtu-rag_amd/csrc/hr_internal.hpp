@@ -74,7 +74,6 @@ int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles,
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
 static constexpr int kCapW = 32;        // private candidate slots per (wave, query) (FILTER mode)
-static constexpr int kCapWide = 256;    // ... per (workgroup, query) of the wide FILTER (8x a wave's tiles)
 static constexpr int kScanThreads = 512;
 
 // Per-batch search workspace.  Two sets ping-pong between consecutive pipelined batches

@@ -283,7 +283,6 @@ struct ScanArgs {
     // reads np windows of consecutive tiles.  0: parts keep contiguous per-wave ranges (tile lists)
     int teams;
     int dyn_pct;             // dynamic-tail percentage the host used (teams recompute their split)
-    int wide_dbg;            // k_scan_wide timing experiments: 1 = no MFMAs, 2 = no LDS reads either (wrong results)
 };
 
 
@@ -306,17 +305,6 @@ struct XFrag;
 // (HR_CORPUS_NT=0 builds the default-policy variant for A/B timing)
 #ifndef HR_CORPUS_NT
 #define HR_CORPUS_NT 1
-#endif
-// HR_RING_SCHED=1: keep every refill right after the use of its slot (sched barriers), a textbook ring
-// with vmcnt(15) before every k-step.  Measured SLOWER than the compiler's own schedule, which waits
-// for the whole ring early in each batch of P k-steps and then issues the P refills back to back
-// (10M rows 3.15 vs 3.00 ms, 1.25M 0.442 vs 0.434, B = 128 4.96 vs 4.51; tools/ab_ring.sh): each wave
-// then sends one contiguous P KiB burst at a time, which the HBM serves better than P requests
-// trickled between the MFMAs of 8 waves.  HR_RING_SCHED=2 double-buffers (compute half the ring, refill
-// it as one P/2 KiB burst while the other half is in flight): 1.25M 0.431 vs 0.433 ms, but 10M 3.18 vs
-// 3.06 ms and B = 128 4.76 vs 4.45 ms.  Both kept as A/B build switches; the default is the compiler's.
-#ifndef HR_RING_SCHED
-#define HR_RING_SCHED 0
 #endif
 // HR_ROTATE_ROUNDS=0 builds the unrotated round-robin dealing (A/B and the regression check of
 // test_periodic_clusters_spread_over_waves only)
@@ -488,12 +476,7 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     if (u0 < u1) {
         const int64_t c0 = tile_at(u0) * S;
 #pragma unroll
-        for (int i = 0; i < P; ++i) {
-            ring[i].load(a.rows, c0 + i, lane);
-#if HR_RING_SCHED
-            __builtin_amdgcn_sched_barrier(0);  // slot order = issue order, as in the loop (no partial drains)
-#endif
-        }
+        for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
     }
 
     // stage the query fragments (QB*S KiB) into LDS once per launch; 8 loads in flight per
@@ -697,51 +680,6 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
         for (int sb = 0; sb < S; sb += P) {
             const bool same = sb + P < S;
             const int64_t nc = same ? t * S + sb + P : tn * S;
-#if HR_RING_SCHED == 1
-            // query fragments one k-step ahead (LDS latency under the MFMAs of the step before)
-            u32x4 qn[QB];
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb) qn[qb] = qs[(sb * QB + qb) * 64 + lane];
-#pragma unroll
-            for (int i = 0; i < P; ++i) {
-                const u32x4 xf = ring[i].get();
-                u32x4 qc[QB];
-#pragma unroll
-                for (int qb = 0; qb < QB; ++qb) qc[qb] = qn[qb];
-                if (i + 1 < P) {
-#pragma unroll
-                    for (int qb = 0; qb < QB; ++qb) qn[qb] = qs[((sb + i + 1) * QB + qb) * 64 + lane];
-                }
-                __builtin_amdgcn_sched_barrier(0);  // the next step's LDS reads go out before these MFMAs
-#pragma unroll
-                for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma32<MT>(qc[qb], xf, acc[qb]);
-                // refill slot i after its last use and keep it there: the new value can then take the
-                // slot's own registers.  Refilling before the MFMAs that read the old value (or letting
-                // the scheduler sink all P refills to the end of the batch) makes the two values
-                // overlap, the loop back-edge then needs register copies of in-flight slots, and every
-                // copy waits for its load: the ring drained to vmcnt(0..2) once per P chunks.
-                ring[i].load(a.rows, nc + i, lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#elif HR_RING_SCHED == 2
-            // double-buffered halves: compute half h, then refill it as one P/2 KiB burst while the
-            // other half's loads are in flight
-            constexpr int H = P / 2;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-#pragma unroll
-                for (int j = 0; j < H; ++j) {
-                    const u32x4 xf = ring[h * H + j].get();
-#pragma unroll
-                    for (int qb = 0; qb < QB; ++qb)
-                        acc[qb] = mfma32<MT>(qs[((sb + h * H + j) * QB + qb) * 64 + lane], xf, acc[qb]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < H; ++j) ring[h * H + j].load(a.rows, nc + h * H + j, lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#else
 #pragma unroll
             for (int i = 0; i < P; ++i) {
                 const u32x4 xf = ring[i].get();
@@ -752,7 +690,6 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
                     acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
                 }
             }
-#endif
         }
 
         // epilogue: (euclidean) approximate score, predicate, group max, threshold filter
@@ -883,238 +820,6 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
             }
         }
     }
-}
-
-
-// ---------------------------------------------------------------- K3w: the wide FILTER pass
-// 16 ds_read_b128 at addr + i * 1024 into v[i] (inline asm: the compiler neither counts nor waits for them)
-template <int I>
-__device__ inline void lds_read16(u32x4 (&v)[16], uint32_t addr) {
-    if constexpr (I < 16) {
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[I]) : "v"(addr), "i"(I * 1024));
-        lds_read16<I + 1>(v, addr);
-    }
-}
-// wait until at most n LDS operations are outstanding, and make x (written by one of them) depend on it
-__device__ inline void lgkm_wait_for(u32x4& x, int n) {
-    switch (n) {
-#define HR_LGKM(N) case N: asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(x)); break;
-        HR_LGKM(0) HR_LGKM(1) HR_LGKM(2) HR_LGKM(3) HR_LGKM(4) HR_LGKM(5) HR_LGKM(6) HR_LGKM(7)
-        HR_LGKM(8) HR_LGKM(9) HR_LGKM(10) HR_LGKM(11) HR_LGKM(12) HR_LGKM(13) HR_LGKM(14) HR_LGKM(15)
-#undef HR_LGKM
-    }
-}
-// 65..256 queries per corpus pass at S = 48 / 64 k-steps (D = 768 / 1024), bf16 / f16 corpora.
-// The query-group launch (k_scan with ng > 1) holds one 64-query tile per CU in LDS and lets ng
-// workgroups stream the same tiles, the others hitting L2: its memory side alone is capped at
-// 5.35 / 3.47 TB/s of unique bytes for ng = 2 / 4 (tools/stream_ceiling mode 3), whatever the
-// arithmetic.  Here ONE workgroup serves 128 queries (two 64-query groups) and reads each tile once:
-// 4 waves, one per SIMD, each holding its 32 queries over the whole depth in registers (the MFMA A
-// operand, 4*S registers), while the corpus streams through an LDS ring of R stages (16 KiB = 16
-// k-step chunks each) filled by LDS-DMA (global_load_lds_dwordx4, 4 per wave per stage) and kept
-// R-1 stages deep across raw barriers with a counted vmcnt (cdna_hip_programming.md §5 "Pipelining
-// across barriers").  Per stage and SIMD: 16 MFMAs (512 cycles) and 16 KiB of LDS reads per wave,
-// against ~1250 cycles of the CU's HBM share -- the pass stays memory-bound.  256 queries: two sets
-// of workgroups (blockIdx % 8 equal per range block, as k_scan) share the tiles through L2.
-// Thresholds, group maxima, the epilogue and the private candidate regions are k_scan's (QB = 1 per
-// wave); a region is (group, workgroup), each wave owning 32 of its 64 query slots, so k_select reads
-// it unchanged with W = workgroups per set.  The group-max keys of the next refresh come in by
-// LDS-DMA too: a plain vector load in this loop would make the compiler drain the ring (vmcnt(0)).
-template <int MT, int DT, int S_, int R, bool NT>
-__global__ __launch_bounds__(256, 1) void k_scan_wide(ScanArgs a) {
-    static_assert(DT != F32, "1 KiB k-step chunks (bf16 / f16 corpora)");
-    static_assert(S_ % 16 == 0, "whole stages per tile");
-    constexpr int SPT = S_ / 16;  // stages per tile
-    constexpr int STAGE = 16 * 1024;
-    constexpr int REFRESH = 4;  // tiles between threshold refreshes
-    static_assert(R >= 3 && R <= REFRESH * SPT, "keys requested at one refresh land before the next reads them");
-    constexpr int Bq = 64;
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, g = lane & 31, wv = tid >> 6;
-    const int nset = a.ng;
-    const int bx = blockIdx.x;
-    const int set = nset > 1 ? (bx >> 3) % nset : 0;
-    const int64_t nrb = gridDim.x / nset;
-    const int64_t rb = nset > 1 ? (int64_t)((bx >> 3) / nset) * 8 + (bx & 7) : bx;
-    const int grp = 2 * set + (wv >> 1), qh = wv & 1;  // this wave: queries qh*32 .. +32 of group grp
-    uint32_t* const keys_g = a.mkeys + ((int64_t)grp * Bq + qh * 32) * 32;  // [32 queries][32 groups]
-    const float* const floor_g = a.floor_q + grp * Bq + qh * 32;
-    const int64_t wg = (int64_t)grp * nrb + rb;  // candidate region of (group, workgroup)
-    float2* const region = a.pbuf + (wg * Bq + qh * 32) * a.capw;
-    const int64_t base = a.n_units / nrb, rem = a.n_units % nrb;
-    const int64_t u0 = rb * base + (rb < rem ? rb : rem);
-    const int64_t u1 = u0 + base + (rb < rem ? 1 : 0);
-    if (u0 >= u1) {  // (the whole workgroup: same range for every wave)
-        if (lane < 32) a.pcnt[wg * Bq + qh * 32 + lane] = 0;
-        return;
-    }
-    auto tile_at = [&](int64_t u) -> int64_t {
-        const int64_t i = wave_uniform(u);
-        return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
-    };
-
-    // this wave's 32 queries over the whole depth, and the starting thresholds: plain loads, all
-    // before the first LDS-DMA goes out
-    u32x4 qreg[S_];
-    const u32x4* qf = (const u32x4*)a.qfrag + (int64_t)grp * S_ * 2 * 64;
-#pragma unroll
-    for (int s = 0; s < S_; ++s) qreg[s] = qf[(s * 2 + qh) * 64 + lane];
-    float th[16], gmax[16], flo[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int q = acc_query(0, i, half);
-        flo[i] = floor_g[q];
-        uint32_t k = __hip_atomic_load(keys_g + q * 32 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        float f = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
-        th[i] = fmaxf(f, flo[i]);
-        gmax[i] = -__builtin_inff();
-    }
-    // the query registers count as used here, so the compiler's wait for their loads lands before the
-    // ring is issued (a first use inside the loop would wait vmcnt(0) and drain the prologue's DMA)
-#pragma unroll
-    for (int s = 0; s < S_; ++s) asm volatile("" : "+a"(qreg[s]));
-    uint32_t* const kl = (uint32_t*)(lds + R * STAGE) + wv * 1024;  // this wave's key copy (LDS)
-    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
-    auto request_keys = [&]() {  // 4 KiB of group-max keys, relaxed agent-scope (sc1) reads into LDS
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(keys_g + j * 256 + lane * 4),
-                                             (__attribute__((address_space(3))) void*)(kl + j * 256), 16, 0, 16);
-    };
-
-    // corpus ring: stage i of the range goes to slot i % R; the last stage is re-requested past the
-    // end, so every stage issues the same 4 LDS-DMA per wave and vmcnt(4 (R - 2)) always means
-    // "this wave's part of the next stage has landed"
-    int64_t ld_u = u0, ld_tile = tile_at(u0);
-    int ld_j = 0;
-    auto issue = [&](int slot) {
-        const uint8_t* src = a.rows + (ld_tile * S_ + ld_j * 16 + wv * 4) * 1024 + lane * 16;
-        uint8_t* dst = lds + slot * STAGE + wv * 4 * 1024;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j * 1024),
-                                             (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, 0, NT ? 2 : 0);
-        if (ld_u + 1 < u1 || ld_j + 1 < SPT) {
-            if (++ld_j == SPT) {
-                ld_j = 0;
-                ++ld_u;
-                ld_tile = tile_at(ld_u);
-                // a scalar load still in flight makes every later LDS wait lgkmcnt(0) (scalar loads
-                // return out of order): take its value now
-                asm volatile("" : "+s"(ld_tile));
-            }
-        }
-    };
-    request_keys();
-#pragma unroll
-    for (int i = 0; i < R - 1; ++i) issue(i);
-
-    uint32_t mycnt = 0;  // lane q < 32: candidates of query q in this region
-    int slot = 0, done = 0;
-    for (int64_t u = u0; u < u1; ++u) {
-        const int64_t t = tile_at(u);
-        uint32_t allow = scalar_word(a.live, t);
-        if (a.mask) allow &= scalar_word(a.mask, t);
-        asm volatile("" : "+s"(allow));  // (as in issue(): no scalar load outstanding across the LDS reads)
-        f32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-#pragma unroll
-        for (int j = 0; j < SPT; ++j) {
-            // RAW: this wave's DMA for the stage has landed (vmcnt), every wave's has (barrier).
-            // WAR: every wave's reads of the slot refilled next are done (lgkmcnt + barrier).
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 2)) : "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            issue(slot == 0 ? R - 1 : slot - 1);
-            // the stage's 16 B fragments in one burst of LDS reads, then each MFMA behind its own counted
-            // wait.  The reads are inline asm: with an LDS-DMA in flight the compiler can only wait
-            // lgkmcnt(0) for its own LDS reads (all 16 before the first MFMA); LDS-DMA is counted by
-            // vmcnt only, so lgkmcnt(15 - i) retires exactly reads 0..i
-            const uint32_t xa = lds_base + slot * STAGE + lane * 16;
-            if (a.wide_dbg == 0) {
-                u32x4 xb[16];
-                lds_read16<0>(xb, xa);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    lgkm_wait_for(xb[i], 15 - i);
-                    acc = mfma32<MT>(qreg[j * 16 + i], xb[i], acc);
-                    __builtin_amdgcn_sched_barrier(0);  // (keeps each MFMA right behind its own wait)
-                }
-            } else if (a.wide_dbg == 1) {
-                u32x4 xb[16];
-                lds_read16<0>(xb, xa);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[i & 15] += __builtin_bit_cast(float, xb[i].x);
-            }
-            slot = slot + 1 == R ? 0 : slot + 1;
-        }
-        // epilogue (k_scan's, one 32-query block)
-        const int rg = slot_row(t, g);
-        const bool ok = (allow >> rg) & 1u;
-        const uint32_t row = (uint32_t)(t * 32 + rg);
-        uint64_t any = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float v = ok ? acc[i] : -__builtin_inff();
-            gmax[i] = fmaxf(gmax[i], v);
-            any |= __ballot(ok && v >= th[i]);
-        }
-        if (any) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float v = acc[i];
-                const bool pass = ok && v >= th[i];
-                const uint64_t m = __ballot(pass);
-                if (m) {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t mh = (uint32_t)(m >> (32 * h));
-                        if (mh) {
-                            const int q = acc_query(0, i, h);
-                            const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)mycnt, q);
-                            if (pass && half == h) {
-                                const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                                if (pos < (uint32_t)a.capw) region[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
-                            }
-                            mycnt += (lane == q) ? (uint32_t)__builtin_popcount(mh) : 0u;
-                        }
-                    }
-                }
-            }
-        }
-        if (++done % REFRESH == 0) {
-            // keys requested at the previous refresh (or the start): older than every stage waited
-            // for since (R <= REFRESH * SPT), so they have landed
-            uint32_t key[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) key[i] = kl[acc_query(0, i, half) * 32 + g];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                key[i] = key[i] > HR_KEY_NEG_INF ? key[i] : HR_KEY_NEG_INF;
-                if (a.publish && gmax[i] > key2f(key[i])) {
-                    atomicMax(keys_g + acc_query(0, i, half) * 32 + g, f2key(gmax[i]));
-                    key[i] = f2key(gmax[i]);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float f = key2f(key[i]);
-#pragma unroll
-                for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
-                gmax[i] = -__builtin_inff();
-                th[i] = fmaxf(th[i], fmaxf(f, flo[i]));
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // key reads done before the DMA rewrites them
-            request_keys();
-        }
-    }
-    if (lane < 32) a.pcnt[wg * Bq + qh * 32 + lane] = mycnt;
-    // no LDS-DMA may still be writing when the workgroup's LDS is handed to the next one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 

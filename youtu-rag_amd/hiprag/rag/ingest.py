@@ -64,6 +64,10 @@ class GpuIngestor:
         self.chunker = chunker or RecursiveTextSplitter(chunking or ChunkingConfig())
         self.embed_batch = int(embed_batch or getattr(embedder, "batch_size", 64))
         self._device = hasattr(embedder, "embed_texts_device") and hasattr(vector_store, "add_chunks_device")
+        # device path, pipelined one batch deep: batch i's vectors are added while batch i+1's forward
+        # runs -- (chunks, vectors, ready event) of the batch embedded but not yet added
+        self._inflight = None
+        self._add_stream = None
 
     def split(self, document: Document, metadata: dict[str, Any] | None = None) -> list[Chunk]:
         chunker = self.chunker
@@ -73,13 +77,31 @@ class GpuIngestor:
                                                                   chunk_overlap=cfg.chunk_overlap))
         return make_chunks(document, chunker.split_text(document.content, document.metadata), metadata)
 
+    def _flush(self) -> int:
+        """Add the batch embedded last (its vectors on the device), ordered after its own forward only:
+        the add stream waits for that batch's event, not for the forward enqueued after it."""
+        if self._inflight is None:
+            return 0
+        chunks, emb, ready = self._inflight
+        self._inflight = None
+        self._add_stream.wait_event(ready)
+        return self.vector_store.add_chunks_device(chunks, emb, stream=self._add_stream.cuda_stream)
+
     async def _store(self, chunks: list[Chunk]) -> int:
         if not chunks:
             return 0
         texts = [c.content for c in chunks]
         if self._device:
-            emb = self.embedder.embed_texts_device(texts)
-            return self.vector_store.add_chunks_device(chunks, emb)
+            import torch
+
+            if self._add_stream is None:
+                self._add_stream = torch.cuda.Stream(getattr(self.embedder, "device", None))
+            emb = self.embedder.embed_texts_device(texts)  # enqueued; the host goes on at once
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(emb.device))
+            n = self._flush()  # the previous batch, while this forward runs
+            self._inflight = (chunks, emb, ready)
+            return n
         for c, e in zip(chunks, await self.embedder.embed_texts(texts)):
             c.embedding = e
         await self.vector_store.add_chunks(chunks)
@@ -94,14 +116,18 @@ class GpuIngestor:
         created, pending = 0, []
         with self.vector_store.deferred_save():
             for doc in documents:
-                if any(c.document_id == doc.id for c in pending):  # same id twice: store the first copy first
+                inflight = self._inflight[0] if self._inflight is not None else ()
+                if any(c.document_id == doc.id for c in pending) or any(c.document_id == doc.id for c in inflight):
+                    # same id twice: store the first copy first
                     await self._store(pending)
+                    self._flush()
                     pending = []
                 created += await self._one(doc, metadata, pending)
                 while len(pending) >= self.embed_batch:
                     await self._store(pending[:self.embed_batch])
                     pending = pending[self.embed_batch:]
             await self._store(pending)
+            self._flush()
         return created
 
     async def _one(self, doc: Document, metadata, pending: list[Chunk]) -> int:

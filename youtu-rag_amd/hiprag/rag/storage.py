@@ -538,12 +538,16 @@ class HipVectorStore(BaseVectorStore):
             keep = self._fresh(chunks)
             if not keep:
                 return 0
-            emb = embeddings if len(keep) == len(chunks) else embeddings[torch.as_tensor(keep, device=embeddings.device)]
-            emb = emb.to(torch.float32).contiguous()
-            self._ensure_index(emb.shape[1])
-            if stream is None:
-                stream = torch.cuda.current_stream(emb.device).cuda_stream
-            first = self._index.add_device(emb.data_ptr(), emb.shape[0], stream)
+            dev = embeddings.device
+            # the given stream orders everything here: gathers / casts run on it too
+            ctx = torch.cuda.stream(torch.cuda.ExternalStream(stream, device=dev)) if stream is not None \
+                else contextlib.nullcontext()
+            with ctx:
+                emb = embeddings if len(keep) == len(chunks) else embeddings[torch.as_tensor(keep, device=dev)]
+                emb = emb.to(torch.float32).contiguous()
+                self._ensure_index(emb.shape[1])
+                stream = torch.cuda.current_stream(dev).cuda_stream
+                first = self._index.add_device(emb.data_ptr(), emb.shape[0], stream)
             need_host = self.keep_embeddings or (self.persist and not self._defer and self._gen > 0)
             self._register([chunks[i] for i in keep], first, emb.cpu().numpy() if need_host else None)
             return len(keep)
@@ -585,7 +589,7 @@ class HipVectorStore(BaseVectorStore):
             return self._remove_tables(list(self._doc_rows.get(document_id, ())))
 
     async def delete_by_document_id(self, document_id: str) -> int:
-        if self._index is None:
+        if self._index is None or document_id not in self._doc_rows:  # (a new document: no thread hop)
             return 0
         n = await asyncio.to_thread(self._delete_document_sync, document_id)
         logger.info("deleted %d chunks for document_id %s", n, document_id)

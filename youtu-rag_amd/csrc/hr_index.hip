@@ -704,7 +704,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // epilogue loads.  HIPRAG_EARLY_REFRESH=0/1 forces either (A/B)
     static const int early_refresh_env = getenv("HIPRAG_EARLY_REFRESH") ? atoi(getenv("HIPRAG_EARLY_REFRESH")) : -1;
     a.diag_nostore = (dbg & 64) ? 1 : 0;
-    a.early_refresh = early_refresh_env >= 0 ? early_refresh_env : (dual ? 1 : 0);
+    // ... and with 4+ row parts (k >= 75: a refresh then also reads the other parts' maxima), where the
+    // early loads pay at 10M too: k = 100 3.217 -> 3.190 ms (profiles/r03_rowpart_knobs_10M.log)
+    a.early_refresh = early_refresh_env >= 0 ? early_refresh_env : ((dual || np >= 4) ? 1 : 0);
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;

@@ -218,10 +218,16 @@ class TorchRocmEmbedder(BaseEmbedder):
         # pads to about its own length instead of the longest text of a random mix; rows are
         # independent through the encoder, so only the order of the output rows changes back
         order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
+        # the permutation goes up first, asynchronously from pinned memory: a pageable copy after the
+        # forwards would wait for all of them (the host then could not tokenise the next pack meanwhile)
+        perm = torch.as_tensor(order, dtype=torch.int64)
+        if self.device.type == "cuda" and _PIN:
+            perm = perm.pin_memory()
+        perm = perm.to(self.device, non_blocking=True)
         parts = [self.encode([texts[j] for j in order[i:i + self.batch_size]], instruction)
                  for i in range(0, len(texts), self.batch_size)]
         out = torch.empty((len(texts), parts[0].shape[1]), dtype=torch.float32, device=self.device)
-        out[torch.as_tensor(order, device=self.device)] = torch.cat(parts)
+        out[perm] = torch.cat(parts)
         return out
 
     def encode_queries(self, queries):

@@ -9,3 +9,5 @@ timeout -k 10 600 python -u tools/bench_ingest.py --chunks 100000 --preset bge-b
 rc=$?; echo "ingest rc=$rc"; cat $O/ingest_100k_base.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u tools/bench_ingest.py --chunks 100000 --preset bge-large --dtype bfloat16 > $O/ingest_100k_large.json 2> $O/ingest_100k_large.err
 rc=$?; echo "ingest large rc=$rc"; cat $O/ingest_100k_large.json
+timeout -k 10 300 python -u tools/attn_micro.py > $O/attn_micro.jsonl 2> $O/attn_micro.err
+echo "attn micro rc=$?"; cat $O/attn_micro.jsonl; tail -3 $O/attn_micro.err

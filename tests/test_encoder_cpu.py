@@ -1,0 +1,51 @@
+"""CPU: the unpadded encoder forward (hiprag.rag.encoder) equals Hugging Face's padded forward at every
+real token -- embedder (BertModel) and cross-encoder (BertForSequenceClassification logits) -- for
+right-padded ragged batches, with the per-sequence SDPA attention (the varlen flash kernel that serves
+fp16 / bf16 models on the GPU is checked in tests/test_gpu_embedder.py)."""
+import numpy as np
+import torch
+
+from hiprag.rag.encoder import UnpaddedEncoder, sequence_logits
+from hiprag.rag.rerankers import build_random_cross_encoder
+from hiprag.rag.rocm_embedder import build_random_bert
+
+
+def _batch(rng, B, T, vocab=30522):
+    lens = rng.integers(3, T + 1, B)
+    lens[0] = T
+    ids = np.zeros((B, T), np.int64)
+    for b, n in enumerate(lens):
+        ids[b, :n] = rng.integers(1000, vocab, n)
+        ids[b, 0], ids[b, n - 1] = 101, 102
+    mask = (np.arange(T)[None, :] < lens[:, None]).astype(np.int64)
+    return torch.from_numpy(ids), torch.from_numpy(mask), lens
+
+
+def test_unpadded_encoder_matches_padded_forward():
+    torch.manual_seed(0)
+    model = build_random_bert("tiny", 3).eval()
+    enc = UnpaddedEncoder(model, use_varlen=False)
+    rng = np.random.default_rng(5)
+    for B, T in ((1, 7), (5, 33), (9, 64)):
+        ids, mask, lens = _batch(rng, B, T)
+        with torch.inference_mode():
+            ref = model(input_ids=ids, attention_mask=mask)[0]
+            got = enc(ids, lens)
+        keep = mask.bool()
+        torch.testing.assert_close(got[keep], ref[keep], rtol=1e-5, atol=2e-5)
+        assert torch.count_nonzero(got[~keep]) == 0
+
+
+def test_unpadded_cross_encoder_logits_match():
+    torch.manual_seed(0)
+    model = build_random_cross_encoder("bge-reranker-base", 4, num_hidden_layers=2, hidden_size=128,
+                                       num_attention_heads=4, intermediate_size=256).eval()
+    enc = UnpaddedEncoder(model.base_model, use_varlen=False)
+    assert sequence_logits(model, None, probe=True)
+    rng = np.random.default_rng(6)
+    ids, mask, lens = _batch(rng, 7, 40)
+    types = torch.from_numpy((np.arange(40)[None, :] >= (lens // 2)[:, None]).astype(np.int64)) * mask
+    with torch.inference_mode():
+        ref = model(input_ids=ids, attention_mask=mask, token_type_ids=types).logits
+        got = sequence_logits(model, enc(ids, lens, types))
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)

@@ -134,3 +134,21 @@ def test_reranker_matches_hf_cross_encoder_fp32(golden_dir):
             want = [torch.sigmoid(ref_model(**tok(q, p, truncation=True, max_length=64, return_tensors="pt"))
                                   .logits[0, 0]).item() for p in ps]
             np.testing.assert_allclose(g, np.asarray(want, np.float32), rtol=0, atol=1e-5)
+
+
+def test_unpadded_reranker_matches_padded_bf16():
+    """Cross-encoder relevance through the unpadded encoder (varlen flash attention, fused QKV) vs the
+    padded Hugging Face forward of the same seeded bf16 model."""
+    from hiprag.rag.rerankers import TorchRocmReranker
+
+    words = [f"w{i}" for i in range(200)]
+    rng = np.random.default_rng(8)
+    texts = [" ".join(rng.choice(words, rng.integers(1, 120))) for _ in range(70)]
+    a = TorchRocmReranker(preset="bge-reranker-base", dtype="bfloat16", batch_size=32, max_length=256, seed=2)
+    b = TorchRocmReranker(preset="bge-reranker-base", dtype="bfloat16", batch_size=32, max_length=256, seed=2,
+                          unpadded=False)
+    assert a.unpadded is not None and b.unpadded is None
+    sa = a.score_pairs(["w1 w2 w9", "w5"], [texts, texts[:9]])
+    sb = b.score_pairs(["w1 w2 w9", "w5"], [texts, texts[:9]])
+    for x, y in zip(sa, sb):
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=0, atol=2e-2)

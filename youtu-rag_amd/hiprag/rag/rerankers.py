@@ -83,7 +83,7 @@ class TorchRocmReranker(BaseReranker):
     def __init__(self, model_name_or_path: str | None = None, *, model=None, tokenizer=None,
                  preset: str = "bge-reranker-base", batch_size: int = 256, max_length: int = 512, gpu_id: int = 0,
                  device=None, dtype: str = "bfloat16", seed: int = 0, cache_size: int = 1 << 20,
-                 fused_layernorm: bool | None = None, **_ignored):
+                 fused_layernorm: bool | None = None, unpadded: bool | None = None, **_ignored):
         import torch
 
         self.torch = torch
@@ -108,6 +108,14 @@ class TorchRocmReranker(BaseReranker):
         self.model = model.to(self.device, self.tdt).eval()
         # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
         self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0
+        # the encoder over the real tokens of each pair only (hiprag.rag.encoder), fp16 / bf16 on the GPU
+        from . import encoder as _enc
+
+        base = getattr(self.model, "base_model", None)
+        if unpadded is None:
+            unpadded = _enc._ENV and self.device.type == "cuda" and self.tdt != torch.float32
+        self.unpadded = _enc.UnpaddedEncoder(base) if (unpadded and base is not None and _enc.UnpaddedEncoder.supported(base)
+                                                       and _enc.sequence_logits(self.model, None, probe=True)) else None
         max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
         self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
         self.batch_size = int(batch_size)
@@ -237,9 +245,16 @@ class TorchRocmReranker(BaseReranker):
                 t_ids, t_mask, t_types = (torch.from_numpy(x) for x in (ids, mask, types))
                 if pin:
                     t_ids, t_mask, t_types = (t.pin_memory() for t in (t_ids, t_mask, t_types))
-                logits = self.model(input_ids=t_ids.to(self.device, non_blocking=pin),
-                                    attention_mask=t_mask.to(self.device, non_blocking=pin),
-                                    token_type_ids=t_types.to(self.device, non_blocking=pin)).logits
+                if self.unpadded is not None:
+                    from .encoder import sequence_logits
+
+                    seq = self.unpadded(t_ids.to(self.device, non_blocking=pin), total[sel],
+                                        t_types.to(self.device, non_blocking=pin))
+                    logits = sequence_logits(self.model, seq)
+                else:
+                    logits = self.model(input_ids=t_ids.to(self.device, non_blocking=pin),
+                                        attention_mask=t_mask.to(self.device, non_blocking=pin),
+                                        token_type_ids=t_types.to(self.device, non_blocking=pin)).logits
                 outs.append(torch.sigmoid(logits[:, 0].float()))
             dst = torch.from_numpy(order)
             if pin:

@@ -137,7 +137,8 @@ class TorchRocmEmbedder(BaseEmbedder):
     def __init__(self, model_name_or_path: str | None = None, *, model=None, tokenizer=None, preset: str = "bge-large",
                  batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
-                 trust_remote_code: bool = False, fused_layernorm: bool | None = None, **_ignored):
+                 trust_remote_code: bool = False, fused_layernorm: bool | None = None, unpadded: bool | None = None,
+                 **_ignored):
         import torch
 
         self.torch = torch
@@ -166,6 +167,14 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.model = model.to(self.device, tdt).eval()
         # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
         self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0
+        # the encoder over the real tokens only (hiprag.rag.encoder): fp16 / bf16 models on the GPU, where the
+        # varlen flash kernel serves the attention; fp32 keeps Hugging Face's padded forward (parity listings)
+        from . import encoder as _enc
+
+        if unpadded is None:
+            unpadded = _enc._ENV and self.device.type == "cuda" and self.dtype_name != "float32"
+        self.unpadded = _enc.UnpaddedEncoder(self.model) if (unpadded and _enc.UnpaddedEncoder.supported(self.model)) \
+            else None
         max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
         self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
         self.batch_size = int(batch_size)
@@ -198,9 +207,13 @@ class TorchRocmEmbedder(BaseEmbedder):
         # pinned staging: the H2D copy is then truly asynchronous, so the host tokenises batch i+1
         # while the GPU runs batch i's forward (a pageable copy waits for the stream to drain)
         pin = self.device.type == "cuda" and _PIN
+        lengths = inputs["attention_mask"].sum(1).numpy() if self.unpadded is not None else None
         inputs = {k: (v.pin_memory() if pin else v).to(self.device, non_blocking=True) for k, v in inputs.items()}
         with torch.inference_mode():
-            hidden = self.model(**inputs)[0]
+            if self.unpadded is not None:
+                hidden = self.unpadded(inputs["input_ids"], lengths, inputs.get("token_type_ids"))
+            else:
+                hidden = self.model(**inputs)[0]
             if hidden.dtype != getattr(torch, self.dtype_name):
                 hidden = hidden.to(getattr(torch, self.dtype_name))
             hidden = hidden.contiguous()

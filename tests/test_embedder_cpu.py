@@ -36,6 +36,28 @@ def test_hash_tokenizer_hf_semantics():
     assert b["input_ids"][0, -1] == 102 and b["input_ids"][1, -1] == 0
 
 
+def test_hash_tokenizer_cached_ids_match_plain_crc32():
+    """The word-id cache and the numpy padding give exactly the ids of the plain definition
+    (crc32 of each lower-cased \\w+ / punctuation token), non-ASCII and truncation included."""
+    import re
+    import zlib
+
+    word = re.compile(r"\w+|[^\w\s]", re.UNICODE)
+    rng = np.random.default_rng(3)
+    alpha = list("abcXYZ019_äÖß€ ,.!?\t\n")
+    texts = ["".join(rng.choice(alpha, size=int(rng.integers(0, 300)))) for _ in range(40)] + ["", "   "]
+    tok = HashWordTokenizer()
+    tok._cache_max = 50  # exercise the cache reset too
+    for max_length in (8, 512):
+        got = tok(texts, padding=True, truncation=True, max_length=max_length, return_tensors="pt")
+        want = [[101, *[1000 + zlib.crc32(w.encode()) % 29522 for w in word.findall(t.lower())][:max_length - 2], 102]
+                for t in texts]
+        width = max(map(len, want))
+        assert got["input_ids"].tolist() == [s + [0] * (width - len(s)) for s in want]
+        assert got["attention_mask"].tolist() == [[1] * len(s) + [0] * (width - len(s)) for s in want]
+        assert got["input_ids"].dtype == torch.long and got["attention_mask"].dtype == torch.long
+
+
 class CpuEmbedder(TorchRocmEmbedder):
     def _pool(self, hidden, mask, n_instr):
         m = mask.clone()

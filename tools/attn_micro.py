@@ -47,6 +47,17 @@ def main():
         from torch.nn.attention.varlen import varlen_attn
 
         out["varlen_unpadded"] = timeit(lambda: varlen_attn(qu, ku, vu, cu, cu, T, T))
+        # the encoder's layout: q, k, v as strided views of one packed (N, 3, nH, d) QKV GEMM output
+        qkv = torch.stack([qu, ku, vu], dim=1)
+        qs, ks, vs = qkv[:, 0], qkv[:, 1], qkv[:, 2]
+        try:
+            out["varlen_unpadded_strided"] = timeit(lambda: varlen_attn(qs, ks, vs, cu, cu, T, T))
+            out["varlen_strided_max_abs_diff"] = float((varlen_attn(qs, ks, vs, cu, cu, T, T).float()
+                                                        - varlen_attn(qu, ku, vu, cu, cu, T, T).float()).abs().max())
+        except Exception as e:  # noqa: BLE001
+            out["varlen_strided_error"] = repr(e)[:300]
+        out["varlen_unpadded_plus_copies"] = timeit(lambda: varlen_attn(qs.contiguous(), ks.contiguous(),
+                                                                        vs.contiguous(), cu, cu, T, T))
         ref = F.scaled_dot_product_attention(q, k, v, attn_mask=add_mask).transpose(1, 2)[keep.to(dev)]
         got = varlen_attn(qu, ku, vu, cu, cu, T, T)
         out["varlen_max_abs_diff_vs_sdpa"] = float((got.float() - ref.float()).abs().max())

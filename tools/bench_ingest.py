@@ -89,7 +89,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from flops import EncoderFlops, mfma_block
 
-    counter = EncoderFlops(emb.model)
+    counter = EncoderFlops(emb.model, getattr(emb, "unpadded", None))
     store = HipVectorStore(VectorStoreConfig(backend="hip", collection_name="bench", persist_directory="/tmp/unused",
                                              index_params={"dtype": "bf16", "persist": False,
                                                            "capacity": int(args.chunks * 1.2)}))

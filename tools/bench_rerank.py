@@ -162,7 +162,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from flops import EncoderFlops, mfma_block
 
-    counter = EncoderFlops(rr.model)
+    counter = EncoderFlops(rr.model, getattr(rr, "unpadded", None))
 
     def passage(row: int) -> str:  # stored chunk text of a row (deterministic synthetic words)
         r = np.random.default_rng(row)

@@ -15,13 +15,19 @@ from __future__ import annotations
 
 
 class EncoderFlops:
-    def __init__(self, model):
+    """Counts the forwards of `model`; pass `unpadded` (the embedder's / reranker's UnpaddedEncoder, which
+    bypasses model.forward) to count those too -- there the executed FLOPs ARE the useful ones."""
+
+    def __init__(self, model, unpadded=None):
         cfg = model.config
         self.L = int(cfg.num_hidden_layers)
         self.H = int(cfg.hidden_size)
         self.I = int(cfg.intermediate_size)
         self.masks = []
+        self.unpadded = []  # host length arrays of unpadded forwards
         self.handle = model.register_forward_pre_hook(self._hook, with_kwargs=True)
+        if unpadded is not None:
+            unpadded.observers.append(lambda B, T, lengths: self.unpadded.append(lengths.copy()))
 
     def _hook(self, module, args, kwargs):
         m = kwargs.get("attention_mask")
@@ -33,6 +39,7 @@ class EncoderFlops:
 
     def reset(self):
         self.masks = []
+        self.unpadded = []
 
     def totals(self) -> dict:
         """{'executed': FLOP, 'useful': FLOP, 'tokens_padded', 'tokens_real', 'sequences'}."""
@@ -49,6 +56,14 @@ class EncoderFlops:
             ns += B
             ex += L * (B * T * dense + B * 4 * T * T * H)
             us += L * (float(lens.sum()) * dense + float((lens * lens).sum()) * 4 * H)
+        for lens in self.unpadded:  # real tokens only: executed = useful
+            n, sq = float(lens.sum()), float((lens.astype("float64") ** 2).sum())
+            f = L * (n * dense + sq * 4 * H)
+            ex += f
+            us += f
+            tp += int(n)
+            tr += int(n)
+            ns += len(lens)
         return {"executed": float(ex), "useful": float(us), "tokens_padded": tp, "tokens_real": tr, "sequences": ns}
 
     def close(self):

@@ -72,6 +72,7 @@ class UnpaddedEncoder:
         if use_varlen and va is None:
             raise RuntimeError("torch.nn.attention.varlen is not available")
         self.varlen = va if use_varlen else None
+        self.observers = []  # callables (B, T, lengths) per forward (tools/flops.py counts FLOPs with it)
 
     @staticmethod
     def supported(base_model) -> bool:
@@ -101,6 +102,8 @@ class UnpaddedEncoder:
             idx, cu_t = idx.pin_memory(), cu_t.pin_memory()
         idx, cu_t = idx.to(dev, non_blocking=pin), cu_t.to(dev, non_blocking=pin)
         max_len = int(lengths.max()) if B else 0
+        for f in self.observers:
+            f(B, T, lengths)
         x = self.emb(input_ids=input_ids, token_type_ids=token_type_ids)  # Hugging Face's positions / types
         H = x.shape[-1]
         h = x.reshape(B * T, H).index_select(0, idx)

@@ -25,9 +25,12 @@ seeded init, with the offline HashWordTokenizer below.
 """
 from __future__ import annotations
 
+import itertools
 import os
 import re
 import zlib
+
+import numpy as np
 
 from .. import _native
 from .base import BaseEmbedder
@@ -61,34 +64,59 @@ class HashWordTokenizer:
     pad_token_id, cls_token_id, sep_token_id, first_id = 0, 101, 102, 1000
     _word = re.compile(r"\w+|[^\w\s]", re.UNICODE)
 
+    _cache_max = 1 << 20  # words; cleared when full (ids are a pure function of the word)
+
     def __init__(self, vocab_size: int = 30522):
         self.vocab_size = int(vocab_size)
+        self._cache: dict[str, int] = {}
+
+    def _hash(self, w: str) -> int:
+        if len(self._cache) >= self._cache_max:
+            self._cache.clear()
+        i = self._cache[w] = self.first_id + zlib.crc32(w.encode("utf-8")) % (self.vocab_size - self.first_id)
+        return i
 
     def _ids(self, text: str) -> list[int]:
-        span = self.vocab_size - self.first_id
-        return [self.first_id + zlib.crc32(w.encode("utf-8")) % span for w in self._word.findall(text.lower())]
+        words = self._word.findall(text.lower())
+        ids = list(map(self._cache.get, words))  # C-speed lookups; misses come back as None
+        if None in ids:
+            ids = [self._hash(w) if i is None else i for w, i in zip(words, ids)]
+        return ids
 
     def __call__(self, text, padding=False, truncation=False, max_length=None, return_tensors=None,
                  add_special_tokens=True, **_):
         single = isinstance(text, str)
         texts = [text] if single else list(text)
+        cap = max(0, int(max_length) - (2 if add_special_tokens else 0)) if truncation and max_length is not None \
+            else None
         seqs = []
         for t in texts:
             ids = self._ids(t)
-            if truncation and max_length is not None:
-                ids = ids[:max(0, int(max_length) - (2 if add_special_tokens else 0))]
-            seqs.append([self.cls_token_id, *ids, self.sep_token_id] if add_special_tokens else ids)
+            if cap is not None:
+                del ids[cap:]
+            if add_special_tokens:
+                ids.insert(0, self.cls_token_id)
+                ids.append(self.sep_token_id)
+            seqs.append(ids)
+        if return_tensors == "pt":  # one (B, W) numpy fill, no nested-list tensor build
+            import torch
+
+            lens = np.fromiter((len(s) for s in seqs), np.int64, len(seqs))
+            width = int(lens.max()) if padding and len(seqs) else None
+            if width is None and len(set(lens.tolist())) > 1:
+                raise ValueError("return_tensors='pt' needs padding=True for ragged inputs")
+            width = width if width is not None else (int(lens[0]) if len(seqs) else 0)
+            ids_np = np.full((len(seqs), width), self.pad_token_id, np.int64)
+            flat = np.fromiter(itertools.chain.from_iterable(seqs), np.int64, int(lens.sum()))
+            mask_np = np.arange(width)[None, :] < lens[:, None]
+            ids_np[mask_np] = flat
+            return {"input_ids": torch.from_numpy(ids_np), "attention_mask": torch.from_numpy(mask_np.astype(np.int64))}
         width = max((len(s) for s in seqs), default=0) if padding else None
         input_ids, mask = [], []
         for s in seqs:
             pad = (width - len(s)) if width is not None else 0
             input_ids.append(s + [self.pad_token_id] * pad)
             mask.append([1] * len(s) + [0] * pad)
-        if return_tensors == "pt":
-            import torch
-
-            return {"input_ids": torch.tensor(input_ids, dtype=torch.long),
-                    "attention_mask": torch.tensor(mask, dtype=torch.long)}
         if single:
             return {"input_ids": input_ids[0], "attention_mask": mask[0]}
         return {"input_ids": input_ids, "attention_mask": mask}

@@ -197,6 +197,11 @@ int hr_topk_records(const void* in_dev, const int64_t* seg_off_records_dev, int6
  * tokens of every sequence masked out, then L2-normalise (fp32 out, B×H). */
 int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev, int B, int T, int H, int n_instr,
                       float* out_dev, void* stream);
+/* K7 over packed (unpadded) hidden states: sequence b is rows [cu[b], cu[b+1]) of an N x H matrix (real
+ * tokens only, cu: B+1 int32 offsets on the device); same mask rule (first n_instr tokens out), same
+ * sums as hr_pool_normalize on the right-padded batch.  The in-process embedder's unpadded forward. */
+int hr_pool_normalize_packed(const void* hidden_dev, int dtype, const int32_t* cu_dev, int B, int H, int n_instr,
+                             float* out_dev, void* stream);
 /* K8: out = LayerNorm(x + r) * gamma + beta over rows x H (H <= 4096), dtype of x, r, gamma, beta and
  * out (HR_F32 / HR_BF16 / HR_F16); the encoder layers' residual add + LayerNorm fused
  * (BertSelfOutput / BertOutput, modeling_bert.py; XLM-R the same).  Ordered on `stream`. */

@@ -49,3 +49,49 @@ def test_unpadded_cross_encoder_logits_match():
         ref = model(input_ids=ids, attention_mask=mask, token_type_ids=types).logits
         got = sequence_logits(model, enc(ids, lens, types))
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
+
+
+def test_packed_forward_matches_padded_bert_and_xlmr():
+    """pack() + forward_packed(): every packed row equals the padded forward's row of that token, for
+    BERT (absolute positions 0..L-1) and XLM-R (positions padding_idx + 1 + t) embeddings."""
+    from transformers import XLMRobertaConfig, XLMRobertaModel
+
+    torch.manual_seed(0)
+    xlmr = XLMRobertaModel(XLMRobertaConfig(vocab_size=2000, hidden_size=64, num_hidden_layers=2,
+                                            num_attention_heads=4, intermediate_size=128, pad_token_id=1,
+                                            max_position_embeddings=80), add_pooling_layer=False).eval()
+    rng = np.random.default_rng(8)
+    for model, vocab in ((build_random_bert("tiny", 3).eval(), 30522), (xlmr, 2000)):
+        enc = UnpaddedEncoder(model, use_varlen=False)
+        for B, T in ((1, 5), (6, 40)):
+            ids, mask, lens = _batch(rng, B, T, vocab)
+            if vocab == 2000:
+                ids[~mask.bool()] = 1  # XLM-R pads with its padding_idx
+            types = torch.zeros_like(ids)
+            with torch.inference_mode():
+                ref = model(input_ids=ids, attention_mask=mask, token_type_ids=types)[0]
+                pk = enc.pack(ids, mask, types)
+                got = enc.forward_packed(pk)
+            assert pk.cu.dtype == torch.int32 and pk.cu.tolist() == [0, *np.cumsum(lens).tolist()]
+            torch.testing.assert_close(got, ref[mask.bool()], rtol=1e-5, atol=2e-5)
+
+
+def test_packed_cross_encoder_head_and_left_padding_refused():
+    import pytest
+
+    from hiprag.rag.encoder import first_tokens
+
+    torch.manual_seed(0)
+    model = build_random_cross_encoder("bge-reranker-base", 4, num_hidden_layers=2, hidden_size=128,
+                                       num_attention_heads=4, intermediate_size=256).eval()
+    enc = UnpaddedEncoder(model.base_model, use_varlen=False)
+    rng = np.random.default_rng(9)
+    ids, mask, lens = _batch(rng, 5, 30)
+    types = torch.from_numpy((np.arange(30)[None, :] >= (lens // 2)[:, None]).astype(np.int64)) * mask
+    with torch.inference_mode():
+        ref = model(input_ids=ids, attention_mask=mask, token_type_ids=types).logits
+        pk = enc.pack(ids.numpy(), mask.numpy(), types.numpy())
+        got = sequence_logits(model, first_tokens(enc.forward_packed(pk), pk.cu_host))
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
+    with pytest.raises(ValueError):
+        enc.pack(ids, mask.flip(1))

@@ -46,6 +46,16 @@ def test_k7_pool_normalize_matches_torch(dt, n_instr):
     # rows whose every token is masked are 0/0 = NaN in the reference too
     torch.testing.assert_close(out, ref, rtol=0, atol=ATOL, equal_nan=True)
     assert torch.isnan(out).any(1).tolist() == (m.sum(1) == 0).tolist()
+    # packed K7 (the unpadded embedder's): the same rows as an (N, H) matrix + offsets -- bit-identical to
+    # the padded kernel (same sums in the same order; the padded one only adds exact zeros besides)
+    keep = mask.bool()
+    packed = hidden[keep].contiguous()
+    cu = torch.tensor([0, *torch.cumsum(lens, 0).tolist()], dtype=torch.int32, device=DEV)
+    out_p = torch.empty_like(out)
+    _native.pool_normalize_packed(packed.data_ptr(), dt, cu.data_ptr(), B, H, n_instr, out_p.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(out_p, nan=7.0), torch.nan_to_num(out, nan=7.0))
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])

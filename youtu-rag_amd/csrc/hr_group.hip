@@ -584,6 +584,8 @@ struct GroupPipe {
     std::vector<std::thread> workers;
     std::vector<std::unique_ptr<WorkerQ>> qs;
     std::vector<hipStream_t> tail;                     // per shard: select + rescore + candidate copy
+    std::vector<hipStream_t> scan;                     // per shard: prep + SAMPLE + FILTER (null = its own stream)
+    std::vector<hipStream_t> owned;                    // streams shared by the shards of one device
     hipStream_t merge = nullptr;                       // primary: merge + flag copy
     std::mutex m;                                      // slot state (pending / err)
     std::condition_variable cv;
@@ -625,6 +627,7 @@ static int pipe_shard(hr_index* g, int s, GroupPipe::Slot& sl) {
         bound = sl.sh_bound[(size_t)s].as<double>();
     }
     hipStream_t tail = p->tail[(size_t)s];
+    hipStream_t scan = p->scan[(size_t)s] ? p->scan[(size_t)s] : sh->stream;
     if (sh->n_live == 0) {  // nothing here: no candidates, bound -inf (tail stream, after the queries)
         std::vector<Cand> c((size_t)sl.B * sl.kc, Cand{-INFINITY, -1});
         std::vector<double> b((size_t)sl.B, -INFINITY);
@@ -644,9 +647,10 @@ static int pipe_shard(hr_index* g, int s, GroupPipe::Slot& sl) {
             qs = sl.sh_q[(size_t)s].as<float>();
             ready = sl.sh_q_ready[(size_t)s];
         } else if (hipEventQuery(ready) != hipSuccess) {
-            HIP_TRY(hipStreamWaitEvent(sh->stream, ready, 0));  // the scan stream's prep reads them
+            HIP_TRY(hipStreamWaitEvent(scan, ready, 0));  // the scan stream's prep reads them
         }
-        if (int rc = index_shard_search_async(sh, qs, sl.B, sl.kc, cand, bound, sh->stream, tail, ready)) return rc;
+        if (!local && scan != sh->stream) HIP_TRY(hipStreamWaitEvent(scan, ready, 0));
+        if (int rc = index_shard_search_async(sh, qs, sl.B, sl.kc, cand, bound, scan, tail, ready)) return rc;
         if (!local) {
             HIP_TRY(hipMemcpyPeerAsync(sl.cand.as<Cand>() + (size_t)s * sl.B * sl.kc, g->device, cand, sh->device, cb,
                                        tail));
@@ -738,6 +742,11 @@ static void pipe_stop(hr_index* g) {
         (void)hipSetDevice(g->shards[(size_t)s]->device);
         if (p->tail[(size_t)s]) (void)hipStreamDestroy(p->tail[(size_t)s]);
     }
+    for (size_t i = 0; i < p->owned.size(); ++i) {
+        for (int s = 0; s < g->G; ++s)
+            if (p->scan[(size_t)s] == p->owned[i]) (void)hipSetDevice(g->shards[(size_t)s]->device);
+        (void)hipStreamDestroy(p->owned[i]);
+    }
     (void)hipSetDevice(g->device);
     if (p->merge) (void)hipStreamDestroy(p->merge);
     delete p;
@@ -750,6 +759,7 @@ static int pipe_start(hr_index* g) {
     g->pipe = p;
     const int G = g->G;
     p->tail.assign((size_t)G, nullptr);
+    p->scan.assign((size_t)G, nullptr);
     p->shard_us.assign((size_t)G, 0.0);
     for (int i = 0; i < GroupPipe::kSlots; ++i) {
         GroupPipe::Slot& sl = p->slot[i];
@@ -770,6 +780,34 @@ static int pipe_start(hr_index* g) {
         for (int i = 0; i < GroupPipe::kSlots && e == hipSuccess; ++i) {
             e = hipEventCreateWithFlags(&p->slot[i].sh_done[(size_t)s], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&p->slot[i].sh_q_ready[(size_t)s], hipEventDisableTiming);
+        }
+    }
+    // Shards sharing a device (dev_ids repeated) go on n scan streams of that device, dealt round-robin,
+    // instead of one stream each: consecutive shards' FILTERs then overlap pairwise (one's ramp / tail
+    // under the other's body, as the dual FILTER streams of one index do) and no hardware queue
+    // (GPU_MAX_HW_QUEUES = 4) interleaves many shards' waits.  8 x 1.25M rows on one GPU: 3.73 ms/batch
+    // with a stream per shard, 3.88 with n = 1, 3.37 with n = 2, 3.58 with n = 4
+    // (profiles/r03_group_scan_streams.log).  HIPRAG_GROUP_SCAN_STREAMS = n (0: a stream per shard)
+    static const int gss_env = getenv("HIPRAG_GROUP_SCAN_STREAMS") ? atoi(getenv("HIPRAG_GROUP_SCAN_STREAMS")) : 2;
+    if (gss_env > 0) {
+        std::vector<std::pair<int, int>> made;  // (device, index) of p->owned
+        for (int s = 0; s < G && e == hipSuccess; ++s) {
+            hr_index* sh = g->shards[(size_t)s];
+            if (!sh->shared_dev) continue;
+            int r = 0;
+            for (int t = 0; t < s; ++t) r += g->shards[(size_t)t]->device == sh->device;
+            const std::pair<int, int> key{sh->device, r % gss_env};
+            size_t i = 0;
+            while (i < made.size() && made[i] != key) ++i;
+            if (i == made.size()) {
+                hipStream_t x = nullptr;
+                e = hipSetDevice(sh->device);
+                if (e == hipSuccess) e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+                if (e != hipSuccess) break;
+                made.push_back(key);
+                p->owned.push_back(x);
+            }
+            p->scan[(size_t)s] = p->owned[i];
         }
     }
     if (e == hipSuccess) e = hipSetDevice(g->device);

@@ -35,6 +35,24 @@ __global__ __launch_bounds__(256) void k_pool_sum(const void* __restrict__ hidde
     out[(int64_t)b * H + h] = s / d;
 }
 
+// packed (unpadded) hidden states: sequence b is rows [cu[b], cu[b+1]) of an (N, H) matrix, every row a
+// real token; the first n_instr of them are masked out.  Same sums, in the same order, as k_pool_sum
+// over the padded batch (whose masked positions add exact zeros).
+template <int DT>
+__global__ __launch_bounds__(256) void k_pool_sum_packed(const void* __restrict__ hidden, const int32_t* __restrict__ cu,
+                                                         int H, int n_instr, float* __restrict__ out) {
+    const int b = blockIdx.x;
+    const int h = blockIdx.y * 256 + threadIdx.x;
+    if (h >= H) return;
+    const int64_t t1 = cu[b + 1];
+    float s = 0.f, d = 0.f;
+    for (int64_t t = (int64_t)cu[b] + n_instr; t < t1; ++t) {
+        s += ld<DT>(hidden, t * H + h);
+        d += 1.f;
+    }
+    out[(int64_t)b * H + h] = s / d;
+}
+
 __global__ __launch_bounds__(256) void k_l2norm(float* __restrict__ x, int H) {
     __shared__ float red[4];
     const int b = blockIdx.x;
@@ -263,6 +281,21 @@ extern "C" int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_
         case HR_F32: hipLaunchKernelGGL(k_pool_sum<hr::F32>, grid, dim3(256), 0, st, hidden_dev, mask_dev, T, H, n_instr, out_dev); break;
         case HR_BF16: hipLaunchKernelGGL(k_pool_sum<hr::BF16>, grid, dim3(256), 0, st, hidden_dev, mask_dev, T, H, n_instr, out_dev); break;
         case HR_F16: hipLaunchKernelGGL(k_pool_sum<hr::F16>, grid, dim3(256), 0, st, hidden_dev, mask_dev, T, H, n_instr, out_dev); break;
+        default: return HR_E_INVALID;
+    }
+    hipLaunchKernelGGL(k_l2norm, dim3((unsigned)B), dim3(256), 0, st, out_dev, H);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
+extern "C" int hr_pool_normalize_packed(const void* hidden_dev, int dtype, const int32_t* cu_dev, int B, int H,
+                                        int n_instr, float* out_dev, void* stream) {
+    if (!hidden_dev || !cu_dev || !out_dev || B <= 0 || H <= 0 || n_instr < 0) return HR_E_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)B, (unsigned)((H + 255) / 256));
+    switch (dtype) {
+        case HR_F32: hipLaunchKernelGGL(k_pool_sum_packed<hr::F32>, grid, dim3(256), 0, st, hidden_dev, cu_dev, H, n_instr, out_dev); break;
+        case HR_BF16: hipLaunchKernelGGL(k_pool_sum_packed<hr::BF16>, grid, dim3(256), 0, st, hidden_dev, cu_dev, H, n_instr, out_dev); break;
+        case HR_F16: hipLaunchKernelGGL(k_pool_sum_packed<hr::F16>, grid, dim3(256), 0, st, hidden_dev, cu_dev, H, n_instr, out_dev); break;
         default: return HR_E_INVALID;
     }
     hipLaunchKernelGGL(k_l2norm, dim3((unsigned)B), dim3(256), 0, st, out_dev, H);

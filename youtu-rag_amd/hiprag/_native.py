@@ -39,7 +39,7 @@ EXPORTS = [
     "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_add_device",
     "hr_index_remove", "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows",
     "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_pool_normalize_packed", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
@@ -111,6 +111,7 @@ def load_library(path: str | None = None):
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_merge_candidates_strided": [i32, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
+            "hr_pool_normalize_packed": [vp, i32, vp, i32, i32, i32, vp, vp],
             "hr_index_last_scan_ms": [vp, vp, vp],
             "hr_index_take_scan_times": [vp, vp, vp, i32, vp],
             "hr_index_set_scan_timing": [vp, i32],
@@ -449,6 +450,14 @@ def pool_normalize(hidden_ptr: int, dtype: str, mask_ptr: int, B: int, T: int, H
     _check(load_library().hr_pool_normalize(ctypes.c_void_p(hidden_ptr), DTYPES[dtype], ctypes.c_void_p(mask_ptr),
                                             int(B), int(T), int(H), int(n_instr), ctypes.c_void_p(out_ptr),
                                             ctypes.c_void_p(stream or None)))
+
+
+def pool_normalize_packed(hidden_ptr: int, dtype: str, cu_ptr: int, B: int, H: int, n_instr: int, out_ptr: int,
+                          stream: int = 0) -> None:
+    """K7 over packed hidden states (rows [cu[b], cu[b+1]) are sequence b; cu: B+1 int32 on the device)."""
+    _check(load_library().hr_pool_normalize_packed(ctypes.c_void_p(hidden_ptr), DTYPES[dtype], ctypes.c_void_p(cu_ptr),
+                                                   int(B), int(H), int(n_instr), ctypes.c_void_p(out_ptr),
+                                                   ctypes.c_void_p(stream or None)))
 
 
 def add_layernorm(x, r, weight, bias, eps: float):

@@ -2,23 +2,27 @@
 cross-encoder (PyTorch-ROCm: the one place the package computes with torch, BASELINE north_star).
 
 Hugging Face's forward runs every encoder GEMM over the padded batch (B x T positions) and masks the
-padding in attention.  Here the embeddings are computed on the padded batch (so position and token-type
-ids are exactly Hugging Face's), then only the real tokens go through the layers, packed as one
-(N, H) matrix:
-  * Q, K and V come from ONE GEMM (the three projections' weights concatenated once, (3H, H));
+padding in attention.  Here only the real tokens are computed, packed as one (N, H) matrix:
+  * the embeddings are the model's own module over the packed ids, token types and Hugging Face's
+    position ids of each token (0..L-1, or padding_idx + 1 + 0..L-1 for RoBERTa / XLM-R);
+  * Q, K and V come from ONE GEMM (the three projections' weights concatenated once, (3H, H)) and go to
+    the attention as strided views of its output;
   * attention is torch's variable-length flash attention over the packed tokens (cumulative sequence
     lengths; no mask, no padded keys), or, where it does not exist (CPU, fp32), plain SDPA per sequence;
   * the attention output and FFN blocks are the model's own modules (dense + residual + LayerNorm -- K8
     when fuse_encoder_layers patched them -- and the intermediate dense + activation), called on 2-D
     token matrices.
-Every real position's output equals the padded forward's (the padded keys carry zero weight there);
-padded positions come back as zeros, which the masked pooling (K7) and the CLS heads never read.
-The per-sequence lengths are host values (the caller built the right-padded batch on the host), so no
-device-to-host sync is needed for the packing indices or the flash kernel's maximum length.
+Every real position's output equals the padded forward's (the padded keys carry zero weight there).
+pack() builds the packed batch on the host from the tokenizer's right-padded output and uploads it in
+one pinned copy; the embedder pools it with the packed K7 (hr_pool_normalize_packed) and the
+cross-encoder's head reads each sequence's first row.  __call__ keeps the padded (B, T, H) interface
+(zeros at padded positions) for callers holding a device batch.  Lengths are host values throughout, so
+no device-to-host sync is needed for the packing or the flash kernel's maximum length.
 """
 from __future__ import annotations
 
 import os
+from typing import Any, NamedTuple
 
 import numpy as np
 
@@ -57,6 +61,7 @@ class UnpaddedEncoder:
 
         self.torch = torch
         self.emb = base_model.embeddings
+        self.device = next(base_model.parameters()).device
         self.layers = []
         p = next(base_model.parameters())
         for layer in base_model.encoder.layer:
@@ -83,6 +88,64 @@ class UnpaddedEncoder:
         return all(hasattr(sa, n) for n in ("query", "key", "value", "num_attention_heads", "attention_head_size")) \
             and not getattr(getattr(base_model, "config", None), "is_decoder", False)
 
+    def _positions(self, lengths: np.ndarray, cu: np.ndarray) -> np.ndarray:
+        """Hugging Face's position ids of the real tokens of right-padded rows: 0..L-1 (BERT's absolute
+        positions), or padding_idx + 1 + (0..L-1) for RoBERTa / XLM-R (create_position_ids_from_input_ids,
+        whose cumulative count of non-pad tokens is exactly that on a right-padded row)."""
+        n = int(cu[-1])
+        pos = np.arange(n, dtype=np.int64) - np.repeat(cu[:-1], lengths)
+        if hasattr(self.emb, "create_position_ids_from_input_ids"):
+            pos += int(self.emb.padding_idx) + 1
+        return pos
+
+    def pack(self, input_ids, attention_mask, token_type_ids=None, device=None):
+        """Host-side packing of a right-padded tokenizer batch (host tensors / arrays (B, T)): the real
+        tokens' ids, token types and positions plus the cumulative lengths, uploaded with ONE pinned
+        asynchronous copy.  Returns the Packed batch forward_packed() takes."""
+        torch = self.torch
+        ids = np.asarray(input_ids)
+        keep = np.asarray(attention_mask).astype(bool, copy=False)
+        B = ids.shape[0]
+        lengths = keep.sum(1).astype(np.int64)
+        if B and not (keep == (np.arange(ids.shape[1])[None, :] < lengths[:, None])).all():
+            raise ValueError("pack() needs right-padded rows (mask = a prefix of ones)")
+        cu = np.zeros(B + 1, np.int64)
+        cu[1:] = np.cumsum(lengths)
+        n = int(cu[-1])
+        buf = np.empty(3 * n + B + 1, np.int64)  # [ids | types | positions | cu]
+        buf[:n] = ids[keep]
+        buf[n:2 * n] = np.asarray(token_type_ids)[keep] if token_type_ids is not None else 0
+        buf[2 * n:3 * n] = self._positions(lengths, cu)
+        buf[3 * n:] = cu
+        dev = torch.device(device) if device is not None else self.device
+        t = torch.from_numpy(buf)
+        if dev.type == "cuda":
+            t = t.pin_memory()
+        t = t.to(dev, non_blocking=dev.type == "cuda")
+        return Packed(t[:n], t[n:2 * n], t[2 * n:3 * n], t[3 * n:].to(torch.int32), cu, lengths,
+                      int(lengths.max()) if B else 0)
+
+    def forward_packed(self, pk: "Packed"):
+        """Last hidden state of the packed real tokens, (N, H) (row cu[b] + t is token t of sequence b)."""
+        n = int(pk.cu_host[-1])
+        for f in self.observers:
+            f(len(pk.lengths), pk.max_len, pk.lengths)
+        x = self.emb(input_ids=pk.ids[None], token_type_ids=pk.types[None], position_ids=pk.pos[None])[0]
+        return self._layers(x, pk.cu, pk.cu_host, pk.max_len, n)
+
+    def _layers(self, h, cu_t, cu_host, max_len, n):
+        torch = self.torch
+        for w, b, nH, d, scale, attn_out, inter, out in self.layers:
+            qkv = torch.nn.functional.linear(h, w, b).view(n, 3, nH, d)
+            q, k, v = qkv.unbind(1)  # strided views: the flash kernel takes them as they are (no copies)
+            if self.varlen is not None and abs(scale * d ** 0.5 - 1.0) < 1e-6:  # (the kernel's own 1/sqrt(d))
+                a = self.varlen(q, k, v, cu_t, cu_t, max_len, max_len)
+            else:
+                a = _sdpa_per_sequence(q, k, v, cu_host, max_len, scale)
+            h = attn_out(a.reshape(n, nH * d), h)
+            h = out(inter(h), h)
+        return h
+
     def __call__(self, input_ids, lengths, token_type_ids=None):
         """input_ids (B, T) device, right-padded; lengths: host int array (B,) of real tokens per row.
         Returns the last hidden state (B, T, H) with zeros at padded positions."""
@@ -95,30 +158,43 @@ class UnpaddedEncoder:
         n = int(cu[-1])
         idx_h = (np.repeat(np.arange(B, dtype=np.int64) * T, lengths)
                  + np.arange(n, dtype=np.int64) - np.repeat(cu[:-1], lengths))
-        pin = dev.type == "cuda"
-        idx = torch.from_numpy(idx_h)
-        cu_t = torch.from_numpy(cu.astype(np.int32))
-        if pin:
-            idx, cu_t = idx.pin_memory(), cu_t.pin_memory()
-        idx, cu_t = idx.to(dev, non_blocking=pin), cu_t.to(dev, non_blocking=pin)
-        max_len = int(lengths.max()) if B else 0
-        for f in self.observers:
-            f(B, T, lengths)
-        x = self.emb(input_ids=input_ids, token_type_ids=token_type_ids)  # Hugging Face's positions / types
-        H = x.shape[-1]
-        h = x.reshape(B * T, H).index_select(0, idx)
-        for w, b, nH, d, scale, attn_out, inter, out in self.layers:
-            qkv = torch.nn.functional.linear(h, w, b).view(n, 3, nH, d)
-            q, k, v = (qkv[:, i].contiguous() for i in range(3))
-            if self.varlen is not None and abs(scale * d ** 0.5 - 1.0) < 1e-6:  # (the kernel's own 1/sqrt(d))
-                a = self.varlen(q, k, v, cu_t, cu_t, max_len, max_len)
-            else:
-                a = _sdpa_per_sequence(q, k, v, cu, max_len, scale)
-            h = attn_out(a.reshape(n, nH * d), h)
-            h = out(inter(h), h)
-        seq = x.new_zeros(B * T, H)
+        host = np.concatenate([idx_h, self._positions(lengths, cu), cu])
+        t = torch.from_numpy(host)
+        if dev.type == "cuda":
+            t = t.pin_memory()
+        t = t.to(dev, non_blocking=dev.type == "cuda")
+        idx, pos, cu_t = t[:n], t[n:2 * n], t[2 * n:].to(torch.int32)
+        ids_p = input_ids.reshape(-1).index_select(0, idx)
+        types_p = token_type_ids.reshape(-1).index_select(0, idx) if token_type_ids is not None \
+            else torch.zeros_like(ids_p)
+        pk = Packed(ids_p, types_p, pos, cu_t, cu, lengths, int(lengths.max()) if B else 0)
+        h = self.forward_packed(pk)
+        seq = h.new_zeros(B * T, h.shape[-1])
         seq.index_copy_(0, idx, h)
-        return seq.view(B, T, H)
+        return seq.view(B, T, -1)
+
+
+class Packed(NamedTuple):
+    """A packed batch on the device (ids, types, pos: (N,) int64; cu: (B+1,) int32) with its host
+    offsets and lengths."""
+    ids: Any
+    types: Any
+    pos: Any
+    cu: Any
+    cu_host: np.ndarray
+    lengths: np.ndarray
+    max_len: int
+
+
+def first_tokens(h, cu_host, device=None):
+    """(B, 1, H) view-like gather of each packed sequence's first token (the [CLS] / <s> position the
+    poolers and classification heads read)."""
+    import torch
+
+    idx = torch.from_numpy(np.ascontiguousarray(cu_host[:-1]))
+    if h.is_cuda:
+        idx = idx.pin_memory().to(h.device, non_blocking=True)
+    return h.index_select(0, idx)[:, None, :]
 
 
 def sequence_logits(model, seq, probe: bool = False):

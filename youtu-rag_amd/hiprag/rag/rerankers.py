@@ -242,16 +242,16 @@ class TorchRocmReranker(BaseReranker):
                 L = total[sel][:, None]
                 mask = (col < L).astype(np.int64)
                 types = ((col >= (s1 + 2)[:, None]) & (col < L) & has_b[:, None]).astype(np.int64)
-                t_ids, t_mask, t_types = (torch.from_numpy(x) for x in (ids, mask, types))
-                if pin:
-                    t_ids, t_mask, t_types = (t.pin_memory() for t in (t_ids, t_mask, t_types))
-                if self.unpadded is not None:
-                    from .encoder import sequence_logits
+                if self.unpadded is not None:  # real tokens only: packed on the host, one upload
+                    from .encoder import first_tokens, sequence_logits
 
-                    seq = self.unpadded(t_ids.to(self.device, non_blocking=pin), total[sel],
-                                        t_types.to(self.device, non_blocking=pin))
-                    logits = sequence_logits(self.model, seq)
+                    pk = self.unpadded.pack(ids, mask, types)
+                    h = self.unpadded.forward_packed(pk)
+                    logits = sequence_logits(self.model, first_tokens(h, pk.cu_host))
                 else:
+                    t_ids, t_mask, t_types = (torch.from_numpy(x) for x in (ids, mask, types))
+                    if pin:
+                        t_ids, t_mask, t_types = (t.pin_memory() for t in (t_ids, t_mask, t_types))
                     logits = self.model(input_ids=t_ids.to(self.device, non_blocking=pin),
                                         attention_mask=t_mask.to(self.device, non_blocking=pin),
                                         token_type_ids=t_types.to(self.device, non_blocking=pin)).logits

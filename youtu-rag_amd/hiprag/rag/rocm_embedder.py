@@ -211,12 +211,16 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.query_instruction = (f"Instruction: {query_instruction} \nQuery:" if query_instruction else "Query:")
         self.doc_instruction = ""
         self.dim = int(getattr(getattr(model, "config", None), "hidden_size", 0)) or None
+        self._n_instr: dict[str, int] = {}  # instruction -> its token count (fixed per tokenizer)
 
     # ------------------------------------------------------------------ core
     def _n_instruction_tokens(self, instruction: str) -> int:
-        ids = self.tokenizer(instruction, padding=False, truncation=True, max_length=self.max_length,
-                             add_special_tokens=True)["input_ids"]
-        return len(ids)
+        n = self._n_instr.get(instruction)
+        if n is None:
+            n = self._n_instr[instruction] = len(self.tokenizer(instruction, padding=False, truncation=True,
+                                                                max_length=self.max_length,
+                                                                add_special_tokens=True)["input_ids"])
+        return n
 
     def _pool(self, hidden, mask, n_instr: int):
         """K7: masked mean-pool + L2 normalise on the GPU -> (B, H) float32."""
@@ -235,18 +239,28 @@ class TorchRocmEmbedder(BaseEmbedder):
         # pinned staging: the H2D copy is then truly asynchronous, so the host tokenises batch i+1
         # while the GPU runs batch i's forward (a pageable copy waits for the stream to drain)
         pin = self.device.type == "cuda" and _PIN
-        lengths = inputs["attention_mask"].sum(1).numpy() if self.unpadded is not None else None
+        n_instr = self._n_instruction_tokens(instruction)
+        if self.unpadded is not None:  # real tokens only: packed on the host, one upload, packed K7
+            with torch.inference_mode():
+                pk = self.unpadded.pack(inputs["input_ids"], inputs["attention_mask"], inputs.get("token_type_ids"))
+                hidden = self.unpadded.forward_packed(pk)
+                if hidden.dtype != getattr(torch, self.dtype_name):
+                    hidden = hidden.to(getattr(torch, self.dtype_name))
+                hidden = hidden.contiguous()
+                B, H = len(pk.lengths), hidden.shape[-1]
+                out = torch.empty((B, H), dtype=torch.float32, device=hidden.device)
+                _native.pool_normalize_packed(hidden.data_ptr(), _K7_DTYPE[self.dtype_name], pk.cu.data_ptr(), B, H,
+                                              n_instr, out.data_ptr(),
+                                              torch.cuda.current_stream(hidden.device).cuda_stream)
+                return out
         inputs = {k: (v.pin_memory() if pin else v).to(self.device, non_blocking=True) for k, v in inputs.items()}
         with torch.inference_mode():
-            if self.unpadded is not None:
-                hidden = self.unpadded(inputs["input_ids"], lengths, inputs.get("token_type_ids"))
-            else:
-                hidden = self.model(**inputs)[0]
+            hidden = self.model(**inputs)[0]
             if hidden.dtype != getattr(torch, self.dtype_name):
                 hidden = hidden.to(getattr(torch, self.dtype_name))
             hidden = hidden.contiguous()
             mask = inputs["attention_mask"].to(torch.int32).contiguous()
-            return self._pool(hidden, mask, self._n_instruction_tokens(instruction))
+            return self._pool(hidden, mask, n_instr)
 
     def _encode_all(self, texts: list[str], prefix: str, instruction: str):
         torch = self.torch

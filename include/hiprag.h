@@ -202,6 +202,13 @@ int hr_pool_normalize(const void* hidden_dev, int dtype, const int32_t* mask_dev
  * sums as hr_pool_normalize on the right-padded batch.  The in-process embedder's unpadded forward. */
 int hr_pool_normalize_packed(const void* hidden_dev, int dtype, const int32_t* cu_dev, int B, int H, int n_instr,
                              float* out_dev, void* stream);
+/* Host (no GPU): the offline tokenizer's word split + crc32 word hash over n_texts ASCII texts (bytes
+ * [offsets[i], offsets[i+1]) of `text`): lower-cased \w+ | [^\w\s] tokens -> first_id + crc32 % span,
+ * at most `cap` per text (cap < 0: all), wrapped in cls_id ... sep_id when both are >= 0.  ids_out
+ * (capacity ids_cap) receives the texts' ids back to back, lengths_out[i] each text's count.
+ * HR_E_INVALID for a non-ASCII byte or a full ids_out.  (hiprag.rag.rocm_embedder.HashWordTokenizer) */
+int hr_hash_words(const char* text, const int64_t* offsets, int64_t n_texts, int64_t first_id, int64_t span, int64_t cap,
+                  int64_t cls_id, int64_t sep_id, int64_t* ids_out, int64_t ids_cap, int64_t* lengths_out);
 /* K8: out = LayerNorm(x + r) * gamma + beta over rows x H (H <= 4096), dtype of x, r, gamma, beta and
  * out (HR_F32 / HR_BF16 / HR_F16); the encoder layers' residual add + LayerNorm fused
  * (BertSelfOutput / BertOutput, modeling_bert.py; XLM-R the same).  Ordered on `stream`. */

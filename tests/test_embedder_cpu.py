@@ -145,3 +145,31 @@ def test_ingestor_batches_across_documents_and_replaces_old_chunks(tmp_path):
                                                                                    "source": "c.md"}))
     assert [c.content for c in hc] == ["# T\n## S\n\nline a\nline b"]
     assert hc[0].metadata == {"source": "c.md", "index_type": "index_content"} and hc[0].id == "h_chunk_0"
+
+
+def test_hash_tokenizer_native_text_kernel_matches_python():
+    """hr_hash_words (the host text kernel ASCII batches take) gives the ids of the re + zlib path:
+    every ASCII whitespace class, punctuation, digits, underscores, control bytes, truncation with
+    and without special tokens; batches with a non-ASCII text stay on the Python path."""
+    import random
+
+    from hiprag.rag import rocm_embedder as re_mod
+
+    rnd = random.Random(11)
+    alpha = "abcXYZ0189_ ,.!?;:'\"()-\t\n\x0b\x0c\r\x1c\x1d\x1e\x1f\x7f\x00@#$%^&*[]{}|\\/~`"
+    texts = ["".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 400))) for _ in range(60)] + ["", " \t "]
+    tok = HashWordTokenizer()
+    old = re_mod._NATIVE_TOK
+    try:
+        for max_length, special in ((8, True), (512, True), (None, True), (6, False)):
+            kw = dict(padding=True, truncation=max_length is not None, max_length=max_length, return_tensors="pt",
+                      add_special_tokens=special)
+            re_mod._NATIVE_TOK = True
+            assert tok._native_batch(texts, None, special) is not None
+            a = tok(texts, **kw)
+            re_mod._NATIVE_TOK = False
+            b = tok(texts, **kw)
+            assert torch.equal(a["input_ids"], b["input_ids"]) and torch.equal(a["attention_mask"], b["attention_mask"])
+        assert tok._native_batch(texts + ["naïve"], None, True) is None
+    finally:
+        re_mod._NATIVE_TOK = old

@@ -518,7 +518,10 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // per-step host submission bounds such small collections -- so the default keeps 2048
     static const int sfrac_env = getenv("HIPRAG_SAMPLE_FRAC") ? atoi(getenv("HIPRAG_SAMPLE_FRAC")) : 0;
     auto sample_target = [&](int64_t n) {
-        const int64_t smin = smin_env > 0 ? smin_env : 2048;
+        // a shard sharing its GPU with other shards of a group samples 512 tiles: the co-located shards'
+        // SAMPLEs add up (8 x 1.25M rows on one GPU: 3.387 / 3.308 / 3.297 ms per batch at 2048 / 1024 /
+        // 512, profiles/r03_group_scan_streams.log)
+        const int64_t smin = smin_env > 0 ? smin_env : (h->shared_dev ? 512 : 2048);
         const int64_t small = sfrac_env > 0 ? std::max<int64_t>(64, n / sfrac_env) : smin;
         return std::max<int64_t>(std::min<int64_t>(smin, small), n / (sdiv_env > 0 ? sdiv_env : 128));
     };

@@ -39,7 +39,7 @@ EXPORTS = [
     "hr_index_create", "hr_index_reserve", "hr_index_add", "hr_index_add_synthetic", "hr_index_add_device",
     "hr_index_remove", "hr_index_search", "hr_index_search_device", "hr_index_size", "hr_index_get_rows",
     "hr_index_save", "hr_index_load", "hr_index_destroy", "hr_index_search_shard", "hr_index_search_shard_collect",
-    "hr_merge_candidates", "hr_pool_normalize", "hr_pool_normalize_packed", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
+    "hr_merge_candidates", "hr_pool_normalize", "hr_pool_normalize_packed", "hr_hash_words", "hr_index_set_scan_timing", "hr_index_take_scan_times", "hr_index_last_scan_ms",
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
@@ -112,6 +112,7 @@ def load_library(path: str | None = None):
             "hr_merge_candidates_strided": [i32, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
             "hr_pool_normalize_packed": [vp, i32, vp, i32, i32, i32, vp, vp],
+            "hr_hash_words": [vp, vp, i64, i64, i64, i64, i64, i64, vp, i64, vp],
             "hr_index_last_scan_ms": [vp, vp, vp],
             "hr_index_take_scan_times": [vp, vp, vp, i32, vp],
             "hr_index_set_scan_timing": [vp, i32],
@@ -458,6 +459,23 @@ def pool_normalize_packed(hidden_ptr: int, dtype: str, cu_ptr: int, B: int, H: i
     _check(load_library().hr_pool_normalize_packed(ctypes.c_void_p(hidden_ptr), DTYPES[dtype], ctypes.c_void_p(cu_ptr),
                                                    int(B), int(H), int(n_instr), ctypes.c_void_p(out_ptr),
                                                    ctypes.c_void_p(stream or None)))
+
+
+def hash_words(data: bytes, offsets, first_id: int, span: int, cap: int = -1, cls_id: int = -1, sep_id: int = -1):
+    """Host text kernel of the offline tokenizer (hr_hash_words): ASCII texts packed in `data` with int64
+    `offsets` (n+1) -> (ids int64 flat, lengths int64 (n,)).  No GPU involved."""
+    import numpy as np
+
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    n = len(offsets) - 1
+    cap_ids = len(data) + 2 * n + 1  # every token takes at least one byte
+    ids = np.empty(cap_ids, np.int64)
+    lengths = np.empty(max(n, 0), np.int64)
+    _check(load_library().hr_hash_words(data, offsets.ctypes.data_as(ctypes.c_void_p), int(n), int(first_id),
+                                        int(span), int(cap), int(cls_id), int(sep_id),
+                                        ids.ctypes.data_as(ctypes.c_void_p), int(cap_ids),
+                                        lengths.ctypes.data_as(ctypes.c_void_p)))
+    return ids[:int(lengths.sum())], lengths
 
 
 def add_layernorm(x, r, weight, bias, eps: float):

@@ -51,6 +51,10 @@ _K7_DTYPE = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
 _PIN = os.environ.get("HIPRAG_EMBED_PIN", "1") != "0"  # A/B switch for the pinned token staging
 
 
+# batches of ASCII texts go through the host text kernel (hr_hash_words; same ids), the rest through re + zlib
+_NATIVE_TOK = os.environ.get("HIPRAG_NATIVE_TOKENIZER", "1") != "0"
+
+
 class HashWordTokenizer:
     """Deterministic offline tokenizer for random-init models (no vocab files exist offline).
 
@@ -83,31 +87,49 @@ class HashWordTokenizer:
             ids = [self._hash(w) if i is None else i for w, i in zip(words, ids)]
         return ids
 
+    def _native_batch(self, texts: list[str], cap, add_special_tokens: bool):
+        """(flat ids, lengths) of all-ASCII texts from the host text kernel (hr_hash_words), else None."""
+        if len(texts) < 8 or not all(t.isascii() for t in texts):
+            return None
+        data = "".join(texts).encode("ascii")
+        offs = np.zeros(len(texts) + 1, np.int64)
+        np.cumsum(np.fromiter(map(len, texts), np.int64, len(texts)), out=offs[1:])
+        sp = add_special_tokens
+        return _native.hash_words(data, offs, self.first_id, self.vocab_size - self.first_id,
+                                  -1 if cap is None else cap, self.cls_token_id if sp else -1,
+                                  self.sep_token_id if sp else -1)
+
     def __call__(self, text, padding=False, truncation=False, max_length=None, return_tensors=None,
                  add_special_tokens=True, **_):
         single = isinstance(text, str)
         texts = [text] if single else list(text)
         cap = max(0, int(max_length) - (2 if add_special_tokens else 0)) if truncation and max_length is not None \
             else None
+        packed = self._native_batch(texts, cap, add_special_tokens) if return_tensors == "pt" and _NATIVE_TOK \
+            else None
         seqs = []
-        for t in texts:
-            ids = self._ids(t)
-            if cap is not None:
-                del ids[cap:]
-            if add_special_tokens:
-                ids.insert(0, self.cls_token_id)
-                ids.append(self.sep_token_id)
-            seqs.append(ids)
+        if packed is None:
+            for t in texts:
+                ids = self._ids(t)
+                if cap is not None:
+                    del ids[cap:]
+                if add_special_tokens:
+                    ids.insert(0, self.cls_token_id)
+                    ids.append(self.sep_token_id)
+                seqs.append(ids)
         if return_tensors == "pt":  # one (B, W) numpy fill, no nested-list tensor build
             import torch
 
-            lens = np.fromiter((len(s) for s in seqs), np.int64, len(seqs))
-            width = int(lens.max()) if padding and len(seqs) else None
+            if packed is not None:
+                flat, lens = packed
+            else:
+                lens = np.fromiter((len(s) for s in seqs), np.int64, len(seqs))
+                flat = np.fromiter(itertools.chain.from_iterable(seqs), np.int64, int(lens.sum()))
+            width = int(lens.max()) if padding and len(lens) else None
             if width is None and len(set(lens.tolist())) > 1:
                 raise ValueError("return_tensors='pt' needs padding=True for ragged inputs")
-            width = width if width is not None else (int(lens[0]) if len(seqs) else 0)
-            ids_np = np.full((len(seqs), width), self.pad_token_id, np.int64)
-            flat = np.fromiter(itertools.chain.from_iterable(seqs), np.int64, int(lens.sum()))
+            width = width if width is not None else (int(lens[0]) if len(lens) else 0)
+            ids_np = np.full((len(lens), width), self.pad_token_id, np.int64)
             mask_np = np.arange(width)[None, :] < lens[:, None]
             ids_np[mask_np] = flat
             return {"input_ids": torch.from_numpy(ids_np), "attention_mask": torch.from_numpy(mask_np.astype(np.int64))}

@@ -173,3 +173,25 @@ def test_hash_tokenizer_native_text_kernel_matches_python():
         assert tok._native_batch(texts + ["naïve"], None, True) is None
     finally:
         re_mod._NATIVE_TOK = old
+
+
+def test_ingest_pauses_the_cyclic_gc_and_restores_it(tmp_path):
+    import gc
+
+    seen = []
+
+    class GcProbe(HashEmbedder):
+        async def embed_texts(self, texts):
+            seen.append(gc.isenabled())
+            return await super().embed_texts(texts)
+
+    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
+                            index_params={"dtype": "f32", "persist": False})
+    store = HipVectorStore(cfg, index_factory=lambda d: OracleIndex(d, "f32"))
+    docs = [Document(id=f"d{i}", content="alpha beta gamma " * 20, metadata={}) for i in range(3)]
+    assert gc.isenabled()
+    run(GpuIngestor(store, GcProbe(), chunking=ChunkingConfig(chunk_size=100, chunk_overlap=0)).ingest(docs))
+    assert seen and not any(seen) and gc.isenabled()
+    seen.clear()
+    run(GpuIngestor(store, GcProbe(), pause_gc=False).ingest(docs[:1]))
+    assert seen and all(seen) and gc.isenabled()

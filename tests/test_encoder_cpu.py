@@ -95,3 +95,17 @@ def test_packed_cross_encoder_head_and_left_padding_refused():
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
     with pytest.raises(ValueError):
         enc.pack(ids, mask.flip(1))
+
+
+def test_pack_of_several_batches_is_their_concatenation():
+    torch.manual_seed(0)
+    model = build_random_bert("tiny", 3).eval()
+    enc = UnpaddedEncoder(model, use_varlen=False)
+    rng = np.random.default_rng(10)
+    (i1, m1, l1), (i2, m2, l2) = _batch(rng, 3, 12), _batch(rng, 4, 30)
+    with torch.inference_mode():
+        both = enc.pack([i1, i2], [m1, m2])
+        h = enc.forward_packed(both)
+        a, b = enc.forward_packed(enc.pack(i1, m1)), enc.forward_packed(enc.pack(i2, m2))
+    assert both.lengths.tolist() == [*l1.tolist(), *l2.tolist()] and both.max_len == 30
+    torch.testing.assert_close(h, torch.cat([a, b]), rtol=1e-5, atol=2e-5)

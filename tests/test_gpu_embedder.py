@@ -200,3 +200,8 @@ def test_unpadded_embedder_matches_padded(dtype):
     torch.testing.assert_close(x, y, rtol=0, atol=2e-2)
     assert float((x * y).sum(1).min()) > 0.999
     torch.testing.assert_close(a.encode_queries(texts[:5]), b.encode_queries(texts[:5]), rtol=0, atol=2e-2)
+    # several tokenizer batches per forward (forward_tokens): the same sequences through bigger GEMMs
+    a.forward_tokens = 1000
+    z = a.encode_passages(texts)
+    torch.testing.assert_close(z, x, rtol=0, atol=2e-2)
+    assert float((z * x).sum(1).min()) > 0.9999

@@ -99,22 +99,35 @@ class UnpaddedEncoder:
         return pos
 
     def pack(self, input_ids, attention_mask, token_type_ids=None, device=None):
-        """Host-side packing of a right-padded tokenizer batch (host tensors / arrays (B, T)): the real
-        tokens' ids, token types and positions plus the cumulative lengths, uploaded with ONE pinned
-        asynchronous copy.  Returns the Packed batch forward_packed() takes."""
+        """Host-side packing of right-padded tokenizer batches (host tensors / arrays (B, T), or lists of
+        them -- several batches become one packed batch): the real tokens' ids, token types and
+        positions plus the cumulative lengths, uploaded with ONE pinned asynchronous copy.  Returns the
+        Packed batch forward_packed() takes."""
         torch = self.torch
-        ids = np.asarray(input_ids)
-        keep = np.asarray(attention_mask).astype(bool, copy=False)
-        B = ids.shape[0]
-        lengths = keep.sum(1).astype(np.int64)
-        if B and not (keep == (np.arange(ids.shape[1])[None, :] < lengths[:, None])).all():
-            raise ValueError("pack() needs right-padded rows (mask = a prefix of ones)")
+        many = isinstance(input_ids, (list, tuple))
+        parts = zip(input_ids, attention_mask, token_type_ids if token_type_ids is not None else [None] * len(input_ids)) \
+            if many else [(input_ids, attention_mask, token_type_ids)]
+        ids_l, types_l, lens_l = [], [], []
+        for ids, mask, types in parts:
+            ids = np.asarray(ids)
+            keep = np.asarray(mask).astype(bool, copy=False)
+            lengths = keep.sum(1).astype(np.int64)
+            if len(lengths) and not (keep == (np.arange(ids.shape[1])[None, :] < lengths[:, None])).all():
+                raise ValueError("pack() needs right-padded rows (mask = a prefix of ones)")
+            ids_l.append(ids[keep])
+            types_l.append(np.asarray(types)[keep] if types is not None else None)
+            lens_l.append(lengths)
+        lengths = np.concatenate(lens_l) if lens_l else np.zeros(0, np.int64)
+        B = len(lengths)
         cu = np.zeros(B + 1, np.int64)
         cu[1:] = np.cumsum(lengths)
         n = int(cu[-1])
         buf = np.empty(3 * n + B + 1, np.int64)  # [ids | types | positions | cu]
-        buf[:n] = ids[keep]
-        buf[n:2 * n] = np.asarray(token_type_ids)[keep] if token_type_ids is not None else 0
+        buf[:n] = np.concatenate(ids_l) if ids_l else 0
+        o = n
+        for t, ids in zip(types_l, ids_l):
+            buf[o:o + len(ids)] = t if t is not None else 0
+            o += len(ids)
         buf[2 * n:3 * n] = self._positions(lengths, cu)
         buf[3 * n:] = cu
         dev = torch.device(device) if device is not None else self.device

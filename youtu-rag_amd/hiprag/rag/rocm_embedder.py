@@ -188,7 +188,7 @@ class TorchRocmEmbedder(BaseEmbedder):
                  batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
                  trust_remote_code: bool = False, fused_layernorm: bool | None = None, unpadded: bool | None = None,
-                 **_ignored):
+                 forward_tokens: int | None = None, **_ignored):
         import torch
 
         self.torch = torch
@@ -234,6 +234,11 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.doc_instruction = ""
         self.dim = int(getattr(getattr(model, "config", None), "hidden_size", 0)) or None
         self._n_instr: dict[str, int] = {}  # instruction -> its token count (fixed per tokenizer)
+        # unpadded forwards: consecutive tokenizer batches are packed into one forward of at least this
+        # many tokens (bigger GEMMs; 0 = one forward per batch)
+        if forward_tokens is None:
+            forward_tokens = int(os.environ.get("HIPRAG_FORWARD_TOKENS", "0"))
+        self.forward_tokens = max(0, int(forward_tokens))
 
     # ------------------------------------------------------------------ core
     def _n_instruction_tokens(self, instruction: str) -> int:
@@ -263,18 +268,7 @@ class TorchRocmEmbedder(BaseEmbedder):
         pin = self.device.type == "cuda" and _PIN
         n_instr = self._n_instruction_tokens(instruction)
         if self.unpadded is not None:  # real tokens only: packed on the host, one upload, packed K7
-            with torch.inference_mode():
-                pk = self.unpadded.pack(inputs["input_ids"], inputs["attention_mask"], inputs.get("token_type_ids"))
-                hidden = self.unpadded.forward_packed(pk)
-                if hidden.dtype != getattr(torch, self.dtype_name):
-                    hidden = hidden.to(getattr(torch, self.dtype_name))
-                hidden = hidden.contiguous()
-                B, H = len(pk.lengths), hidden.shape[-1]
-                out = torch.empty((B, H), dtype=torch.float32, device=hidden.device)
-                _native.pool_normalize_packed(hidden.data_ptr(), _K7_DTYPE[self.dtype_name], pk.cu.data_ptr(), B, H,
-                                              n_instr, out.data_ptr(),
-                                              torch.cuda.current_stream(hidden.device).cuda_stream)
-                return out
+            return self._forward_packed([inputs], n_instr)
         inputs = {k: (v.pin_memory() if pin else v).to(self.device, non_blocking=True) for k, v in inputs.items()}
         with torch.inference_mode():
             hidden = self.model(**inputs)[0]
@@ -283,6 +277,39 @@ class TorchRocmEmbedder(BaseEmbedder):
             hidden = hidden.contiguous()
             mask = inputs["attention_mask"].to(torch.int32).contiguous()
             return self._pool(hidden, mask, n_instr)
+
+    def _forward_packed(self, batches: list, n_instr: int):
+        """Unpadded forward of one or more tokenizer batches as ONE packed batch -> (sum B, H) float32."""
+        torch = self.torch
+        with torch.inference_mode():
+            pk = self.unpadded.pack([b["input_ids"] for b in batches], [b["attention_mask"] for b in batches],
+                                    [b.get("token_type_ids") for b in batches])
+            hidden = self.unpadded.forward_packed(pk)
+            if hidden.dtype != getattr(torch, self.dtype_name):
+                hidden = hidden.to(getattr(torch, self.dtype_name))
+            hidden = hidden.contiguous()
+            B, H = len(pk.lengths), hidden.shape[-1]
+            out = torch.empty((B, H), dtype=torch.float32, device=hidden.device)
+            _native.pool_normalize_packed(hidden.data_ptr(), _K7_DTYPE[self.dtype_name], pk.cu.data_ptr(), B, H,
+                                          n_instr, out.data_ptr(), torch.cuda.current_stream(hidden.device).cuda_stream)
+            return out
+
+    def _encode_packs(self, texts: list[str], order: list[int], instruction: str) -> list:
+        """Unpadded path over many batches: tokenizer batches of batch_size (in `order`) gathered into
+        forwards of >= forward_tokens real tokens."""
+        n_instr = self._n_instruction_tokens(instruction)
+        outs, group, tok = [], [], 0
+        for i in range(0, len(texts), self.batch_size):
+            b = self.tokenizer([texts[j] for j in order[i:i + self.batch_size]], padding=True, truncation=True,
+                               return_tensors="pt", max_length=self.max_length, add_special_tokens=True)
+            group.append(b)
+            tok += int(b["attention_mask"].sum())
+            if tok >= self.forward_tokens:
+                outs.append(self._forward_packed(group, n_instr))
+                group, tok = [], 0
+        if group:
+            outs.append(self._forward_packed(group, n_instr))
+        return outs
 
     def _encode_all(self, texts: list[str], prefix: str, instruction: str):
         torch = self.torch
@@ -301,8 +328,11 @@ class TorchRocmEmbedder(BaseEmbedder):
         if self.device.type == "cuda" and _PIN:
             perm = perm.pin_memory()
         perm = perm.to(self.device, non_blocking=True)
-        parts = [self.encode([texts[j] for j in order[i:i + self.batch_size]], instruction)
-                 for i in range(0, len(texts), self.batch_size)]
+        if self.unpadded is not None and self.forward_tokens > 0:
+            parts = self._encode_packs(texts, order, instruction)
+        else:
+            parts = [self.encode([texts[j] for j in order[i:i + self.batch_size]], instruction)
+                     for i in range(0, len(texts), self.batch_size)]
         out = torch.empty((len(texts), parts[0].shape[1]), dtype=torch.float32, device=self.device)
         out[perm] = torch.cat(parts)
         return out

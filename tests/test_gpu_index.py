@@ -902,6 +902,67 @@ def test_query_group_edges_vs_oracle(native, dim, dtype, metric):
         _check(s, r, *oracle.c_search(stored, dtype, qn, k, oracle.mask_from_bool(live), metric=metric))
 
 
+# ---------------------------------------------------------------- the 128-query FILTER (hr_wide.hip)
+@pytest.mark.parametrize("dim,dtype,n,B,k", [(256, "bf16", 20_011, 128, 10), (512, "f16", 33_333, 97, 16),
+                                             (768, "bf16", 41_000, 129, 20), (1024, "bf16", 70_001, 256, 10),
+                                             (1024, "f16", 3_000, 80, 5), (512, "bf16", 64, 128, 3),
+                                             (1024, "bf16", 1_000_003, 128, 10)])
+def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
+    """65..256 queries at D = 256..1024 (bf16 / f16, k <= 22) take the 128-query FILTER: one workgroup per CU
+    scores every tile pair once for two 64-query groups, the queries streaming through LDS in depth
+    windows.  Odd tile counts (a pair's second tile read through a one-tile V#), fewer pairs than waves (idle
+    waves walk the windows on zero-record V#s), a padded second set (B = 129, 80, 97), a mask, deleted rows,
+    ip scores: identical to the oracle and to the same queries 64 at a time."""
+    rng = np.random.default_rng(dim + B + n)
+    # (raw inner products of the synthetic rows overflow f16 storage: ip on bf16 only)
+    for metric in ("cosine", "ip") if dtype == "bf16" else ("cosine",):
+        idx = native.NativeIndex(dim, dtype, metric)
+        idx.add_synthetic(9, 0, n)
+        raw = R.gen_rows(9, 0, n, dim)
+        nq = min(B // 2, n)
+        q = np.concatenate([_planted_queries(raw, nq, rng), rng.standard_normal((B - nq, dim)).astype(np.float32)])
+        stored = oracle.c_build_synthetic(9, 0, n, dim, dtype, metric)
+        qn = R.process_queries(q, metric)
+        allowed = rng.random(n) < 0.7
+        for m in (None, allowed):
+            mk = None if m is None else oracle.mask_from_bool(m)
+            s, r = idx.search(q, k, mk)
+            _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk, metric=metric))
+        parts = [idx.search(q[i:i + 64], k) for i in range(0, B, 64)]
+        s, r = idx.search(q, k)
+        np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))
+        if n > 1000:
+            gone = np.arange(n // 3, n // 3 + n // 7)
+            idx.remove(gone)
+            live = np.ones(n, bool)
+            live[gone] = False
+            s, r = idx.search(q, k)
+            _check(s, r, *oracle.c_search(stored, dtype, qn, k, oracle.mask_from_bool(live), metric=metric))
+        if n > 500_000:
+            break  # (one metric at a million rows)
+
+
+def test_wide_filter_periodic_clusters(native):
+    """The 128-query FILTER deals tile pairs round-robin with each full round rotated by a hash of the
+    round: clusters repeating every 4096 rows (a factor of the wave count) still reach every wave, so the
+    32-slot private regions hold and the guard passes for nearly every query; identical to the oracle."""
+    dim, n, B, C = 256, 2_000_000, 128, 4096
+    rng = np.random.default_rng(23)
+    centers = rng.standard_normal((C, dim)).astype(np.float32)
+    centers /= np.linalg.norm(centers, axis=1, keepdims=True)
+    noise = R.gen_rows(43, 0, n, dim)
+    noise /= np.linalg.norm(noise, axis=1, keepdims=True)
+    raw = centers[(np.arange(n, dtype=np.int64) * 2654435761) % C] + 0.7 * noise
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    stored = R.process_rows(raw, "cosine", "bf16")
+    q = (raw[rng.choice(n, B, replace=False)] + 0.1 * rng.standard_normal((B, dim))).astype(np.float32)
+    before = idx.stats()["guard_failures"]
+    s, r = idx.search(q, 10)
+    _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10))
+    assert idx.stats()["guard_failures"] - before <= B // 8
+
+
 def test_query_groups_pipelined_vs_oracle(native):
     """The bench's pipelined path at B = 256 and 128 (early SAMPLE, two workspaces, dual FILTER
     streams) on a shard large enough for all of them: every batch identical to the oracle."""

@@ -354,6 +354,8 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     // batch was two corpus passes; 32-query groups share one (HIPRAG_QB1_GROUPS=0: separate passes, A/B)
     static const int qb1_env = getenv("HIPRAG_QB1_GROUPS") ? atoi(getenv("HIPRAG_QB1_GROUPS")) : 1;
     if (QB == 1 && B > 32 && h->dtype != F32 && qb1_env) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
+    // the 128-query FILTER (hr_wide.hip) serves query groups in pairs: round the group count up to even
+    if (p->NG > 1 && QB == 2 && wide_filter_ok(h->dtype, h->S)) p->NG = (p->NG + 1) & ~1;
     p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
     const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
@@ -438,6 +440,34 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // (HIPRAG_SAMPLE_NT=1: non-temporal SAMPLE loads, for A/B)
     static const bool sample_nt = getenv("HIPRAG_SAMPLE_NT") && atoi(getenv("HIPRAG_SAMPLE_NT")) != 0;
     const bool dflt = pl.NG > 1 || (MODE == SCAN_SAMPLE && !sample_nt);
+    // more than 64 queries (query groups) in a plain FILTER: the 128-query pass reads every tile once for
+    // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
+    if constexpr (MODE == SCAN_FILTER && DT != F32) {
+        if (pl.NG >= 2 && pl.QB == 2 && a.np == 1 && !a.tile_list && !a.xnorm && a.use_groups && !a.stamps &&
+            wide_filter_ok(h->dtype, h->S)) {
+            const int64_t n_pairs = (a.n_units + 1) / 2;
+            const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (n_pairs + 3) / 4));
+            const int64_t W = (int64_t)blocks * 4;  // waves: one candidate region per (group, wave)
+            HIP_TRY(sc.pbuf.ensure((size_t)pl.NG * 64 * W * kCapW * sizeof(float2)));
+            HIP_TRY(sc.pcnt.ensure((size_t)pl.NG * 64 * W * 4));
+            sc.last_W = W;
+            sc.last_Bp = 64;
+            sc.last_ng = pl.NG;
+            sc.last_capw = kCapW;
+            h->last_scr = &sc;
+            for (int set = 0; set < pl.NG / 2; ++set) {  // two groups per launch
+                ScanArgs b = a;
+                b.qfrag = a.qfrag + (int64_t)set * 2 * h->S * 2 * 64 * 8;
+                b.mkeys = a.mkeys + set * 128 * 32;
+                b.floor_q = a.floor_q + set * 128;
+                b.pbuf = sc.pbuf.as<float2>() + (int64_t)set * 2 * W * 64 * kCapW;
+                b.pcnt = sc.pcnt.as<uint32_t>() + (int64_t)set * 2 * W * 64;
+                b.capw = kCapW;
+                if (int rc = launch_filter_wide(MT, DT, h->S, blocks, b, st)) return set_err(rc, "wide FILTER launch failed");
+            }
+            return HR_OK;
+        }
+    }
 #define HR_SCAN_CASE(QBv, Pv)                                                                     \
     if (pl.QB == QBv && pl.P == Pv)                                                               \
         return dflt ? launch_scan_t<MT, DT, QBv, Pv, MODE, false>(h, sc, cus, a, st, lds)         \

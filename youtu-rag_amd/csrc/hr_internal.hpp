@@ -70,6 +70,10 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
 size_t tile_list_scratch_bytes(int64_t n_tiles);
 int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles, uint32_t* list, uint32_t* count,
                     void* scratch, size_t scratch_bytes, hipStream_t st);
+// hr_wide.hip: the 128-query FILTER (one workgroup per CU, 4 waves; pbuf / pcnt regions [2 groups][4 * cus][64])
+struct ScanArgs;
+bool wide_filter_ok(int dtype, int S);
+int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st);
 }  // namespace hr
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)

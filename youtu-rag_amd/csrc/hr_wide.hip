@@ -1,0 +1,338 @@
+// hr_wide.hip -- the 128-query FILTER pass: one read of every corpus tile for 128 queries (two 64-query groups).
+//
+// k_scan holds one 64-query group's A-fragments in LDS for the whole depth (128 KiB at D = 1024), so a batch of
+// 65-128 queries used to be two groups of workgroups streaming the same tiles, the second reading them from L2
+// (query groups): bounded by that access shape at 4.4-4.6 ms per 10M x 1024 batch, 1.13x the HBM
+// bytes.  Here ONE workgroup serves 128 queries and every tile is read from HBM once:
+//  * 4 waves (one per SIMD, up to 512 registers each); a wave scores two consecutive tiles at a time
+//    (a tile pair), so every query fragment read from LDS feeds two MFMAs;
+//  * the queries' fragments do not fit in LDS (256 KiB at D = 1024), so they stream through it in depth
+//    windows of 8 k-steps (2 groups x 8 k-steps x 2 blocks x 1 KiB = 32 KiB, double-buffered) that the four
+//    waves walk in lock step -- one barrier per window; each window is staged by LDS-DMA
+//    (buffer_load ... lds: L2 -> LDS with no registers and no ds_write) one window ahead;
+//  * the corpus streams through a 32-deep register ring (two halves of 2 tiles x 8 k-steps, non-temporal
+//    buffer loads, one V# per tile pair);
+//  * per-query thresholds live in LDS, and so do the group maxima: one table per workgroup raised with ds_max,
+//    only by scores at or above their query's threshold (nothing below the minimum over the groups can raise
+//    it, so these updates are as rare as the appends); at a refresh (every 2 pairs) wave w swaps query block
+//    w's maxima out, publishes them (atomicMax only where they beat the global key) and recomputes its 32
+//    thresholds.  The final keys may then sit below a group's true maximum, which only lowers k_select's
+//    threshold: the candidates still hold every row at or above the scan's highest threshold, and 32 of them
+//    (one per group) lie at or above it, so the kc-th best candidate bounds every dropped row;
+//  * candidates go to k_scan's private per-(group, wave) regions, so k_select reads them unchanged.
+// Timing prototype and its measurements: tools/q128_proto.hip (10M x 1024 bf16, 128 queries: 3.01 ms on 224
+// CUs against 2.92 ms with the staging switched off, 3.37 ms with one tile per wave, 3.77 ms with register
+// staging).
+// Scope: bf16 / f16 corpora, D a multiple of 256 up to 1024 (S = 16, 32, 48, 64 k-steps), one row part (kc <= 32),
+// cosine / inner product, no tile list -- every other FILTER keeps k_scan's query groups.
+#include "hr_internal.hpp"
+#include "hr_kernels.hpp"
+
+// A/B timing builds only (0 = wrong results): HR_WIDE_APPEND (candidate appends), HR_WIDE_REFRESH (threshold refresh)
+#ifndef HR_WIDE_APPEND
+#define HR_WIDE_APPEND 1
+#endif
+#ifndef HR_WIDE_REFRESH
+#define HR_WIDE_REFRESH 1
+#endif
+#ifndef HR_WIDE_GMAX  // timing experiments only (0: no group maxima; wrong thresholds)
+#define HR_WIDE_GMAX 1
+#endif
+namespace hr {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kWN = 8;       // k-steps per query window
+constexpr int kRefreshPairs = 2;  // tile pairs between threshold refreshes (k_scan: every 4 tiles)
+
+template <int MT, int DT, int S_>
+__global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
+    static_assert(DT != F32, "1 KiB k-step chunks (bf16 / f16 corpora)");
+    static_assert(S_ % (2 * kWN) == 0, "an even number of windows per tile (the ring halves alternate by window)");
+    constexpr int NW = S_ / kWN;           // windows per tile
+    constexpr int WQ = kWN * 4 * 64;       // u32x4 per window buffer: [group][k-step][block][lane]
+    constexpr int PER = WQ / 256;          // LDS-DMA chunks per thread per window
+    __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
+    __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
+    __shared__ __attribute__((aligned(16))) float th_lds[128];
+    // the workgroup's group maxima since the last refresh, as keys (f2key: ordered like the scores):
+    // G[block][register][lane], raised with ds_max_u32 by every wave, swapped out by the block's owner at a refresh
+    __shared__ __attribute__((aligned(16))) uint32_t G[4][16][64];
+    // per-wave scratch of a tile's 64 score registers for the append loop: dump[wave][register][lane]
+    __shared__ __attribute__((aligned(16))) float dump[4][64][64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;  // wave-major: a round's pairs spread over the CUs
+    const int64_t n_tiles = a.n_units;
+    const int64_t n_pairs = (n_tiles + 1) / 2;
+    const int64_t rounds = (n_pairs + W - 1) / W;  // the same for every wave: the waves of a workgroup stay in step
+    const int64_t full_rounds = n_pairs / W;
+    // pair of round u for this wave (-1: none -- the wave still walks the windows with the others, on a V# of
+    // zero records that reads zeros); full rounds are rotated by a hash of u as in k_scan (periodic clusters
+    // must not land in the same waves)
+    auto pair_at = [&](int64_t u) -> int64_t {
+        int64_t pos = wr;
+        if (HR_ROTATE_ROUNDS && u < full_rounds) {
+            pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
+            if (pos >= W) pos -= W;
+        }
+        const int64_t p = u * W + pos;
+        return wave_uniform(p < n_pairs ? p : -1);
+    };
+    auto rsrc = [&](int64_t p) {
+        const int64_t t0 = p < 0 ? 0 : 2 * p;
+        const int nt = p < 0 ? 0 : (int)std::min<int64_t>(2, n_tiles - t0);
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + t0 * (S_ * 1024)), (short)0, nt * S_ * 1024, 0x00020000);
+    };
+    const int voff = lane * 16;
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int chunk) -> u32x4 {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024, 2);  // non-temporal
+    };
+    // query fragments [group][S][2][64] (k_prep_q's layout, two groups); window w of group gq is one contiguous
+    // 16 KiB block.  Wave wv's j-th DMA moves the 1 KiB at buffer position j * 256 + wv * 64 (u32x4)
+    const __amdgpu_buffer_rsrc_t qr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 2 * S_ * 2 * 1024, 0x00020000);
+    auto stage = [&](int w, u32x4* buf) {
+        int vo = tid * 16;
+        asm volatile("" : "+v"(vo));  // (per call: keeps the offsets out of loop-invariant registers)
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int gq = j / (PER / 2), jj = j % (PER / 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 256 + wv * 64),
+                                                     16, vo, gq * S_ * 2048 + w * kWN * 2048 + jj * 4096, 0, 0);
+        }
+    };
+    // ring slot i of a half: tile (i >> 3) of the pair, k-step (i & 7) of the window
+    u32x4 ra[2 * kWN], rb[2 * kWN];
+    {
+        const auto r0 = rsrc(pair_at(0));
+#pragma unroll
+        for (int i = 0; i < 2 * kWN; ++i) ra[i] = ld(r0, (i >> 3) * S_ + (i & 7));
+#pragma unroll
+        for (int i = 0; i < 2 * kWN; ++i) rb[i] = ld(r0, (i >> 3) * S_ + kWN + (i & 7));
+    }
+    stage(0, lb0);
+
+    // this wave's query block for refreshes: block wv = group wv >> 1, queries (wv & 1) * 32 .. + 32 of it
+    uint32_t* const keys_w = a.mkeys + (wv * 32 + 4 * half) * 32 + g;  // + 32 * ((i & 3) + 8 (i >> 2))
+    auto qoff_i = [](int i) { return 32 * ((i & 3) + 8 * (i >> 2)); };
+    auto publish_refresh = [&](const float (&m)[16], const uint32_t (&key)[16], bool publish) {
+        float th16[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t k = key[i] > HR_KEY_NEG_INF ? key[i] : HR_KEY_NEG_INF;
+            if (publish && a.publish && m[i] > key2f(k)) {
+                atomicMax(keys_w + qoff_i(i), f2key(m[i]));
+                k = f2key(m[i]);
+            }
+            float f = key2f(k);
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+            th16[i] = f;
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = wv * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+                th_lds[q] = fmaxf(th_lds[q], fmaxf(th16[i], a.floor_q[q]));
+            }
+        }
+    };
+    // first thresholds (the SAMPLE's group maxima and the floors)
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) th_lds[wv * 32 + i] = -__builtin_inff();
+    }
+    {
+        uint32_t key[16];
+        float m[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            key[i] = __hip_atomic_load(keys_w + qoff_i(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m[i] = -__builtin_inff();
+        }
+        publish_refresh(m, key, false);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) G[wv][i][lane] = HR_KEY_NEG_INF;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    uint32_t mycnt[2] = {0u, 0u};  // lane q: candidates of query q of group 0 / 1 in this wave's regions
+    float2* const reg0 = a.pbuf + (wr * 64) * a.capw;        // region (group 0, wave wr)
+    float2* const reg1 = a.pbuf + ((W + wr) * 64) * a.capw;  // region (group 1, wave wr)
+
+    // the live / mask words of a pair (scalar loads), fetched one pair ahead: a scalar load still in flight at
+    // a window barrier would hold it (the barrier's lgkmcnt(0) waits for scalar loads too)
+    auto allow_words = [&](int64_t p, uint32_t& w0, uint32_t& w1) {
+        w0 = w1 = 0;
+        if (p < 0) return;
+        const int64_t t = 2 * p;
+        w0 = scalar_word(a.live, t);
+        if (a.mask) w0 &= scalar_word(a.mask, t);
+        if (t + 1 < n_tiles) {
+            w1 = scalar_word(a.live, t + 1);
+            if (a.mask) w1 &= scalar_word(a.mask, t + 1);
+        }
+    };
+    uint32_t next0, next1;
+    allow_words(pair_at(0), next0, next1);
+    for (int64_t u = 0; u < rounds; ++u) {
+        const int64_t p = pair_at(u), pn = pair_at(u + 1);
+        const auto rt = rsrc(p), rn = rsrc(pn);
+        const int64_t t0 = p < 0 ? 0 : 2 * p;
+        const uint32_t allow0 = next0, allow1 = next1;
+        allow_words(pn, next0, next1);
+        const bool refresh = HR_WIDE_REFRESH && u > 0 && (u % kRefreshPairs) == 0;  // workgroup-uniform
+        f32x16 acc[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[h][qb][i] = 0.0f;
+        uint32_t key[16];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            u32x4(&ring)[2 * kWN] = (w & 1) ? rb : ra;
+            if (w > 0 || u > 0) {
+                // window w's fragments are in LDS: this wave's DMA landed (every VMEM op issued after it -- the
+                // previous window's 16 ring refills at least -- may still be in flight), every wave's (barrier);
+                // every wave is also through the other buffer
+                asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            stage((w + 1) % NW, (w & 1) ? lb0 : lb1);
+            if (refresh && w == NW - 1) {  // the global keys, applied after the epilogue: issued before this
+                // window's ring refills, they are in by the time the next window's barrier wait would be anyway
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    key[i] = __hip_atomic_load(keys_w + qoff_i(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            unsigned qo = (unsigned)lane;
+            asm volatile("" : "+v"(qo));  // (per window: fragment offsets fold into the ds_read immediates)
+            const u32x4* qs = ((w & 1) ? lb1 : lb0) + qo;
+            // fragment (k-step i, block qb) at [qb >> 1][i][qb & 1]; one k-step ahead of its MFMAs
+            auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * kWN * 2 + i * 2 + (qb & 1)) * 64]; };
+            u32x4 qf[2][4];
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb) qf[0][qb] = qfrag(0, qb);
+#pragma unroll
+            for (int i = 0; i < kWN; ++i) {
+                if (i + 1 < kWN) {
+#pragma unroll
+                    for (int qb = 0; qb < 4; ++qb) qf[(i + 1) & 1][qb] = qfrag(i + 1, qb);
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const u32x4 x = ring[h * kWN + i];
+                    ring[h * kWN + i] = (w + 2 < NW) ? ld(rt, h * S_ + (w + 2) * kWN + i) : ld(rn, h * S_ + (w + 2 - NW) * kWN + i);
+#pragma unroll
+                    for (int qb = 0; qb < 4; ++qb) acc[h][qb] = mfma32<MT>(qf[i & 1][qb], x, acc[h][qb]);
+                }
+                __builtin_amdgcn_sched_barrier(0);  // (keeps the next k-step's fragment reads ahead of these MFMAs)
+            }
+        }
+
+        // epilogue: predicate, group maxima (max over the pair's two tiles, then one ds_max per register),
+        // threshold compare, then the appends into the private regions
+        const int rg0 = slot_row(t0, g), rg1 = slot_row(t0 + 1, g);
+        const bool ok0 = (allow0 >> rg0) & 1u, ok1 = (allow1 >> rg1) & 1u;
+        uint64_t regs0 = 0, regs1 = 0;
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * r + c;
+                    const float v0 = ok0 ? acc[0][qb][i] : -__builtin_inff();
+                    const float v1 = ok1 ? acc[1][qb][i] : -__builtin_inff();
+                    const bool p0 = ok0 && v0 >= t4[c], p1 = ok1 && v1 >= t4[c];
+                    // only a score at or above the query's threshold can raise it (the threshold is the minimum
+                    // over the groups), so only those reach the group maxima -- as rare as the appends
+                    if (HR_WIDE_GMAX && (p0 || p1)) atomicMax(&G[qb][i][lane], f2key(fmaxf(v0, v1)));
+                    regs0 |= (uint64_t)(__ballot(p0) != 0 ? 1u : 0u) << (qb * 16 + i);
+                    regs1 |= (uint64_t)(__ballot(p1) != 0 ? 1u : 0u) << (qb * 16 + i);
+                }
+            }
+        }
+        // appends: a tile with passing scores dumps its 64 score registers into this wave's LDS scratch, then a
+        // compact loop visits the passing registers (a fully unrolled append pass over 2 x 64 registers made the
+        // loop body 3x larger and cost 0.7 ms of a 4.2 ms pass at 10M rows)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint64_t regs = h ? regs1 : regs0;
+            if (!HR_WIDE_APPEND || !regs) continue;
+            const bool ok = h ? ok1 : ok0;
+            const uint32_t row = (uint32_t)((t0 + h) * 32 + (h ? rg1 : rg0));
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dump[wv][qb * 16 + i][lane] = ok ? acc[h][qb][i] : -__builtin_inff();
+            while (regs) {
+                const int b = __builtin_ctzll(regs);  // wave-uniform
+                regs &= regs - 1;
+                const int qb = b >> 4, i = b & 15;
+                const float v = dump[wv][b][lane];
+                const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
+                const bool pass = v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
+                const uint64_t msk = __ballot(pass);
+                const int gq = qb >> 1;
+                uint32_t cnt = gq ? mycnt[1] : mycnt[0];
+                float2* const reg = gq ? reg1 : reg0;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const uint32_t mh = (uint32_t)(msk >> (32 * hh));
+                    if (!mh) continue;
+                    const int ql = ql0 + 4 * hh;
+                    const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
+                    if (pass && half == hh) {
+                        const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                        if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                    }
+                    cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
+                }
+                if (gq) mycnt[1] = cnt;
+                else mycnt[0] = cnt;
+            }
+        }
+        if (refresh) {  // block wv's maxima since the last refresh, swapped out of G (nothing raised meanwhile is lost)
+            float m[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                m[i] = key2f(__hip_atomic_exchange(&G[wv][i][lane], (uint32_t)HR_KEY_NEG_INF, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
+            publish_refresh(m, key, true);
+        }
+    }
+    a.pcnt[wr * 64 + lane] = mycnt[0];
+    a.pcnt[(W + wr) * 64 + lane] = mycnt[1];
+}
+
+template <int MT, int DT, int S_>
+int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
+}  // namespace
+
+bool wide_filter_ok(int dtype, int S) {
+    static const int env = getenv("HIPRAG_WIDE_FILTER") ? atoi(getenv("HIPRAG_WIDE_FILTER")) : 1;  // 0: query groups (A/B)
+    return env && dtype != F32 && (S == 16 || S == 32 || S == 48 || S == 64);
+}
+
+int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st) {
+#define HR_WIDE_CASE(MTv, DTv, Sv) \
+    if (mt == MTv && dtype == DTv && S == Sv) return launch_t<MTv, DTv, Sv>(cus, a, st);
+    HR_WIDE_CASE(BF16, BF16, 64) HR_WIDE_CASE(BF16, BF16, 48) HR_WIDE_CASE(BF16, BF16, 32) HR_WIDE_CASE(BF16, BF16, 16)
+    HR_WIDE_CASE(F16, F16, 64) HR_WIDE_CASE(F16, F16, 48) HR_WIDE_CASE(F16, F16, 32) HR_WIDE_CASE(F16, F16, 16)
+#undef HR_WIDE_CASE
+    return HR_E_UNSUPPORTED;
+}
+
+}  // namespace hr

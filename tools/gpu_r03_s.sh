@@ -1,0 +1,14 @@
+# round 3: 128-query FILTER, eight-wave form vs the four-wave pair form: parity, diagnostics, sweep, prototype
+set -o pipefail
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+O=gpurun_out/r03s
+mkdir -p $O
+timeout -k 10 120 tools/q128_proto 20.48 > $O/proto.jsonl 2>&1; echo "proto rc=$?"; cat $O/proto.jsonl
+timeout -k 10 600 python -u -m pytest tests/test_gpu_index.py -x -q --timeout 300 --timeout-method thread -k "wide or query_group" > $O/wide_tests.log 2>&1
+rc=$?; echo "wide tests rc=$rc"; tail -3 $O/wide_tests.log; [ $rc -ne 0 ] && exit $rc
+for cfg in "HIPRAG_WIDE_WAVES=8" "HIPRAG_WIDE_WAVES=4"; do
+  env $cfg timeout -k 10 200 python -u tools/diag_wide.py --reps 20 >> $O/diag.jsonl 2>> $O/diag.err || { echo "$cfg failed"; exit 1; }
+  tail -1 $O/diag.jsonl
+done
+timeout -k 10 300 python -u tools/sweep_batch.py --batches 64,128,256 --steps 60 > $O/sweep_wide.jsonl 2> $O/sweep_wide.err
+rc=$?; echo "sweep rc=$rc"; cat $O/sweep_wide.jsonl

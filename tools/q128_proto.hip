@@ -426,6 +426,118 @@ __global__ __launch_bounds__(256, 1) void k_qd2(const u32x4* __restrict__ corpus
     if (s == 1234.5f || passes == 0xFFFFFFFFu) sink[0] = 1u;
 }
 
+// Eight waves (two per SIMD), one tile per wave, window = 8 k-steps: the same staging per tile as k_qd2 (eight
+// tiles per staged window per workgroup) with half the registers per wave, so a wave's epilogue runs beside the
+// other wave's MFMAs on its SIMD
+template <int QB>
+__global__ __launch_bounds__(512, 1) void k_qd8(const u32x4* __restrict__ corpus, const u32x4* __restrict__ qfrag,
+                                               long long n_tiles, int mode_unused, unsigned* __restrict__ sink) {
+    constexpr int WN = 8;
+    constexpr int NW = S / WN;
+    constexpr int WQ = WN * QB * 64;
+    constexpr int PER = WQ / 512;
+    __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
+    __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
+    __shared__ __attribute__((aligned(16))) float th_lds[QB * 32];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const long long W = (long long)gridDim.x * 8;
+    const long long wr = (long long)wv * gridDim.x + blockIdx.x;
+    const long long n_rounds = n_tiles / W;
+    auto uni = [](long long v) -> long long {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)((unsigned long long)v >> 32));
+        return (long long)(((unsigned long long)hi << 32) | lo);
+    };
+    auto tile = [&](long long u) -> long long { return uni((u < n_rounds ? u : n_rounds - 1) * W + wr); };
+    auto rsrc = [&](long long t) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)corpus + t * (S * 1024)), (short)0, S * 1024, 0x00020000);
+    };
+    const int voff = lane * 16;
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int chunk) -> u32x4 { return __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024, 2); };
+    const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc((void*)qfrag, (short)0, S * QB * 1024, 0x00020000);
+    auto stage = [&](int w, u32x4* buf) {
+        int vo = tid * 16;
+        asm volatile("" : "+v"(vo));
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 512 + wv * 64),
+                                                     16, vo, w * WQ * 16 + j * 8192, 0, 0);
+    };
+    u32x4 ra[WN], rb[WN];
+    {
+        const auto r0 = rsrc(tile(0));
+#pragma unroll
+        for (int i = 0; i < WN; ++i) ra[i] = ld(r0, i);
+#pragma unroll
+        for (int i = 0; i < WN; ++i) rb[i] = ld(r0, WN + i);
+    }
+    stage(0, lb0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid < QB * 32) th_lds[tid] = __builtin_bit_cast(float, (unsigned)(0x7E000000u + tid));
+    __syncthreads();
+    float gmax[QB][16];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) gmax[qb][i] = -1e30f;
+    unsigned passes = 0;
+    for (long long u = 0; u < n_rounds; ++u) {
+        const auto rt = rsrc(tile(u)), rn = rsrc(tile(u + 1));
+        f32x16 acc[QB];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[qb][i] = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            u32x4(&ring)[WN] = (w & 1) ? rb : ra;
+            if (w > 0 || u > 0) {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            stage((w + 1) % NW, (w & 1) ? lb0 : lb1);
+            unsigned qoff = (unsigned)lane;
+            asm volatile("" : "+v"(qoff));
+            const u32x4* qs = ((w & 1) ? lb1 : lb0) + qoff;
+            u32x4 qf[2][QB];
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) qf[0][qb] = qs[qb * 64];
+#pragma unroll
+            for (int i = 0; i < WN; ++i) {
+                if (i + 1 < WN) {
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb) qf[(i + 1) & 1][qb] = qs[((i + 1) * QB + qb) * 64];
+                }
+                const u32x4 x = ring[i];
+                ring[i] = (w + 2 < NW) ? ld(rt, (w + 2) * WN + i) : ld(rn, (w + 2 - NW) * WN + i);
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) acc[qb] = mfma(qf[i & 1][qb], x, acc[qb]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                typedef float f32x4 __attribute__((ext_vector_type(4)));
+                const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * (lane >> 5)];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * r + c;
+                    const float v = acc[qb][i];
+                    gmax[qb][i] = fmaxf(gmax[qb][i], v);
+                    passes += __ballot(v >= t4[c]) != 0 ? 1u : 0u;
+                }
+            }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += gmax[qb][i];
+    if (s == 1234.5f || passes == 0xFFFFFFFFu) sink[0] = 1u;
+}
+
 int main(int argc, char** argv) {
     const double gb = argc > 1 ? atof(argv[1]) : 20.48;
     const long long tile_bytes = (long long)S * 1024;
@@ -462,12 +574,27 @@ int main(int argc, char** argv) {
                     "\"qps_equiv\": %.0f}\n", qb * 32, cus, mode, bytes, t, bytes / (t * 1e-3) / 1e12, qb * 32 / (t * 1e-3));
         std::fflush(stdout);
     };
+    auto time8 = [&](auto kern, int qb, int cus, int mode) {
+        hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, corpus, qf, n_tiles, mode, sink);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(a, 0));
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, corpus, qf, n_tiles, mode, sink);
+        CHECK(hipEventRecord(b, 0));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0.f;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        const double t = ms / reps;
+        std::printf("{\"proto\": \"q%d 8 waves\", \"cus\": %d, \"mode\": %d, \"bytes\": %lld, \"ms\": %.4f, \"TBps\": %.4f, "
+                    "\"qps_equiv\": %.0f}\n", qb * 32, cus, mode, bytes, t, bytes / (t * 1e-3) / 1e12, qb * 32 / (t * 1e-3));
+        std::fflush(stdout);
+    };
     const int only = argc > 2 ? atoi(argv[2]) : -1;  // one variant (profiling): 0..4 at all CUs
     for (int cus : {n_cu - 32, n_cu}) {
         if (only >= 0 && cus != n_cu) continue;
         if (only < 0 || only == 0) time(k_qd<4>, 4, cus, 1000);                // LDS-DMA staging
         if (only < 0 || only == 1) time(k_qd2<4>, 4, cus, 2000);               // + two tiles per wave
         if (only < 0 || only == 2) time(k_q<4, 12, 1>, 4, cus, 12);           // neither staging nor barriers
+        if (only < 0 || only == 3) time8(k_qd8<4>, 4, cus, 3000);              // eight waves, one tile each
     }
     CHECK(hipFree(corpus));
     CHECK(hipFree(qf));

@@ -445,9 +445,11 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     if constexpr (MODE == SCAN_FILTER && DT != F32) {
         if (pl.NG >= 2 && pl.QB == 2 && a.np == 1 && !a.tile_list && !a.xnorm && a.use_groups && !a.stamps &&
             wide_filter_ok(h->dtype, h->S)) {
-            const int64_t n_pairs = (a.n_units + 1) / 2;
-            const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (n_pairs + 3) / 4));
-            const int64_t W = (int64_t)blocks * 4;  // waves: one candidate region per (group, wave)
+            // waves: one candidate region per (group, wave); a wave takes a tile (8 waves) or a tile pair (4)
+            const int wpb = wide_waves();
+            const int64_t units = wpb == 8 ? a.n_units : (a.n_units + 1) / 2;
+            const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (units + wpb - 1) / wpb));
+            const int64_t W = (int64_t)blocks * wpb;
             HIP_TRY(sc.pbuf.ensure((size_t)pl.NG * 64 * W * kCapW * sizeof(float2)));
             HIP_TRY(sc.pcnt.ensure((size_t)pl.NG * 64 * W * 4));
             sc.last_W = W;

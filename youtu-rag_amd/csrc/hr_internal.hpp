@@ -73,6 +73,7 @@ int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles,
 // hr_wide.hip: the 128-query FILTER (one workgroup per CU, 4 waves; pbuf / pcnt regions [2 groups][4 * cus][64])
 struct ScanArgs;
 bool wide_filter_ok(int dtype, int S);
+int wide_waves();  // 8 (one tile per wave, 512 threads) or 4 (tile pairs, 256 threads)
 int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st);
 }  // namespace hr
 

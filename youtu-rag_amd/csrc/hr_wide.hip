@@ -40,6 +40,8 @@
 #endif
 namespace hr {
 
+int wide_waves();
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -236,11 +238,15 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
             }
         }
 
-        // epilogue: predicate, group maxima (max over the pair's two tiles, then one ds_max per register),
-        // threshold compare, then the appends into the private regions
+        // epilogue.  Fast test first: does any allowed row of either tile reach its query's threshold?
+        // acc - th >= 0 exactly when acc >= th (a flushed denormal difference can only add a false positive,
+        // which the exact compares below then reject; th = -inf gives +inf, a padded query's th = +inf gives
+        // -inf).  After the first rounds almost no tile does, and the pair costs 2 subtractions + 2 maxima per
+        // register.  (The full per-register compare and ballot of both tiles cost ~25 instructions per
+        // register on the one wave of its SIMD.)
         const int rg0 = slot_row(t0, g), rg1 = slot_row(t0 + 1, g);
         const bool ok0 = (allow0 >> rg0) & 1u, ok1 = (allow1 >> rg1) & 1u;
-        uint64_t regs0 = 0, regs1 = 0;
+        float d0 = -__builtin_inff(), d1 = -__builtin_inff();
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb) {
 #pragma unroll
@@ -248,39 +254,35 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
                 const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const int i = 4 * r + c;
-                    const float v0 = ok0 ? acc[0][qb][i] : -__builtin_inff();
-                    const float v1 = ok1 ? acc[1][qb][i] : -__builtin_inff();
-                    const bool p0 = ok0 && v0 >= t4[c], p1 = ok1 && v1 >= t4[c];
-                    // only a score at or above the query's threshold can raise it (the threshold is the minimum
-                    // over the groups), so only those reach the group maxima -- as rare as the appends
-                    if (HR_WIDE_GMAX && (p0 || p1)) atomicMax(&G[qb][i][lane], f2key(fmaxf(v0, v1)));
-                    regs0 |= (uint64_t)(__ballot(p0) != 0 ? 1u : 0u) << (qb * 16 + i);
-                    regs1 |= (uint64_t)(__ballot(p1) != 0 ? 1u : 0u) << (qb * 16 + i);
+                    d0 = fmaxf(d0, acc[0][qb][4 * r + c] - t4[c]);
+                    d1 = fmaxf(d1, acc[1][qb][4 * r + c] - t4[c]);
                 }
             }
         }
-        // appends: a tile with passing scores dumps its 64 score registers into this wave's LDS scratch, then a
-        // compact loop visits the passing registers (a fully unrolled append pass over 2 x 64 registers made the
-        // loop body 3x larger and cost 0.7 ms of a 4.2 ms pass at 10M rows)
+        const bool hit0 = ok0 && d0 >= 0.0f, hit1 = ok1 && d1 >= 0.0f;
+        // Slow path, per tile with a hit: its 64 score registers (-inf where the row is not allowed) go to this
+        // wave's LDS scratch, and a compact loop over the registers does the exact compares, raises the group
+        // maxima (only scores at or above their query's threshold can raise it: the threshold is the minimum
+        // over the groups) and appends to the private regions
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            uint64_t regs = h ? regs1 : regs0;
-            if (!HR_WIDE_APPEND || !regs) continue;
+            if (!__ballot(h ? hit1 : hit0)) continue;
             const bool ok = h ? ok1 : ok0;
             const uint32_t row = (uint32_t)((t0 + h) * 32 + (h ? rg1 : rg0));
 #pragma unroll
             for (int qb = 0; qb < 4; ++qb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) dump[wv][qb * 16 + i][lane] = ok ? acc[h][qb][i] : -__builtin_inff();
-            while (regs) {
-                const int b = __builtin_ctzll(regs);  // wave-uniform
-                regs &= regs - 1;
+            for (int b = 0; b < 64; ++b) {  // (not unrolled: rare, keep the loop body small)
                 const int qb = b >> 4, i = b & 15;
                 const float v = dump[wv][b][lane];
                 const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
-                const bool pass = v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
+                // (a masked row holds -inf: it must not pass a threshold that is still -inf)
+                const bool pass = v > -__builtin_inff() && v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
                 const uint64_t msk = __ballot(pass);
+                if (!msk) continue;
+                if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
+                if (!HR_WIDE_APPEND) continue;
                 const int gq = qb >> 1;
                 uint32_t cnt = gq ? mycnt[1] : mycnt[0];
                 float2* const reg = gq ? reg1 : reg0;
@@ -313,13 +315,246 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
     a.pcnt[(W + wr) * 64 + lane] = mycnt[1];
 }
 
+// The eight-wave form: two waves per SIMD, one tile per wave per round.  Staging per tile is the same as the
+// four-wave pair form (each staged window serves eight tiles per workgroup), the registers per wave half, and a
+// wave's epilogue runs beside the other wave's MFMAs on its SIMD -- with 128 queries per tile a third of the tiles
+// hold a candidate (10M rows, k = 10), so the epilogue is no longer rare.  Group maxima, thresholds, refreshes
+// and appends as in k_filter_wide; a refresh splits each query block's 16 registers between two waves.
+template <int MT, int DT, int S_>
+__global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
+    static_assert(DT != F32, "1 KiB k-step chunks (bf16 / f16 corpora)");
+    static_assert(S_ % (2 * kWN) == 0, "an even number of windows per tile (the ring halves alternate by window)");
+    constexpr int NW = S_ / kWN;
+    constexpr int WQ = kWN * 4 * 64;   // u32x4 per window buffer: [group][k-step][block][lane]
+    constexpr int PER = WQ / 512;      // LDS-DMA chunks per thread per window
+    // rounds between refreshes (every 2 by default: 4 measured 1291 candidates per query at 10M rows, B = 128)
+    const int RT = std::max(1, a.refresh_every / 2);
+    __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
+    __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
+    __shared__ __attribute__((aligned(16))) float th_lds[128];
+    __shared__ __attribute__((aligned(16))) uint32_t G[4][16][64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
+    const int64_t W = (int64_t)gridDim.x * 8;
+    const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;
+    const int64_t n_tiles = a.n_units;
+    const int64_t rounds = (n_tiles + W - 1) / W;
+    const int64_t full_rounds = n_tiles / W;
+    auto tile_at = [&](int64_t u) -> int64_t {  // -1: no tile this round (zero-record V#)
+        int64_t pos = wr;
+        if (HR_ROTATE_ROUNDS && u < full_rounds) {
+            pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
+            if (pos >= W) pos -= W;
+        }
+        const int64_t t = u * W + pos;
+        return wave_uniform(t < n_tiles ? t : -1);
+    };
+    auto rsrc = [&](int64_t t) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024)), (short)0,
+                                                 t < 0 ? 0 : S_ * 1024, 0x00020000);
+    };
+    const int voff = lane * 16;
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int chunk) -> u32x4 {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024, 2);  // non-temporal
+    };
+    const __amdgpu_buffer_rsrc_t qr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 2 * S_ * 2 * 1024, 0x00020000);
+    auto stage = [&](int w, u32x4* buf) {  // chunk c = j * 512 + tid: group c >> 10 (j >> 1), offset c & 1023
+        int vo = tid * 16;
+        asm volatile("" : "+v"(vo));
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 512 + wv * 64),
+                                                     16, vo, (j >> 1) * S_ * 2048 + w * kWN * 2048 + (j & 1) * 8192, 0, 0);
+    };
+    u32x4 ra[kWN], rb[kWN];
+    {
+        const auto r0 = rsrc(tile_at(0));
+#pragma unroll
+        for (int i = 0; i < kWN; ++i) ra[i] = ld(r0, i);
+#pragma unroll
+        for (int i = 0; i < kWN; ++i) rb[i] = ld(r0, kWN + i);
+    }
+    stage(0, lb0);
+
+    // refresh share of this wave: block wb = wv & 3, registers [8 * (wv >> 2), + 8)
+    const int wb = wv & 3, i0 = 8 * (wv >> 2);
+    uint32_t* const keys_w = a.mkeys + (wb * 32 + 4 * half) * 32 + g;
+    auto qoff_i = [](int i) { return 32 * ((i & 3) + 8 * (i >> 2)); };
+    auto publish_refresh = [&](const float (&m)[8], const uint32_t (&key)[8], bool publish) {
+        float th8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = i0 + j;
+            uint32_t k = key[j] > HR_KEY_NEG_INF ? key[j] : HR_KEY_NEG_INF;
+            if (publish && a.publish && m[j] > key2f(k)) {
+                atomicMax(keys_w + qoff_i(i), f2key(m[j]));
+                k = f2key(m[j]);
+            }
+            float f = key2f(k);
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+            th8[j] = f;
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = i0 + j;
+                const int q = wb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+                th_lds[q] = fmaxf(th_lds[q], fmaxf(th8[j], a.floor_q[q]));
+            }
+        }
+    };
+    if (tid < 128) th_lds[tid] = -__builtin_inff();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) G[wb][i0 + j][lane] = HR_KEY_NEG_INF;
+    __syncthreads();
+    {
+        uint32_t key[8];
+        float m[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            key[j] = __hip_atomic_load(keys_w + qoff_i(i0 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m[j] = -__builtin_inff();
+        }
+        publish_refresh(m, key, false);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    uint32_t mycnt[2] = {0u, 0u};
+    float2* const reg0 = a.pbuf + (wr * 64) * a.capw;
+    float2* const reg1 = a.pbuf + ((W + wr) * 64) * a.capw;
+    auto allow_word = [&](int64_t t) -> uint32_t {
+        if (t < 0) return 0u;
+        uint32_t w0 = scalar_word(a.live, t);
+        if (a.mask) w0 &= scalar_word(a.mask, t);
+        return w0;
+    };
+    uint32_t next_allow = allow_word(tile_at(0));
+    for (int64_t u = 0; u < rounds; ++u) {
+        const int64_t t = tile_at(u), tn = tile_at(u + 1);
+        const auto rt = rsrc(t), rn = rsrc(tn);
+        const uint32_t allow = next_allow;
+        next_allow = allow_word(tn);
+        const bool refresh = u > 0 && ((u % RT) == 0 || u == 1);  // workgroup-uniform (and early: the SAMPLE's
+        // thresholds are loose, the first rounds append the most)
+        f32x16 acc[4];
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
+        uint32_t key[8];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            u32x4(&ring)[kWN] = (w & 1) ? rb : ra;
+            if (w > 0 || u > 0) {
+                // this wave's DMA for window w landed (the previous window's 8 ring refills were issued after it)
+                asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            stage((w + 1) % NW, (w & 1) ? lb0 : lb1);
+            if (refresh && w == NW - 1) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    key[j] = __hip_atomic_load(keys_w + qoff_i(i0 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            unsigned qo = (unsigned)lane;
+            asm volatile("" : "+v"(qo));
+            const u32x4* qs = ((w & 1) ? lb1 : lb0) + qo;
+            auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * kWN * 2 + i * 2 + (qb & 1)) * 64]; };
+            u32x4 qf[2][4];
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb) qf[0][qb] = qfrag(0, qb);
+#pragma unroll
+            for (int i = 0; i < kWN; ++i) {
+                if (i + 1 < kWN) {
+#pragma unroll
+                    for (int qb = 0; qb < 4; ++qb) qf[(i + 1) & 1][qb] = qfrag(i + 1, qb);
+                }
+                const u32x4 x = ring[i];
+                ring[i] = (w + 2 < NW) ? ld(rt, (w + 2) * kWN + i) : ld(rn, (w + 2 - NW) * kWN + i);
+#pragma unroll
+                for (int qb = 0; qb < 4; ++qb) acc[qb] = mfma32<MT>(qf[i & 1][qb], x, acc[qb]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+        // epilogue: fast test (acc - th >= 0 exactly when acc >= th; see k_filter_wide), then, for a tile with a
+        // hit, the exact per-register compares, group maxima (ds_max, scores at or above their threshold
+        // only) and appends
+        const int rg = slot_row(t < 0 ? 0 : t, g);
+        const bool ok = (allow >> rg) & 1u;
+        float d = -__builtin_inff();
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) d = fmaxf(d, acc[qb][4 * r + c] - t4[c]);
+            }
+        if (__ballot(ok && d >= 0.0f)) {
+            const uint32_t row = (uint32_t)(t * 32 + rg);
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int i = 4 * r + c;
+                        const float v = acc[qb][i];
+                        const bool pass = ok && v >= t4[c];
+                        const uint64_t msk = __ballot(pass);
+                        if (!msk) continue;
+                        if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
+                        if (!HR_WIDE_APPEND) continue;
+                        uint32_t& cnt = (qb >> 1) ? mycnt[1] : mycnt[0];
+                        float2* const reg = (qb >> 1) ? reg1 : reg0;
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            const uint32_t mh = (uint32_t)(msk >> (32 * hh));
+                            if (!mh) continue;
+                            const int ql = acc_query(qb & 1, i, hh);
+                            const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
+                            if (pass && half == hh) {
+                                const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                                if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                            }
+                            cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
+                        }
+                    }
+                }
+            }
+        }
+        if (refresh) {  // this wave's share of block wb, swapped out of G
+            float m[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                m[j] = key2f(__hip_atomic_exchange(&G[wb][i0 + j][lane], (uint32_t)HR_KEY_NEG_INF, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
+            publish_refresh(m, key, true);
+        }
+    }
+    a.pcnt[wr * 64 + lane] = mycnt[0];
+    a.pcnt[(W + wr) * 64 + lane] = mycnt[1];
+}
+
 template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
+    if (wide_waves() == 8) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 
 }  // namespace
+
+// waves per workgroup of the 128-query FILTER: 8 (one tile per wave) or 4 (tile pairs); HIPRAG_WIDE_WAVES (A/B)
+int wide_waves() {
+    static const int env = getenv("HIPRAG_WIDE_WAVES") ? atoi(getenv("HIPRAG_WIDE_WAVES")) : 8;
+    return env == 4 ? 4 : 8;
+}
 
 bool wide_filter_ok(int dtype, int S) {
     static const int env = getenv("HIPRAG_WIDE_FILTER") ? atoi(getenv("HIPRAG_WIDE_FILTER")) : 1;  // 0: query groups (A/B)

@@ -365,6 +365,12 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     return HR_OK;
 }
 
+// the FILTER of this plan runs as the 128-query pass (hr_wide.hip): query groups in pairs, bf16 / f16, D a multiple
+// of 256, one row part, no tile list, cosine / inner product
+static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list) {
+    return pl.NG >= 2 && pl.QB == 2 && np == 1 && !tile_list && h->metric != L2 && wide_filter_ok(h->dtype, h->S);
+}
+
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
 static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
     const int ng = std::max(1, a.ng);
@@ -443,8 +449,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // more than 64 queries (query groups) in a plain FILTER: the 128-query pass reads every tile once for
     // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
     if constexpr (MODE == SCAN_FILTER && DT != F32) {
-        if (pl.NG >= 2 && pl.QB == 2 && a.np == 1 && !a.tile_list && !a.xnorm && a.use_groups && !a.stamps &&
-            wide_filter_ok(h->dtype, h->S)) {
+        if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && !a.xnorm && a.use_groups && !a.stamps) {
             // waves: one candidate region per (group, wave); a wave takes a tile (8 waves) or a tile pair (4)
             const int wpb = wide_waves();
             const int64_t units = wpb == 8 ? a.n_units : (a.n_units + 1) / 2;
@@ -567,8 +572,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // Not for a group shard sharing its GPU with other shards (dev_ids repeated): their early SAMPLEs on
     // high-priority streams then cut into each other's FILTERs -- 8 shards of 1.25M rows on one GPU
     // 4.87 ms/batch with, 3.76 without (profiles/r03_group_shared_gpu.log)
+    // (not for the 128-query FILTER, which takes every CU: an early SAMPLE on the spare CUs would only start
+    // when the previous FILTER ends, on 32 CUs instead of all of them)
+    const bool wide_likely = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, h->tl_n >= 0);
     const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && tail_cus(h) > 0 &&
-                       !h->shared_dev && n_tiles >= early_min * sample_target(n_tiles);
+                       !h->shared_dev && !wide_likely && n_tiles >= early_min * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -637,7 +645,12 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         }
         sf = sc.scan;
     }
-    const int cus = piped ? h->n_cu - tail_cus(h) : h->n_cu;
+    // the 128-query FILTER takes every CU even when pipelined: with two of its 512-thread workgroups' waves per
+    // SIMD (248 registers each) no tail kernel fits beside it anyway, and its per-CU rate, not HBM, bounds it
+    // (10M x 1024, B = 128: 3.60 -> 3.43 ms per batch, B = 256: 7.19 -> 6.81 ms)
+    static const int wide_tail_env = getenv("HIPRAG_WIDE_TAIL_CUS") ? atoi(getenv("HIPRAG_WIDE_TAIL_CUS")) : 0;
+    const bool wide = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, tl_ptr != nullptr);
+    const int cus = piped ? h->n_cu - (wide ? std::max(0, std::min(wide_tail_env, h->n_cu - 8)) : tail_cus(h)) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)pl.NG * h->S * pl.QB * 1024));
     HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));

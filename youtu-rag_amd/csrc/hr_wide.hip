@@ -327,8 +327,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     constexpr int NW = S_ / kWN;
     constexpr int WQ = kWN * 4 * 64;   // u32x4 per window buffer: [group][k-step][block][lane]
     constexpr int PER = WQ / 512;      // LDS-DMA chunks per thread per window
-    // rounds between refreshes (every 2 by default: 4 measured 1291 candidates per query at 10M rows, B = 128)
-    const int RT = std::max(1, a.refresh_every / 2);
+    // rounds between refreshes (k_scan's tiles per refresh: 4).  At 10M rows, B = 128, every 1 / 2 / 4 rounds
+    // appended 850 / 897 / 1128 candidates per query and took 3.51 / 3.41 / 3.32 ms: the refresh costs more than
+    // the candidates it saves
+    const int RT = std::max(1, a.refresh_every);
     __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
     __shared__ __attribute__((aligned(16))) float th_lds[128];
@@ -437,8 +439,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         const auto rt = rsrc(t), rn = rsrc(tn);
         const uint32_t allow = next_allow;
         next_allow = allow_word(tn);
-        const bool refresh = u > 0 && ((u % RT) == 0 || u == 1);  // workgroup-uniform (and early: the SAMPLE's
-        // thresholds are loose, the first rounds append the most)
+        const bool refresh = u > 0 && (u % RT) == 0;  // workgroup-uniform
         f32x16 acc[4];
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)
@@ -495,37 +496,63 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 for (int c = 0; c < 4; ++c) d = fmaxf(d, acc[qb][4 * r + c] - t4[c]);
             }
         if (__ballot(ok && d >= 0.0f)) {
+            // the registers holding a passing score: per-lane bits, OR-reduced over the wave, then a loop over
+            // the set bits only (usually one or two) that reads each register by a uniform dynamic index.  The
+            // workgroup's eight waves meet at the next window barrier, so a long epilogue on one wave holds all
             const uint32_t row = (uint32_t)(t * 32 + rg);
+            uint32_t bl = 0, bh = 0;
 #pragma unroll
-            for (int qb = 0; qb < 4; ++qb) {
+            for (int qb = 0; qb < 4; ++qb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        const int i = 4 * r + c;
-                        const float v = acc[qb][i];
-                        const bool pass = ok && v >= t4[c];
-                        const uint64_t msk = __ballot(pass);
-                        if (!msk) continue;
-                        if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
-                        if (!HR_WIDE_APPEND) continue;
-                        uint32_t& cnt = (qb >> 1) ? mycnt[1] : mycnt[0];
-                        float2* const reg = (qb >> 1) ? reg1 : reg0;
-#pragma unroll
-                        for (int hh = 0; hh < 2; ++hh) {
-                            const uint32_t mh = (uint32_t)(msk >> (32 * hh));
-                            if (!mh) continue;
-                            const int ql = acc_query(qb & 1, i, hh);
-                            const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
-                            if (pass && half == hh) {
-                                const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                                if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
-                            }
-                            cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
-                        }
+                        const int b = qb * 16 + 4 * r + c;
+                        const bool p = ok && acc[qb][4 * r + c] >= t4[c];
+                        if (b < 32) bl |= p ? (1u << b) : 0u;
+                        else bh |= p ? (1u << (b - 32)) : 0u;
                     }
                 }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                bl |= (uint32_t)__shfl_xor((int)bl, off, 64);
+                bh |= (uint32_t)__shfl_xor((int)bh, off, 64);
+            }
+            uint64_t bits = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bh) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)bl);
+            while (bits) {
+                const int b = __builtin_ctzll(bits);  // wave-uniform
+                bits &= bits - 1;
+                const int qb = b >> 4, i = b & 15;
+                // register b by uniform selects (16 per read; a dynamic register index spilled)
+                float v = 0.0f;
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) v = (b == q4 * 16 + j) ? acc[q4][j] : v;
+                const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
+                const bool pass = ok && v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
+                const uint64_t msk = __ballot(pass);
+                if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
+                if (!HR_WIDE_APPEND || !msk) continue;
+                const int gq = qb >> 1;
+                uint32_t cnt = gq ? mycnt[1] : mycnt[0];
+                float2* const reg = gq ? reg1 : reg0;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const uint32_t mh = (uint32_t)(msk >> (32 * hh));
+                    if (!mh) continue;
+                    const int ql = ql0 + 4 * hh;
+                    const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
+                    if (pass && half == hh) {
+                        const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                        if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                    }
+                    cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
+                }
+                if (gq) mycnt[1] = cnt;
+                else mycnt[0] = cnt;
             }
         }
         if (refresh) {  // this wave's share of block wb, swapped out of G

@@ -574,9 +574,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // 4.87 ms/batch with, 3.76 without (profiles/r03_group_shared_gpu.log)
     // (not for the 128-query FILTER, which takes every CU: an early SAMPLE on the spare CUs would only start
     // when the previous FILTER ends, on 32 CUs instead of all of them)
+    // CUs the pipelined FILTER leaves to the tail stream and the early SAMPLE: tail_cus(h) for k_scan; none by
+    // default for the 128-query FILTER (HIPRAG_WIDE_TAIL_CUS), whose per-CU rate bounds it, so its SAMPLE is not
+    // early (it would only start when the previous FILTER ends, on the few spare CUs)
+    static const int wide_tail_env = getenv("HIPRAG_WIDE_TAIL_CUS") ? atoi(getenv("HIPRAG_WIDE_TAIL_CUS")) : 0;
     const bool wide_likely = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, h->tl_n >= 0);
-    const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && tail_cus(h) > 0 &&
-                       !h->shared_dev && !wide_likely && n_tiles >= early_min * sample_target(n_tiles);
+    const int spare = wide_likely ? std::max(0, std::min(wide_tail_env, h->n_cu - 8)) : tail_cus(h);
+    const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && spare > 0 &&
+                       !h->shared_dev && n_tiles >= early_min * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -645,10 +650,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         }
         sf = sc.scan;
     }
-    // the 128-query FILTER takes every CU even when pipelined: with two of its 512-thread workgroups' waves per
-    // SIMD (248 registers each) no tail kernel fits beside it anyway, and its per-CU rate, not HBM, bounds it
-    // (10M x 1024, B = 128: 3.60 -> 3.43 ms per batch, B = 256: 7.19 -> 6.81 ms)
-    static const int wide_tail_env = getenv("HIPRAG_WIDE_TAIL_CUS") ? atoi(getenv("HIPRAG_WIDE_TAIL_CUS")) : 0;
+    // the 128-query FILTER takes every CU even when pipelined (by default): with two of its 512-thread
+    // workgroups' waves per SIMD (248 registers each) no tail kernel fits beside it anyway, and its per-CU rate,
+    // not HBM, bounds it (10M x 1024, B = 128: 3.60 -> 3.43 ms per batch, B = 256: 7.19 -> 6.81 ms)
     const bool wide = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, tl_ptr != nullptr);
     const int cus = piped ? h->n_cu - (wide ? std::max(0, std::min(wide_tail_env, h->n_cu - 8)) : tail_cus(h)) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
@@ -781,7 +785,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
             const int pub = a.publish;
             a.publish = (dbg & 32) ? 0 : 1;
-            if (int rc = launch_scan(h, sc, early ? tail_cus(h) : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
+            if (int rc = launch_scan(h, sc, early ? spare : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
             a.publish = pub;
             ev.sampled = true;
             if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE

@@ -47,6 +47,8 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWN = 8;       // k-steps per query window
 constexpr int kRefreshPairs = 2;  // tile pairs between threshold refreshes (k_scan: every 4 tiles)
+// eight-wave form: depth windows kept resident in LDS for the whole launch (the rest stream): 2 x 32 KiB
+constexpr int kResidentWindows = 2;
 
 template <int MT, int DT, int S_>
 __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
@@ -331,6 +333,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     // appended 850 / 897 / 1128 candidates per query and took 3.51 / 3.41 / 3.32 ms: the refresh costs more than
     // the candidates it saves
     const int RT = std::max(1, a.refresh_every);
+    // windows [0, NR) stay resident for the whole launch; [NR, NW) stream through lb0 / lb1 (window w in
+    // buffer (w - NR) & 1), each staged during the window before it
+    constexpr int NR = NW < kResidentWindows ? NW : kResidentWindows;
+    __shared__ __attribute__((aligned(16))) u32x4 lres[NR][WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
     __shared__ __attribute__((aligned(16))) float th_lds[128];
@@ -377,7 +383,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 #pragma unroll
         for (int i = 0; i < kWN; ++i) rb[i] = ld(r0, kWN + i);
     }
-    stage(0, lb0);
+#pragma unroll
+    for (int w = 0; w < NR; ++w) stage(w, lres[w]);
+    if constexpr (NR < NW) stage(NR, lb0);
 
     // refresh share of this wave: block wb = wv & 3, registers [8 * (wv >> 2), + 8)
     const int wb = wv & 3, i0 = 8 * (wv >> 2);
@@ -449,12 +457,17 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             u32x4(&ring)[kWN] = (w & 1) ? rb : ra;
-            if (w > 0 || u > 0) {
-                // this wave's DMA for window w landed (the previous window's 8 ring refills were issued after it)
+            if (w >= NR && (w > NR || u > 0)) {
+                // streamed window w: this wave's DMA for it landed (the previous window's 8 ring refills were
+                // issued after it), every wave's (barrier); every wave is also through window w - 1, whose
+                // buffer the next staging refills
                 asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
             }
-            stage((w + 1) % NW, (w & 1) ? lb0 : lb1);
+            // stage window w + 1 when it streams (window NR, the first, is staged during window NR - 1: its
+            // buffer was last read by window NW - 2 of the previous tile, which every wave finished before
+            // window NW - 1's barrier)
+            if (w + 1 >= NR && w + 1 < NW) stage(w + 1, ((w + 1 - NR) & 1) ? lb1 : lb0);
             if (refresh && w == NW - 1) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
@@ -462,7 +475,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
             }
             unsigned qo = (unsigned)lane;
             asm volatile("" : "+v"(qo));
-            const u32x4* qs = ((w & 1) ? lb1 : lb0) + qo;
+            const u32x4* qs = (w < NR ? lres[w < NR ? w : 0] : (((w - NR) & 1) ? lb1 : lb0)) + qo;
             auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * kWN * 2 + i * 2 + (qb & 1)) * 64]; };
             u32x4 qf[2][4];
 #pragma unroll

@@ -845,7 +845,7 @@ def test_fuzz_filters_and_large_k_vs_oracle(native, case):
                                              (256, "bf16", 30_000, 65, 32), (1024, "bf16", 9_000, 128, 128),
                                              (128, "f32", 20_000, 150, 10), (1024, "bf16", 100_000, 128, 10),
                                              (768, "bf16", 50_000, 100, 20), (1024, "f16", 30_000, 150, 5),
-                                             (768, "f16", 20_000, 192, 32)])
+                                             (768, "f16", 20_000, 192, 32), (768, "f32", 20_000, 130, 45)])
 def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
     """B > 64: ceil(B/64) workgroup groups stream the same tiles in one pass (one XCD per range
     block), each with 64 queries in LDS; per-group private candidate regions, thresholds and
@@ -906,7 +906,8 @@ def test_query_group_edges_vs_oracle(native, dim, dtype, metric):
 @pytest.mark.parametrize("dim,dtype,n,B,k", [(256, "bf16", 20_011, 128, 10), (512, "f16", 33_333, 97, 16),
                                              (768, "bf16", 41_000, 129, 20), (1024, "bf16", 70_001, 256, 10),
                                              (1024, "f16", 3_000, 80, 5), (512, "bf16", 64, 128, 3),
-                                             (1024, "bf16", 1_000_003, 128, 10)])
+                                             (1024, "bf16", 1_000_003, 128, 10), (1024, "f32", 50_001, 128, 10),
+                                             (768, "f32", 20_000, 200, 16), (256, "f32", 3_001, 65, 5)])
 def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
     """65..256 queries at D = 256..1024 (bf16 / f16, k <= 22) take the 128-query FILTER: one workgroup per CU
     scores every tile pair once for two 64-query groups, the queries streaming through LDS in depth
@@ -914,8 +915,9 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
     waves walk the windows on zero-record V#s), a padded second set (B = 129, 80, 97), a mask, deleted rows,
     ip scores: identical to the oracle and to the same queries 64 at a time."""
     rng = np.random.default_rng(dim + B + n)
-    # (raw inner products of the synthetic rows overflow f16 storage: ip on bf16 only)
-    for metric in ("cosine", "ip") if dtype == "bf16" else ("cosine",):
+    # (raw inner products of the synthetic rows overflow f16 storage: ip on bf16 / fp32 only; fp32 rows reach the
+    # MFMA as f16 for cosine, bf16 for ip)
+    for metric in ("cosine", "ip") if dtype != "f16" else ("cosine",):
         idx = native.NativeIndex(dim, dtype, metric)
         idx.add_synthetic(9, 0, n)
         raw = R.gen_rows(9, 0, n, dim)

@@ -346,10 +346,12 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     p->QB = QB;
     // More than 64 queries: up to HIPRAG_MAX_GROUPS (default 4) groups of 64 share one corpus pass --
     // each group's workgroups stream the same tiles on one XCD, the others reading them from L2
-    // (DESIGN.md "Query groups").  fp32 corpora (2 KiB k-steps) keep one group.
+    // (DESIGN.md "Query groups").  fp32 corpora (2 KiB k-steps) form groups only at the dims the 128-query FILTER
+    // takes (below); elsewhere they keep one group.
     static const int mg_env = getenv("HIPRAG_MAX_GROUPS") ? atoi(getenv("HIPRAG_MAX_GROUPS")) : 4;
     const int max_groups = std::max(1, std::min(8, mg_env));
-    p->NG = (QB == 2 && h->dtype != F32) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
+    // (fp32 rows form groups only where the 128-query FILTER takes them: its eight-wave form reads fp32 rows)
+    p->NG = (QB == 2 && (h->dtype != F32 || wide_filter_ok(h->dtype, h->S))) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
     // D > 1280 (Youtu-Embedding's 2048 / 2304 dims) leaves LDS for one 32-query block only: a 64-query
     // batch was two corpus passes; 32-query groups share one (HIPRAG_QB1_GROUPS=0: separate passes, A/B)
     static const int qb1_env = getenv("HIPRAG_QB1_GROUPS") ? atoi(getenv("HIPRAG_QB1_GROUPS")) : 1;

@@ -23,8 +23,9 @@
 // Timing prototype and its measurements: tools/q128_proto.hip (10M x 1024 bf16, 128 queries: 3.01 ms on 224
 // CUs against 2.92 ms with the staging switched off, 3.37 ms with one tile per wave, 3.77 ms with register
 // staging).
-// Scope: bf16 / f16 corpora, D a multiple of 256 up to 1024 (S = 16, 32, 48, 64 k-steps), one row part (kc <= 32),
-// cosine / inner product, no tile list -- every other FILTER keeps k_scan's query groups.
+// Scope: bf16 / f16 / fp32 corpora (fp32: the eight-wave form), D a multiple of 256 up to 1024 (S = 16, 32, 48, 64
+// k-steps), one row part (kc <= 32), cosine / inner product, no tile list -- every other FILTER keeps k_scan's query
+// groups.
 #include "hr_internal.hpp"
 #include "hr_kernels.hpp"
 
@@ -324,18 +325,24 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
 // and appends as in k_filter_wide; a refresh splits each query block's 16 registers between two waves.
 template <int MT, int DT, int S_>
 __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
-    static_assert(DT != F32, "1 KiB k-step chunks (bf16 / f16 corpora)");
-    static_assert(S_ % (2 * kWN) == 0, "an even number of windows per tile (the ring halves alternate by window)");
-    constexpr int NW = S_ / kWN;
-    constexpr int WQ = kWN * 4 * 64;   // u32x4 per window buffer: [group][k-step][block][lane]
-    constexpr int PER = WQ / 512;      // LDS-DMA chunks per thread per window
+    // fp32 rows: 2 KiB k-step chunks (two 16-byte loads per lane, rounded to the MFMA type on use, as k_scan's
+    // XFrag<F32>), so a window / ring half is 4 k-steps -- the same 8 loads and 16 KiB in flight per wave
+    constexpr int LPC = DT == F32 ? 2 : 1;  // 16-byte loads per lane per k-step chunk
+    constexpr int WN = kWN / LPC;           // k-steps per query window and per ring half
+    static_assert(S_ % (2 * WN) == 0, "an even number of windows per tile (the ring halves alternate by window)");
+    constexpr int NW = S_ / WN;
+    constexpr int WQ = WN * 4 * 64;   // u32x4 per window buffer: [group][k-step][block][lane]
+    constexpr int PER = WQ / 512;     // LDS-DMA chunks per thread per window
     // rounds between refreshes (k_scan's tiles per refresh: 4).  At 10M rows, B = 128, every 1 / 2 / 4 rounds
     // appended 850 / 897 / 1128 candidates per query and took 3.51 / 3.41 / 3.32 ms: the refresh costs more than
     // the candidates it saves
     const int RT = std::max(1, a.refresh_every);
     // windows [0, NR) stay resident for the whole launch; [NR, NW) stream through lb0 / lb1 (window w in
     // buffer (w - NR) & 1), each staged during the window before it
-    constexpr int NR = NW < kResidentWindows ? NW : kResidentWindows;
+    // (LDS: (NR + 2) windows + the 16.5 KiB key / threshold tables within 160 KiB: 2 windows of 32 KiB resident,
+    // or 6 of 16 KiB for fp32 rows)
+    constexpr int NR_MAX = DT == F32 ? 3 * kResidentWindows : kResidentWindows;
+    constexpr int NR = NW < NR_MAX ? NW : NR_MAX;
     __shared__ __attribute__((aligned(16))) u32x4 lres[NR][WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
@@ -358,30 +365,45 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         return wave_uniform(t < n_tiles ? t : -1);
     };
     auto rsrc = [&](int64_t t) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024)), (short)0,
-                                                 t < 0 ? 0 : S_ * 1024, 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024 * LPC)), (short)0,
+                                                 t < 0 ? 0 : S_ * 1024 * LPC, 0x00020000);
     };
     const int voff = lane * 16;
-    auto ld = [&](__amdgpu_buffer_rsrc_t r, int chunk) -> u32x4 {
-        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024, 2);  // non-temporal
+    // ring slot i (k-step i of a window) holds LPC 16-byte loads: ring[i * LPC + l]
+    auto ld = [&](u32x4* ring, int i, __amdgpu_buffer_rsrc_t r, int chunk) {
+#pragma unroll
+        for (int l = 0; l < LPC; ++l)
+            ring[i * LPC + l] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024 * LPC + l * 1024, 2);  // nt
+    };
+    auto xfrag = [&](const u32x4* ring, int i) -> u32x4 {  // the MFMA B operand of ring slot i
+        if constexpr (LPC == 1) {
+            return ring[i];
+        } else {
+            typedef float f32x8 __attribute__((ext_vector_type(8)));
+            const f32x8 f = __builtin_shufflevector(__builtin_bit_cast(f32x4, ring[2 * i]), __builtin_bit_cast(f32x4, ring[2 * i + 1]),
+                                                    0, 1, 2, 3, 4, 5, 6, 7);
+            if constexpr (MT == BF16) return __builtin_bit_cast(u32x4, __builtin_convertvector(f, bf16x8));
+            else return __builtin_bit_cast(u32x4, __builtin_convertvector(f, f16x8));
+        }
     };
     const __amdgpu_buffer_rsrc_t qr =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 2 * S_ * 2 * 1024, 0x00020000);
-    auto stage = [&](int w, u32x4* buf) {  // chunk c = j * 512 + tid: group c >> 10 (j >> 1), offset c & 1023
+    // chunk c = j * 512 + tid of a window buffer: group j / (PER / 2), position (j % (PER / 2)) * 512 + tid in it
+    auto stage = [&](int w, u32x4* buf) {
         int vo = tid * 16;
         asm volatile("" : "+v"(vo));
 #pragma unroll
         for (int j = 0; j < PER; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 512 + wv * 64),
-                                                     16, vo, (j >> 1) * S_ * 2048 + w * kWN * 2048 + (j & 1) * 8192, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 512 + wv * 64), 16, vo,
+                                                     (j / (PER / 2)) * S_ * 2048 + w * WN * 2048 + (j % (PER / 2)) * 8192, 0, 0);
     };
-    u32x4 ra[kWN], rb[kWN];
+    u32x4 ra[WN * LPC], rb[WN * LPC];
     {
         const auto r0 = rsrc(tile_at(0));
 #pragma unroll
-        for (int i = 0; i < kWN; ++i) ra[i] = ld(r0, i);
+        for (int i = 0; i < WN; ++i) ld(ra, i, r0, i);
 #pragma unroll
-        for (int i = 0; i < kWN; ++i) rb[i] = ld(r0, kWN + i);
+        for (int i = 0; i < WN; ++i) ld(rb, i, r0, WN + i);
     }
 #pragma unroll
     for (int w = 0; w < NR; ++w) stage(w, lres[w]);
@@ -456,7 +478,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         uint32_t key[8];
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
-            u32x4(&ring)[kWN] = (w & 1) ? rb : ra;
+            u32x4(&ring)[WN * LPC] = (w & 1) ? rb : ra;
             if (w >= NR && (w > NR || u > 0)) {
                 // streamed window w: this wave's DMA for it landed (the previous window's 8 ring refills were
                 // issued after it), every wave's (barrier); every wave is also through window w - 1, whose
@@ -476,18 +498,19 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
             unsigned qo = (unsigned)lane;
             asm volatile("" : "+v"(qo));
             const u32x4* qs = (w < NR ? lres[w < NR ? w : 0] : (((w - NR) & 1) ? lb1 : lb0)) + qo;
-            auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * kWN * 2 + i * 2 + (qb & 1)) * 64]; };
+            auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * WN * 2 + i * 2 + (qb & 1)) * 64]; };
             u32x4 qf[2][4];
 #pragma unroll
             for (int qb = 0; qb < 4; ++qb) qf[0][qb] = qfrag(0, qb);
 #pragma unroll
-            for (int i = 0; i < kWN; ++i) {
-                if (i + 1 < kWN) {
+            for (int i = 0; i < WN; ++i) {
+                if (i + 1 < WN) {
 #pragma unroll
                     for (int qb = 0; qb < 4; ++qb) qf[(i + 1) & 1][qb] = qfrag(i + 1, qb);
                 }
-                const u32x4 x = ring[i];
-                ring[i] = (w + 2 < NW) ? ld(rt, (w + 2) * kWN + i) : ld(rn, (w + 2 - NW) * kWN + i);
+                const u32x4 x = xfrag(ring, i);
+                if (w + 2 < NW) ld(ring, i, rt, (w + 2) * WN + i);
+                else ld(ring, i, rn, (w + 2 - NW) * WN + i);
 #pragma unroll
                 for (int qb = 0; qb < 4; ++qb) acc[qb] = mfma32<MT>(qf[i & 1][qb], x, acc[qb]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -583,8 +606,12 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 
 template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
-    if (wide_waves() == 8) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
+    if constexpr (DT == F32) {  // (the tile-pair form is built for 1 KiB k-step chunks only)
+        hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
+    } else {
+        if (wide_waves() == 8) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
+    }
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 
@@ -598,7 +625,7 @@ int wide_waves() {
 
 bool wide_filter_ok(int dtype, int S) {
     static const int env = getenv("HIPRAG_WIDE_FILTER") ? atoi(getenv("HIPRAG_WIDE_FILTER")) : 1;  // 0: query groups (A/B)
-    return env && dtype != F32 && (S == 16 || S == 32 || S == 48 || S == 64);
+    return env && (S == 16 || S == 32 || S == 48 || S == 64);
 }
 
 int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st) {
@@ -606,6 +633,9 @@ int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hip
     if (mt == MTv && dtype == DTv && S == Sv) return launch_t<MTv, DTv, Sv>(cus, a, st);
     HR_WIDE_CASE(BF16, BF16, 64) HR_WIDE_CASE(BF16, BF16, 48) HR_WIDE_CASE(BF16, BF16, 32) HR_WIDE_CASE(BF16, BF16, 16)
     HR_WIDE_CASE(F16, F16, 64) HR_WIDE_CASE(F16, F16, 48) HR_WIDE_CASE(F16, F16, 32) HR_WIDE_CASE(F16, F16, 16)
+    // fp32 rows: the MFMA type follows the metric (mfma_type: cosine -> f16, inner product -> bf16)
+    HR_WIDE_CASE(F16, F32, 64) HR_WIDE_CASE(F16, F32, 48) HR_WIDE_CASE(F16, F32, 32) HR_WIDE_CASE(F16, F32, 16)
+    HR_WIDE_CASE(BF16, F32, 64) HR_WIDE_CASE(BF16, F32, 48) HR_WIDE_CASE(BF16, F32, 32) HR_WIDE_CASE(BF16, F32, 16)
 #undef HR_WIDE_CASE
     return HR_E_UNSUPPORTED;
 }

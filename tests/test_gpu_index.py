@@ -660,7 +660,9 @@ def _embedding_like(rng, n, dim, scale=1.0):
 
 
 L2_CASES = [(128, "bf16", 5000, 16, 10), (768, "f16", 20000, 64, 10), (1024, "f32", 8000, 33, 5),
-            (256, "bf16", 9000, 20, 100), (96, "bf16", 700, 5, 32), (1024, "bf16", 600_000 // 20, 64, 10)]
+            (256, "bf16", 9000, 20, 100), (96, "bf16", 700, 5, 32), (1024, "bf16", 600_000 // 20, 64, 10),
+            # more than 64 queries: the 128-query FILTER with euclidean scores (2 q.x - |x|^2)
+            (1024, "bf16", 40_001, 128, 10), (768, "f32", 20_000, 200, 16), (512, "f16", 9_000, 97, 20)]
 
 
 @pytest.mark.parametrize("dim,dtype,n,B,k", L2_CASES)

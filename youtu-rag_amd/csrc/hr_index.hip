@@ -367,10 +367,11 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     return HR_OK;
 }
 
-// the FILTER of this plan runs as the 128-query pass (hr_wide.hip): query groups in pairs, bf16 / f16, D a multiple
-// of 256, one row part, no tile list, cosine / inner product
+// the FILTER of this plan runs as the 128-query pass (hr_wide.hip): query groups in pairs, D a multiple of 256 up to
+// 1024, one row part, no tile list
 static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list) {
-    return pl.NG >= 2 && pl.QB == 2 && np == 1 && !tile_list && h->metric != L2 && wide_filter_ok(h->dtype, h->S);
+    return pl.NG >= 2 && pl.QB == 2 && np == 1 && !tile_list && (h->metric != L2 || wide_waves() == 8) &&
+           wide_filter_ok(h->dtype, h->S);
 }
 
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
@@ -451,7 +452,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // more than 64 queries (query groups) in a plain FILTER: the 128-query pass reads every tile once for
     // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
     if constexpr (MODE == SCAN_FILTER && DT != F32) {
-        if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && !a.xnorm && a.use_groups && !a.stamps) {
+        if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups && !a.stamps) {
             // waves: one candidate region per (group, wave); a wave takes a tile (8 waves) or a tile pair (4)
             const int wpb = wide_waves();
             const int64_t units = wpb == 8 ? a.n_units : (a.n_units + 1) / 2;

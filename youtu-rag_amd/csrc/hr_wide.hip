@@ -24,8 +24,8 @@
 // CUs against 2.92 ms with the staging switched off, 3.37 ms with one tile per wave, 3.77 ms with register
 // staging).
 // Scope: bf16 / f16 / fp32 corpora (fp32: the eight-wave form), D a multiple of 256 up to 1024 (S = 16, 32, 48, 64
-// k-steps), one row part (kc <= 32), cosine / inner product, no tile list -- every other FILTER keeps k_scan's query
-// groups.
+// k-steps), one row part (kc <= 32), cosine / inner product (and euclidean: the eight-wave form), no tile list --
+// every other FILTER keeps k_scan's query groups.
 #include "hr_internal.hpp"
 #include "hr_kernels.hpp"
 
@@ -476,6 +476,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[qb][i] = 0.0f;
         uint32_t key[8];
+        const int rg = slot_row(t < 0 ? 0 : t, g);  // row of the tile held by this lane's slot
+        float xs = 0.0f;  // euclidean: the row's fp32 |x|^2 (score 2 q.x - |x|^2, as k_scan)
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             u32x4(&ring)[WN * LPC] = (w & 1) ? rb : ra;
@@ -495,6 +497,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 for (int j = 0; j < 8; ++j)
                     key[j] = __hip_atomic_load(keys_w + qoff_i(i0 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            // (issued before the last window's refills, like the keys: read after the k-loop, it waits for nothing
+            // newer than itself)
+            if (a.xnorm && w == NW - 1 && t >= 0) xs = a.xnorm[t * 32 + rg];
             unsigned qo = (unsigned)lane;
             asm volatile("" : "+v"(qo));
             const u32x4* qs = (w < NR ? lres[w < NR ? w : 0] : (((w - NR) & 1) ? lb1 : lb0)) + qo;
@@ -520,8 +525,13 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         // epilogue: fast test (acc - th >= 0 exactly when acc >= th; see k_filter_wide), then, for a tile with a
         // hit, the exact per-register compares, group maxima (ds_max, scores at or above their threshold
         // only) and appends
-        const int rg = slot_row(t < 0 ? 0 : t, g);
         const bool ok = (allow >> rg) & 1u;
+        if (a.xnorm) {
+#pragma unroll
+            for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[qb][i] = __builtin_fmaf(2.0f, acc[qb][i], -xs);
+        }
         float d = -__builtin_inff();
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)

@@ -430,6 +430,7 @@ def main():
     # three records: before SAMPLE, between the two, after FILTER): each event record leaves a
     # ~6 us bubble on the scan stream, so timing every launch would slow the steps being measured
     index.set_scan_timing(TIME_EVERY)
+    wide0 = index.wide_launches()
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -442,6 +443,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     sample_ms, scan_ms = index.take_scan_times()
+    wide_per_step = (index.wide_launches() - wide0) / args.steps  # 128-query FILTER launches per batch
     # one untimed batch of isotropic queries (the worst case for ranking: no planted neighbour), for the
     # recall checks; every rank takes part (the merge is collective)
     q_iso = isotropic_queries(B, D)
@@ -463,9 +465,9 @@ def main():
     n_max_local = -(-N // G)
     alg_bytes = n_max_local * D * esz  # corpus bytes one filter-scan launch must read (largest shard)
     # FILTER launches per batch (the timed events bracket them all): 65-128 queries are one launch of the 128-query
-    # FILTER (hr_wide.hip: bf16 / f16, D a multiple of 256 up to 1024, k <= 22), 129-256 two; otherwise one launch
-    wide = B > 64 and args.dtype in ("bf16", "f16") and D % 256 == 0 and D <= 1024 and K <= 22
-    passes = -(-B // 128) if wide else 1
+    # FILTER (hr_wide.hip), 129-256 two -- counted by the index (hr_index_wide_launches); otherwise one launch
+    wide = wide_per_step > 0
+    passes = max(1, round(wide_per_step)) if wide else 1
     achieved = passes * alg_bytes / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
     mfma_flops = 2 * 32 * -(-B // 32) * n_max_local * D  # padded query slots x rows x dims per FILTER launch
     mfma_tflops = mfma_flops / (scan_avg * 1e-3) / 1e12 if scan_avg > 0 else 0.0

@@ -237,6 +237,9 @@ int hr_index_stats(hr_index* h, int64_t out[3]);
  * untimed search with k <= HR_MAX_K, from the second call of a (B, k) shape on; HIPRAG_SYNC_GRAPH=0
  * turns the graphs off).  The results are those of the normal path: the graph is that path, captured. */
 int hr_index_graph_replays(hr_index* h, int64_t* out);
+/* Diagnostics: 128-query FILTER launches issued so far (65..256-query chunks at D = 256..1024; graph replays
+ * not counted) -- tests use it to check which FILTER served a batch. */
+int hr_index_wide_launches(hr_index* h, int64_t* out);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

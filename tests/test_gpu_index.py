@@ -909,14 +909,21 @@ def test_query_group_edges_vs_oracle(native, dim, dtype, metric):
                                              (768, "bf16", 41_000, 129, 20), (1024, "bf16", 70_001, 256, 10),
                                              (1024, "f16", 3_000, 80, 5), (512, "bf16", 64, 128, 3),
                                              (1024, "bf16", 1_000_003, 128, 10), (1024, "f32", 50_001, 128, 10),
-                                             (768, "f32", 20_000, 200, 16), (256, "f32", 3_001, 65, 5)])
+                                             (768, "f32", 20_000, 200, 16), (256, "f32", 3_001, 65, 5),
+                                             # row parts (kc > 32: 2..7 parts of 32 groups), and k = 128 on bf16
+                                             # (kc 192: 6 parts, beyond the 5 key tables) in query groups
+                                             (1024, "bf16", 100_003, 128, 50), (768, "f16", 41_000, 130, 100),
+                                             (512, "f32", 30_001, 128, 64), (256, "f32", 20_011, 256, 128),
+                                             (1024, "bf16", 20_000, 97, 128)])
 def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
-    """65..256 queries at D = 256..1024 (bf16 / f16, k <= 22) take the 128-query FILTER: one workgroup per CU
-    scores every tile pair once for two 64-query groups, the queries streaming through LDS in depth
-    windows.  Odd tile counts (a pair's second tile read through a one-tile V#), fewer pairs than waves (idle
-    waves walk the windows on zero-record V#s), a padded second set (B = 129, 80, 97), a mask, deleted rows,
-    ip scores: identical to the oracle and to the same queries 64 at a time."""
+    """65..256 queries at D = 256..1024 take the 128-query FILTER: one workgroup per CU scores every tile once
+    for two 64-query groups, the queries streaming through LDS in depth windows.  Fewer tiles than waves (idle
+    waves walk the windows on zero-record V#s), a padded second set (B = 129, 80, 97), fp32 rows, row parts
+    (k > 16), a mask, deleted rows, ip scores: identical to the oracle and to the same queries 64 at a time.
+    The first unmasked search must have launched the 128-query FILTER exactly where the plan takes it."""
     rng = np.random.default_rng(dim + B + n)
+    kc = native.kc_for_k(k, dim)
+    wide_expected = (kc + 31) // 32 <= (7 if dtype == "f32" else 5)
     # (raw inner products of the synthetic rows overflow f16 storage: ip on bf16 / fp32 only; fp32 rows reach the
     # MFMA as f16 for cosine, bf16 for ip)
     for metric in ("cosine", "ip") if dtype != "f16" else ("cosine",):
@@ -930,8 +937,11 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
         allowed = rng.random(n) < 0.7
         for m in (None, allowed):
             mk = None if m is None else oracle.mask_from_bool(m)
+            w0 = idx.wide_launches()
             s, r = idx.search(q, k, mk)
             _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk, metric=metric))
+            if m is None:
+                assert (idx.wide_launches() > w0) == wide_expected
         parts = [idx.search(q[i:i + 64], k) for i in range(0, B, 64)]
         s, r = idx.search(q, k)
         np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))

@@ -6,7 +6,7 @@ mkdir -p $O
 L=youtu-rag_amd/hiprag
 timeout -k 10 600 python -u -m pytest tests/test_gpu_index.py -x -q --timeout 300 --timeout-method thread -k "wide or query_group" > $O/wide_tests.log 2>&1
 rc=$?; echo "wide tests rc=$rc"; tail -3 $O/wide_tests.log; [ $rc -ne 0 ] && exit $rc
-for cfg in "HIPRAG_WIDE_FILTER=1" "HIPRAG_LIB_OVERRIDE=$L/libhiprag_noapp.so"; do
+for cfg in "HIPRAG_WIDE_FILTER=1"; do
   env $cfg timeout -k 10 200 python -u tools/diag_wide.py --reps 20 >> $O/diag.jsonl 2>> $O/diag.err || { echo "$cfg failed"; exit 1; }
   tail -1 $O/diag.jsonl
 done

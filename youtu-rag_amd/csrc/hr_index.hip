@@ -368,10 +368,14 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
 }
 
 // the FILTER of this plan runs as the 128-query pass (hr_wide.hip): query groups in pairs, D a multiple of 256 up to
-// 1024, one row part, no tile list
+// 1024, no tile list; row parts (kc > 32), euclidean scores and fp32 rows in the eight-wave form only
 static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list) {
-    return pl.NG >= 2 && pl.QB == 2 && np == 1 && !tile_list && (h->metric != L2 || wide_waves() == 8) &&
-           wide_filter_ok(h->dtype, h->S);
+    const bool eight = wide_waves() == 8;
+    // (HIPRAG_WIDE_PARTS: most row parts it takes, A/B)
+    static const int parts_env = getenv("HIPRAG_WIDE_PARTS") ? atoi(getenv("HIPRAG_WIDE_PARTS")) : 99;
+    const int max_parts = std::max(1, std::min(parts_env, wide_max_parts(h->dtype)));
+    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || (eight && np <= max_parts)) &&
+           (eight || (h->metric != L2 && h->dtype != F32)) && wide_filter_ok(h->dtype, h->S);
 }
 
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
@@ -451,7 +455,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     const bool dflt = pl.NG > 1 || (MODE == SCAN_SAMPLE && !sample_nt);
     // more than 64 queries (query groups) in a plain FILTER: the 128-query pass reads every tile once for
     // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
-    if constexpr (MODE == SCAN_FILTER && DT != F32) {
+    if constexpr (MODE == SCAN_FILTER) {
         if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups && !a.stamps) {
             // waves: one candidate region per (group, wave); a wave takes a tile (8 waves) or a tile pair (4)
             const int wpb = wide_waves();
@@ -474,6 +478,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
                 b.pcnt = sc.pcnt.as<uint32_t>() + (int64_t)set * 2 * W * 64;
                 b.capw = kCapW;
                 if (int rc = launch_filter_wide(MT, DT, h->S, blocks, b, st)) return set_err(rc, "wide FILTER launch failed");
+                h->n_wide++;
             }
             return HR_OK;
         }
@@ -1822,6 +1827,16 @@ extern "C" int hr_index_stats(hr_index* h, int64_t out[3]) {
     out[1] = h->n_guard_fail;
     out[2] = h->n_exhaustive;
     if (h->G > 1) group_stats(h, out);
+    return HR_OK;
+}
+
+// diagnostics: 128-query FILTER launches issued by this index (summed over a group's shards)
+extern "C" int hr_index_wide_launches(hr_index* h, int64_t* out) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *out = h->n_wide;
+    for (hr_index* s : h->shards)
+        if (s != h) *out += s->n_wide;
     return HR_OK;
 }
 

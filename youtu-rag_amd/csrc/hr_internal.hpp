@@ -75,6 +75,10 @@ struct ScanArgs;
 bool wide_filter_ok(int dtype, int S);
 int wide_waves();  // 8 (one tile per wave, 512 threads) or 4 (tile pairs, 256 threads)
 int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st);
+// row parts of the eight-wave form (kc > 32): 32 groups per part, one 16 KiB key table each in LDS beside the two
+// streamed window buffers (2 x 32 KiB, or 2 x 16 KiB for fp32 rows): at most 5 (bf16 / f16) or 7 (fp32) parts,
+// kc <= 160 / 224
+constexpr int wide_max_parts(int dtype) { return dtype == F32 ? 7 : 5; }
 }  // namespace hr
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
@@ -149,6 +153,7 @@ struct hr_index {
     const Scratch* last_scr = nullptr;  // set of the most recent FILTER launch (diagnostics)
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
     int64_t n_guard_fail = 0;         // queries that failed the exactness guard (collect fallback)
+    int64_t n_wide = 0;               // 128-query FILTER launches issued (hr_wide.hip; not graph replays)
     std::vector<float> floor_host;
     // ---- hr_index_search (host queries, no mask) replayed as one HIP graph per batch shape: H2D of
     // the queries from pinned staging, prep, SAMPLE, FILTER, select, rescore, merge, D2H of results

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
 // wave's epilogue runs beside the other wave's MFMAs on its SIMD -- with 128 queries per tile a third of the tiles
 // hold a candidate (10M rows, k = 10), so the epilogue is no longer rare.  Group maxima, thresholds, refreshes
 // and appends as in k_filter_wide; a refresh splits each query block's 16 registers between two waves.
-template <int MT, int DT, int S_>
+template <int MT, int DT, int S_, bool PARTS = false>
 __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     // fp32 rows: 2 KiB k-step chunks (two 16-byte loads per lane, rounded to the MFMA type on use, as k_scan's
     // XFrag<F32>), so a window / ring half is 4 k-steps -- the same 8 loads and 16 KiB in flight per wave
@@ -341,27 +341,41 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     // buffer (w - NR) & 1), each staged during the window before it
     // (LDS: (NR + 2) windows + the 16.5 KiB key / threshold tables within 160 KiB: 2 windows of 32 KiB resident,
     // or 6 of 16 KiB for fp32 rows)
-    constexpr int NR_MAX = DT == F32 ? 3 * kResidentWindows : kResidentWindows;
+    // With row parts (PARTS: kc > 32, np parts of 32 groups each) the per-part key tables take the resident
+    // windows' LDS: none stay resident
+    constexpr int NR_MAX = PARTS ? 0 : (DT == F32 ? 3 * kResidentWindows : kResidentWindows);
     constexpr int NR = NW < NR_MAX ? NW : NR_MAX;
-    __shared__ __attribute__((aligned(16))) u32x4 lres[NR][WQ];
+    constexpr int KP = PARTS ? wide_max_parts(DT) : 1;  // key tables (row parts) in LDS
+    __shared__ __attribute__((aligned(16))) u32x4 lres[NR > 0 ? NR : 1][WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
     __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
     __shared__ __attribute__((aligned(16))) float th_lds[128];
-    __shared__ __attribute__((aligned(16))) uint32_t G[4][16][64];
+    __shared__ __attribute__((aligned(16))) uint32_t G[KP][4][16][64];
+    // row parts: per part the min over its 32 groups' keys at that part's last refresh, per query
+    __shared__ __attribute__((aligned(16))) float pmin[KP][128];
+    const int np = PARTS ? a.np : 1;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
     const int64_t W = (int64_t)gridDim.x * 8;
     const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;
     const int64_t n_tiles = a.n_units;
-    const int64_t rounds = (n_tiles + W - 1) / W;
-    const int64_t full_rounds = n_tiles / W;
+    // row parts: deal position s takes tile (s % np) * part_tiles + s / np, so every round spans all parts (a part's
+    // group maxima bound nothing until every part has some: parts dealt one after another would leave the
+    // threshold at the floor until the last part); positions past the last part's end hold no tile
+    const int64_t n_pos = PARTS ? (int64_t)np * a.part_tiles : n_tiles;
+    const int64_t rounds = (n_pos + W - 1) / W;
+    const int64_t full_rounds = n_pos / W;
     auto tile_at = [&](int64_t u) -> int64_t {  // -1: no tile this round (zero-record V#)
         int64_t pos = wr;
         if (HR_ROTATE_ROUNDS && u < full_rounds) {
             pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
             if (pos >= W) pos -= W;
         }
-        const int64_t t = u * W + pos;
+        int64_t t = u * W + pos;
+        if constexpr (PARTS) {
+            const uint32_t s = (uint32_t)t;
+            t = t < n_pos ? (int64_t)(s % (uint32_t)np) * a.part_tiles + (int64_t)(s / (uint32_t)np) : n_tiles;
+        }
         return wave_uniform(t < n_tiles ? t : -1);
     };
     auto rsrc = [&](int64_t t) {
@@ -413,14 +427,19 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     const int wb = wv & 3, i0 = 8 * (wv >> 2);
     uint32_t* const keys_w = a.mkeys + (wb * 32 + 4 * half) * 32 + g;
     auto qoff_i = [](int i) { return 32 * ((i & 3) + 8 * (i >> 2)); };
-    auto publish_refresh = [&](const float (&m)[8], const uint32_t (&key)[8], bool publish) {
+    // refresh of part p (p = 0 without parts): publish this wave's share of G[p] (m) where it beats the global key,
+    // the min over the part's 32 groups -> pmin, the threshold = max(old, floor, min over the parts' mins).  With
+    // parts, each refresh serves one part in rotation: the other parts' mins are older, hence lower -- still a
+    // valid bound on the (32 np)-th best score
+    auto publish_refresh = [&](const float (&m)[8], const uint32_t (&key)[8], bool publish, int p) {
+        uint32_t* const kp = keys_w + (int64_t)p * a.pstride;
         float th8[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int i = i0 + j;
             uint32_t k = key[j] > HR_KEY_NEG_INF ? key[j] : HR_KEY_NEG_INF;
             if (publish && a.publish && m[j] > key2f(k)) {
-                atomicMax(keys_w + qoff_i(i), f2key(m[j]));
+                atomicMax(kp + qoff_i(i), f2key(m[j]));
                 k = f2key(m[j]);
             }
             float f = key2f(k);
@@ -433,23 +452,36 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
             for (int j = 0; j < 8; ++j) {
                 const int i = i0 + j;
                 const int q = wb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
-                th_lds[q] = fmaxf(th_lds[q], fmaxf(th8[j], a.floor_q[q]));
+                float f = th8[j];
+                if constexpr (PARTS) {
+                    pmin[p][q] = f;
+                    for (int p2 = 0; p2 < np; ++p2) f = fminf(f, pmin[p2][q]);
+                }
+                th_lds[q] = fmaxf(th_lds[q], fmaxf(f, a.floor_q[q]));
             }
         }
     };
     if (tid < 128) th_lds[tid] = -__builtin_inff();
+    for (int p = 0; p < KP; ++p) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) G[wb][i0 + j][lane] = HR_KEY_NEG_INF;
+        for (int j = 0; j < 8; ++j) G[p][wb][i0 + j][lane] = HR_KEY_NEG_INF;
+        if (tid < 128) pmin[p][tid] = -__builtin_inff();  // (parts beyond np stay out of the minimum below)
+    }
     __syncthreads();
-    {
+    if constexpr (PARTS) {  // every part's minimum first, then the thresholds from all of them
+        if (tid < 128)
+            for (int p = np; p < KP; ++p) pmin[p][tid] = __builtin_inff();
+    }
+    for (int p = 0; p < np; ++p) {
         uint32_t key[8];
         float m[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            key[j] = __hip_atomic_load(keys_w + qoff_i(i0 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            key[j] = __hip_atomic_load(keys_w + (int64_t)p * a.pstride + qoff_i(i0 + j), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             m[j] = -__builtin_inff();
         }
-        publish_refresh(m, key, false);
+        publish_refresh(m, key, false, p);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
@@ -470,6 +502,10 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         const uint32_t allow = next_allow;
         next_allow = allow_word(tn);
         const bool refresh = u > 0 && (u % RT) == 0;  // workgroup-uniform
+        // the part whose keys the refresh prefetches (rotating; a refresh serves every part) and the part of this
+        // wave's tile (its G table)
+        const int pr = PARTS ? (int)((u / RT) % np) : 0;
+        const int pt = PARTS && t >= 0 ? (int)(t / a.part_tiles) : 0;
         f32x16 acc[4];
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)
@@ -492,10 +528,15 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
             // buffer was last read by window NW - 2 of the previous tile, which every wave finished before
             // window NW - 1's barrier)
             if (w + 1 >= NR && w + 1 < NW) stage(w + 1, ((w + 1 - NR) & 1) ? lb1 : lb0);
+            // no resident windows (row parts): window 0 of the next tile streams too, staged during the last window
+            // into lb0 (NW is even: window NW - 2, lb0's last reader, is done everywhere at this window's barrier)
+            if constexpr (NR == 0)
+                if (w == NW - 1 && u + 1 < rounds) stage(0, lb0);
             if (refresh && w == NW - 1) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    key[j] = __hip_atomic_load(keys_w + qoff_i(i0 + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    key[j] = __hip_atomic_load(keys_w + (int64_t)pr * a.pstride + qoff_i(i0 + j), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
             }
             // (issued before the last window's refills, like the keys: read after the k-loop, it waits for nothing
             // newer than itself)
@@ -580,7 +621,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
                 const bool pass = ok && v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
                 const uint64_t msk = __ballot(pass);
-                if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
+                if (HR_WIDE_GMAX && pass) atomicMax(&G[pt][qb][i][lane], f2key(v));
                 if (!HR_WIDE_APPEND || !msk) continue;
                 const int gq = qb >> 1;
                 uint32_t cnt = gq ? mycnt[1] : mycnt[0];
@@ -601,13 +642,22 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 else mycnt[0] = cnt;
             }
         }
-        if (refresh) {  // this wave's share of block wb, swapped out of G
-            float m[8];
+        if (refresh) {  // this wave's share of block wb, swapped out of G -- every part's (part pr's keys prefetched)
+            for (int p = 0; p < np; ++p) {
+                const int pp = PARTS ? (pr + p < np ? pr + p : pr + p - np) : 0;
+                if (PARTS && p > 0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                m[j] = key2f(__hip_atomic_exchange(&G[wb][i0 + j][lane], (uint32_t)HR_KEY_NEG_INF, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
-            publish_refresh(m, key, true);
+                    for (int j = 0; j < 8; ++j)
+                        key[j] = __hip_atomic_load(keys_w + (int64_t)pp * a.pstride + qoff_i(i0 + j), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                }
+                float m[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    m[j] = key2f(__hip_atomic_exchange(&G[pp][wb][i0 + j][lane], (uint32_t)HR_KEY_NEG_INF,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                publish_refresh(m, key, true, pp);
+            }
         }
     }
     a.pcnt[wr * 64 + lane] = mycnt[0];
@@ -616,7 +666,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 
 template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
-    if constexpr (DT == F32) {  // (the tile-pair form is built for 1 KiB k-step chunks only)
+    if (a.np > 1) {  // row parts: the eight-wave form only
+        hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_, true>), dim3((unsigned)cus), dim3(512), 0, st, a);
+    } else if constexpr (DT == F32) {  // (the tile-pair form is built for 1 KiB k-step chunks only)
         hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
     } else {
         if (wide_waves() == 8) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);

@@ -43,7 +43,7 @@ EXPORTS = [
     "hr_device_count", "hr_index_debug_approx", "hr_index_last_candidates", "hr_last_error", "hr_abi_version",
     "hr_kc_for_k", "hr_merge_candidates_strided", "hr_index_search_shard_async", "hr_index_add_device_at",
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
-    "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_kc_for_k_dim",
+    "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_index_wide_launches", "hr_kc_for_k_dim",
     "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
     "hr_index_search_collect",
 ]
@@ -121,6 +121,7 @@ def load_library(path: str | None = None):
             "hr_index_last_candidates": [vp, vp, vp],
             "hr_index_stats": [vp, vp],
             "hr_index_graph_replays": [vp, vp],
+            "hr_index_wide_launches": [vp, vp],
             "hr_add_layernorm": [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, i32, vp],
         }
         for name, args in sig.items():
@@ -365,6 +366,12 @@ class NativeIndex:
         out = (ctypes.c_int64 * 3)()
         _check(self.lib.hr_index_stats(self._h, out))
         return {"main_passes": out[0], "guard_failures": out[1], "exhaustive": out[2]}
+
+    def wide_launches(self) -> int:
+        """128-query FILTER launches issued so far (hr_index_wide_launches)."""
+        out = ctypes.c_int64(0)
+        _check(self.lib.hr_index_wide_launches(self._h, ctypes.byref(out)))
+        return out.value
 
     def graph_replays(self) -> int:
         """hr_index_search calls answered by a captured HIP graph (hr_index_graph_replays)."""

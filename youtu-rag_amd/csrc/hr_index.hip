@@ -371,10 +371,16 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
 // 1024, no tile list; row parts (kc > 32), euclidean scores and fp32 rows in the eight-wave form only
 static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list) {
     const bool eight = wide_waves() == 8;
-    // (HIPRAG_WIDE_PARTS: most row parts it takes, A/B)
-    static const int parts_env = getenv("HIPRAG_WIDE_PARTS") ? atoi(getenv("HIPRAG_WIDE_PARTS")) : 99;
-    const int max_parts = std::max(1, std::min(parts_env, wide_max_parts(h->dtype)));
-    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || (eight && np <= max_parts)) &&
+    // Row parts: fp32 rows up to the LDS's 7 (10M x 1024, B = 128, pipelined: k = 20 / 50 / 100 at 20.0k / 19.0k /
+    // 17.3k QPS vs the query groups' 16.2k / 16.0k / 15.7k); 16-bit rows up to 3 parts and one 128-query set
+    // (bf16, k = 20 / 50: B = 128 31.9k / 29.6k vs 28.2k / 27.6k QPS, but B = 256 32.4k / 29.8k vs 33.0k / 32.2k,
+    // and k = 100's 5 parts FILTER in 5.0 vs 4.5 ms: the appends of its slower-rising thresholds cost more than
+    // the L2 re-reads of the groups; profiles/r03_wide_parts_*).  HIPRAG_WIDE_PARTS: most parts it takes (A/B)
+    static const int parts_env = getenv("HIPRAG_WIDE_PARTS") ? atoi(getenv("HIPRAG_WIDE_PARTS")) : -1;
+    const bool f32 = h->dtype == F32;
+    const int max_parts = std::max(1, std::min(parts_env >= 0 ? parts_env : (f32 ? 7 : 3), wide_max_parts(h->dtype)));
+    const bool parts_ok = eight && np <= max_parts && (f32 || pl.NG == 2 || parts_env >= 0);
+    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) &&
            (eight || (h->metric != L2 && h->dtype != F32)) && wide_filter_ok(h->dtype, h->S);
 }
 

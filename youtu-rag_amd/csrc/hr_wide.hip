@@ -33,6 +33,9 @@
 #ifndef HR_WIDE_APPEND
 #define HR_WIDE_APPEND 1
 #endif
+#ifndef HR_WIDE_STAGGER
+#define HR_WIDE_STAGGER 1
+#endif
 #ifndef HR_WIDE_REFRESH
 #define HR_WIDE_REFRESH 1
 #endif
@@ -46,6 +49,31 @@ int wide_waves();
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Cross-lane reductions without LDS round trips (a __shfl_xor is a ds_bpermute, and a 5-step reduction waited for
+// each: 40 serialised LDS round trips per refresh): DPP within each row of 16 lanes (xor 1, xor 2, half-mirror,
+// mirror), then a ds_swizzle (xor 16 within 32 lanes) or four readlanes across the rows
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+// min over the 32 lanes of each half-wave, in every lane
+__device__ __forceinline__ float half_min32(float f) {
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 1,0,3,2
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 2,3,0,1
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, f))));  // row_half_mirror
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x140>(__builtin_bit_cast(uint32_t, f))));  // row_mirror
+    return fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, f), 0x401F)));
+}
+// OR over the wave's 64 lanes, wave-uniform
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= dpp_u32<0xB1>(x);
+    x |= dpp_u32<0x4E>(x);
+    x |= dpp_u32<0x141>(x);
+    x |= dpp_u32<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) | __builtin_amdgcn_readlane((int)x, 16) |
+                      __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
+}
 constexpr int kWN = 8;       // k-steps per query window
 constexpr int kRefreshPairs = 2;  // tile pairs between threshold refreshes (k_scan: every 4 tiles)
 // eight-wave form: depth windows kept resident in LDS for the whole launch (the rest stream): 2 x 32 KiB
@@ -133,8 +161,7 @@ __global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
                 k = f2key(m[i]);
             }
             float f = key2f(k);
-#pragma unroll
-            for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+            f = half_min32(f);
             th16[i] = f;
         }
         if (g == 0) {
@@ -443,8 +470,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 k = f2key(m[j]);
             }
             float f = key2f(k);
-#pragma unroll
-            for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+            f = half_min32(f);
             th8[j] = f;
         }
         if (g == 0) {
@@ -501,7 +527,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         const auto rt = rsrc(t), rn = rsrc(tn);
         const uint32_t allow = next_allow;
         next_allow = allow_word(tn);
-        const bool refresh = u > 0 && (u % RT) == 0;  // workgroup-uniform
+        // workgroup-uniform; staggered over the workgroups (HR_WIDE_STAGGER), so each round a 1 / RT share of
+        // them publishes and reads fresh keys instead of all at once
+        const bool refresh = u > 0 && ((u + (HR_WIDE_STAGGER ? blockIdx.x : 0)) % RT) == 0;
         // the part whose keys the refresh prefetches (rotating; a refresh serves every part) and the part of this
         // wave's tile (its G table)
         const int pr = PARTS ? (int)((u / RT) % np) : 0;
@@ -601,13 +629,7 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                         else bh |= p ? (1u << (b - 32)) : 0u;
                     }
                 }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                bl |= (uint32_t)__shfl_xor((int)bl, off, 64);
-                bh |= (uint32_t)__shfl_xor((int)bh, off, 64);
-            }
-            uint64_t bits = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)bh) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int)bl);
+            uint64_t bits = ((uint64_t)wave_or(bh) << 32) | wave_or(bl);
             while (bits) {
                 const int b = __builtin_ctzll(bits);  // wave-uniform
                 bits &= bits - 1;

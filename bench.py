@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--recall-queries", type=int, default=8, help="planted and isotropic queries of the recall checks")
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
+    p.add_argument("--collective", action="store_true",
+                   help="run the exchange through an RCCL process group even at --gpus 1 (world size 1): the timed "
+                        "loop then includes the all-gather an 8-GPU node runs")
     p.add_argument("--single-process", action="store_true",
                    help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()
@@ -389,8 +392,11 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    elif args.collective:  # world size 1 through RCCL (no launcher: a private rendezvous on 127.0.0.1)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=dev)
     # the rank count the collective library actually sees goes into the JSON line
-    G = dist.get_world_size() if world > 1 else 1
+    G = dist.get_world_size() if dist.is_initialized() else 1
 
     N, D, B, K = args.rows, args.dim, args.batch, args.k
     start = N * rank // G
@@ -415,7 +421,7 @@ def main():
     q_ready.record()
     s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
     r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
-    searcher = ShardedSearch(index, start, max_batch=B, device=dev, max_k=K)
+    searcher = ShardedSearch(index, start, max_batch=B, device=dev, max_k=K, force_collective=args.collective)
 
     # One step = one batch through the whole path.  Steps are pipelined two deep: submit()
     # enqueues batch i (scan, gather, merge, async copy of the guard flags) and finalizes the
@@ -486,7 +492,10 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic: counter-based corpus generator (hiprag.synth), planted queries q = x_j/|x_j| + 0.05·eps",
         "config": {"workload": f"{N / 1e6:g}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, row-sharded",
-                   "rows": N, "dim": D, "batch": B, "k": K, "parallelism": f"rowshard{G}"},
+                   "rows": N, "dim": D, "batch": B, "k": K,
+                   "parallelism": f"rowshard{G}" + ("+rccl" if searcher.collective else ""),
+                   "exchange": (f"RCCL all_gather_into_tensor ({dist.get_backend()})" if searcher.collective
+                                else "none (one shard: local copy)")},
         "roofline": {"bound": "hbm", "kernel": "k_filter_wide8 (128-query FILTER)" if wide else "k_scan (FILTER pass)",
                      "filter_launches_per_batch": passes, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -579,6 +588,7 @@ def main():
         print(json.dumps(result), flush=True)
     if G > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

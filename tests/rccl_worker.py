@@ -1,0 +1,86 @@
+"""Child process of tests/test_gpu_rccl.py: the production exchange of hiprag.dist.ShardedSearch
+through a REAL RCCL process group (backend "nccl", world size 1, one GPU).
+
+Usage: python tests/rccl_worker.py <port> <queries.npz> <out.npz> <rows> <dim>
+
+At world size 1 the exchange is normally a local copy; ``force_collective=True`` sends the packed
+per-shard records through ``all_gather_into_tensor`` and src_rank batches through ``broadcast`` on the
+tail / scan streams -- the branch an 8-GPU node runs (dist.py ``_all_gather`` / ``_broadcast``).  A
+subclass forces every query of one batch through the collect fallback, so ``_fallback``'s second
+all-gather runs too.  Every collective call is counted and the backend is reported, so the parent can
+assert the RCCL branch executed.  Runs in its own process so a hung communicator is bounded by the
+parent's timeout.
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (REPO, os.path.join(REPO, "youtu-rag_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+
+def main(port: int, q_path: str, out_path: str, rows: int, dim: int) -> None:
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    # the process group first, with its device: RCCL's communicator is created eagerly on it
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    backend = dist.get_backend()
+
+    from hiprag import _native
+    from hiprag.dist import ShardedSearch
+
+    counts = {"all_gather_into_tensor": 0, "broadcast": 0}
+    real_ag, real_bc = dist.all_gather_into_tensor, dist.broadcast
+
+    def ag(*a, **kw):
+        counts["all_gather_into_tensor"] += 1
+        return real_ag(*a, **kw)
+
+    def bc(*a, **kw):
+        counts["broadcast"] += 1
+        return real_bc(*a, **kw)
+
+    dist.all_gather_into_tensor, dist.broadcast = ag, bc
+
+    q = np.load(q_path)["q"]  # (2, B, dim): planted batch, isotropic batch
+    nb, B, _ = q.shape
+    k = 10
+    idx = _native.NativeIndex(dim, "bf16", "cosine", device=0)
+    idx.reserve(rows)
+    idx.add_synthetic(0, 0, rows)
+    qd = torch.from_numpy(q).to(dev)
+    ready = torch.cuda.Event()
+    ready.record()
+
+    ss = ShardedSearch(idx, 0, max_batch=B, device=dev, max_k=k, force_collective=True)
+    n_out = 6
+    s = torch.empty((n_out, B, k), dtype=torch.float32, device=dev)
+    r = torch.empty((n_out, B, k), dtype=torch.int64, device=dev)
+    # 0-3: the bench's pipelined path (scan + tail streams, early SAMPLE, two slots), planted / isotropic
+    for i in range(4):
+        ss.submit(qd[i % 2], k, s_out=s[i], r_out=r[i], q_ready=ready)
+    ss.finalize_all()
+    # 4: a batch known to rank 0 only, broadcast on the scan stream before the scan
+    ss.finalize(ss.submit(qd[0].clone(), k, s_out=s[4], r_out=r[4], q_ready=ready, src_rank=0))
+
+    # 5: every query of the isotropic batch forced through the collect fallback (second all-gather)
+    class ForcedFallback(ShardedSearch):
+        def _failed_queries(self, slot, B):
+            return np.arange(B)
+
+    ff = ForcedFallback(idx, 0, max_batch=B, device=dev, max_k=k, force_collective=True)
+    ff.search(qd[1], k, s_out=s[5], r_out=r[5])
+    torch.cuda.synchronize()
+    np.savez(out_path, s=s.cpu().numpy(), r=r.cpu().numpy(), backend=np.array(backend),
+             ag=np.array(counts["all_gather_into_tensor"]), bc=np.array(counts["broadcast"]))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))

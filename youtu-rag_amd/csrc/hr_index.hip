@@ -387,7 +387,7 @@ static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list)
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
 static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
     const int ng = std::max(1, a.ng);
-    auto kern = k_scan<MT, DT, QB, P, MODE, NT, TPB>;
+    auto kern = scan_kernel<MT, DT, QB, P, MODE, NT, TPB>();
     static std::mutex attr_mu;
     static int attr_lds[64] = {};     // per device: largest dynamic LDS already allowed
     static int occ[64][4] = {};       // per device: blocks/CU for lds buckets (0 = unknown), per instantiation

@@ -382,8 +382,10 @@ enum { SCAN_SAMPLE = 0, SCAN_FILTER = 1, SCAN_COLLECT = 2 };
 // TPB: threads per workgroup (512 = 8 waves, 2 per SIMD, <= 256 registers each).  A 4-wave variant
 // with a 32- / 64-deep corpus ring (one wave per SIMD, up to 512 registers) was measured for the
 // query-group launches and was slower (B = 128 at 10M rows: 5.7 / 6.3 ms vs 4.6 ms), so it is not built.
-template <int MT, int DT, int QB, int P, int MODE, bool NT = true, int TPB = 512>
-__global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) {  // (2nd: min waves per SIMD)
+// The body is shared; each MODE is its own kernel symbol (k_scan_sample / k_scan_filter / k_scan_collect,
+// below), so profiles tell the passes apart by name rather than by grid size or duration.
+template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB>
+__device__ __forceinline__ void scan_body(ScanArgs a) {
     constexpr bool FILTER = MODE != SCAN_SAMPLE;
     constexpr bool priv = MODE == SCAN_FILTER;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -822,6 +824,26 @@ __global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan(ScanArgs a) { 
     }
 }
 
+
+// (2nd launch bound: min waves per SIMD)
+template <int MT, int DT, int QB, int P, bool NT, int TPB>
+__global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan_sample(ScanArgs a) {
+    scan_body<MT, DT, QB, P, SCAN_SAMPLE, NT, TPB>(a);
+}
+template <int MT, int DT, int QB, int P, bool NT, int TPB>
+__global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan_filter(ScanArgs a) {
+    scan_body<MT, DT, QB, P, SCAN_FILTER, NT, TPB>(a);
+}
+template <int MT, int DT, int QB, int P, bool NT, int TPB>
+__global__ __launch_bounds__(TPB, TPB >= 512 ? 2 : 1) void k_scan_collect(ScanArgs a) {
+    scan_body<MT, DT, QB, P, SCAN_COLLECT, NT, TPB>(a);
+}
+template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB>
+constexpr auto scan_kernel() {
+    if constexpr (MODE == SCAN_SAMPLE) return &k_scan_sample<MT, DT, QB, P, NT, TPB>;
+    else if constexpr (MODE == SCAN_FILTER) return &k_scan_filter<MT, DT, QB, P, NT, TPB>;
+    else return &k_scan_collect<MT, DT, QB, P, NT, TPB>;
+}
 
 // ---------------------------------------------------------------- diagnostics
 // Approximate (MFMA) scores of every row for the queries in LDS, written densely

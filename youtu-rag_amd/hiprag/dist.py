@@ -48,10 +48,11 @@ def _record_views(rec, B: int, kc: int):
 
 
 class _Slot:
-    def __init__(self, torch, device, G, B, kc, pinned):
+    def __init__(self, torch, device, G, B, kc, pinned, gather: bool):
         f64 = dict(dtype=torch.float64, device=device)
         self.rec = torch.empty((_record_len(B, kc),), **f64)  # this rank's packed record
-        self.rec_all = torch.empty((G, _record_len(B, kc)), **f64) if G > 1 else None
+        # the gathered records (G > 1, or G = 1 with the collective forced); else the merge reads rec itself
+        self.rec_all = torch.empty((G, _record_len(B, kc)), **f64) if gather else None
         self.kth = torch.empty((B,), **f64)
         self.fail = torch.empty((B,), dtype=torch.int32, device=device)
         self.fail_h = torch.empty((B,), dtype=torch.int32, pin_memory=pinned)
@@ -83,7 +84,7 @@ class _Slot:
         v = self._views.get(("a", B))
         if v is None:
             L, rec = self.views(B, kc)[:2]
-            rec_all = rec.view(1, L) if G == 1 else self.rec_all.view(-1)[: G * L].view(G, L)
+            rec_all = rec.view(1, L) if self.rec_all is None else self.rec_all.view(-1)[: G * L].view(G, L)
             v = self._views[("a", B)] = (rec_all, *_record_views(rec_all, B, kc), self.kth[:B], self.fail[:B])
         return v
 
@@ -92,7 +93,10 @@ class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
     def __init__(self, index, row_offset: int, max_batch: int, kc: int | None = None, group=None,
-                 device=None, depth: int = 2, max_k: int = 16, overlap: bool = True):
+                 device=None, depth: int = 2, max_k: int = 16, overlap: bool = True, force_collective: bool = False):
+        """force_collective: run the exchange (all-gather of the packed records, broadcast of src_rank
+        batches) through the process group even at world size 1, where it is otherwise a local copy --
+        so a one-GPU box executes the RCCL branch an 8-GPU node runs (bench.py --collective)."""
         import torch
         import torch.distributed as dist
 
@@ -101,6 +105,9 @@ class ShardedSearch:
         self.row_offset = int(row_offset)
         self.group = group
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
+        if force_collective and not dist.is_initialized():
+            raise ValueError("force_collective needs an initialised process group")
+        self.collective = self.G > 1 or bool(force_collective)  # the exchange goes through the process group
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
         # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
         self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k, int(getattr(index, "dim", 0)))
@@ -108,7 +115,8 @@ class ShardedSearch:
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         pinned = self.device.type == "cuda"
         self._dev_index = self.device.index if self.device.index is not None else 0
-        self.slots = [_Slot(torch, self.device, self.G, self.max_batch, self.kc, pinned) for _ in range(max(1, depth))]
+        self.slots = [_Slot(torch, self.device, self.G, self.max_batch, self.kc, pinned, self.collective)
+                      for _ in range(max(1, depth))]
         self._next = 0
         # tail stream: select/rescore, all-gather, merge and the flag copy of each batch
         self.tail = torch.cuda.Stream(self.device) if (overlap and pinned) else None
@@ -141,7 +149,7 @@ class ShardedSearch:
                                         cand.data_ptr(), bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
 
     def _all_gather(self, out, inp):
-        if self.G == 1:
+        if not self.collective:
             out[0].copy_(inp)
         else:
             # output as the rank-concatenation along dim 0 (accepted by RCCL and gloo alike)
@@ -180,7 +188,7 @@ class ShardedSearch:
         if slot.ticket is not None:
             self.finalize(slot)
         q = q.contiguous()
-        if src_rank is not None and self.G > 1:
+        if src_rank is not None and self.collective:
             # the batch arrives on one rank: ONE broadcast (RCCL over xGMI, 4*B*dim bytes) on the scan
             # stream puts it on every rank before the scan (queries sent with a broadcast)
             qb = slot.qbuf(q.shape, q.dtype)
@@ -209,7 +217,7 @@ class ShardedSearch:
     def _exchange_and_merge(self, slot, rec, L, B, k, s_out, r_out):
         torch = self.torch
         rec_all, cand_all, bound_all, kth, fail = slot.views_all(B, self.kc, self.G)
-        if self.G > 1:  # ONE collective per batch: every rank's packed record
+        if self.collective:  # ONE collective per batch: every rank's packed record
             self._all_gather(rec_all, rec)
         self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
         if slot.event is not None:
@@ -226,10 +234,14 @@ class ShardedSearch:
         slot.ticket = None
         if slot.event is not None:
             slot.event.synchronize()
-        failed = np.nonzero(slot.fail_h[:B].numpy())[0]
+        failed = self._failed_queries(slot, B)
         if len(failed):
             self._fallback(q, k, failed, slot.kth[:B], s_out, r_out, mask_ptr)
         return s_out, r_out
+
+    def _failed_queries(self, slot, B: int):
+        """Indices of the batch's queries whose guard failed (hook: tests force the fallback)."""
+        return np.nonzero(slot.fail_h[:B].numpy())[0]
 
     def finalize_all(self):
         for i in range(len(self.slots)):

@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU search time the cpu_baseline accumulates")
     p.add_argument("--cpu-ref-rows", type=int, default=1_000_000, help="row sample of the reference-path CPU baseline")
     p.add_argument("--cpu-embed-preset", default="bge-large")
-    p.add_argument("--recall-queries", type=int, default=8, help="planted and isotropic queries of the recall checks")
+    p.add_argument("--recall-queries", type=int, default=64, help="planted and isotropic queries of the recall checks")
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
     p.add_argument("--collective", action="store_true",

@@ -110,12 +110,17 @@ int hr_index_search_finalize(hr_index* h, int64_t ticket);
  * batch's results are in host memory a host function writes an 8-byte 1 to notify_fd (an eventfd the
  * caller polls; -1: none).  hr_index_search_collect(ticket) then copies the scores / rows out (after
  * running the exact fallback for queries that need it, synchronously).  At most two batches are in
- * flight (a third submit fails with HR_E_INVALID until one is collected); adds, removes and reserve wait
- * for batches in flight first; submit never blocks on the handle: while another call holds it, it returns
+ * flight, collected in any order (a third submit returns HR_E_BUSY until one is collected); adds, removes
+ * and reserve wait for batches in flight first and run their exact fallbacks against the rows the batches
+ * were submitted against; submit never blocks on the handle: while another call holds it, it returns
  * HR_E_BUSY at once.  No row mask; 1 <= k <= HR_MAX_K; an empty index or a multi-device handle
  * returns HR_E_UNSUPPORTED (use hr_index_search). */
 int hr_index_search_submit_host(hr_index* h, const float* q, int B, int k, int notify_fd, int64_t* ticket_out);
 int hr_index_search_collect(hr_index* h, int64_t ticket, float* scores_out, int64_t* rows_out);
+/* State of a submitted batch without waiting: *state_out = 0 still running, 1 results ready, 2 ready but some
+ * queries need the exact fallback (collect then runs a corpus pass: call it off the event loop).  HR_E_BUSY
+ * while another call holds the handle. */
+int hr_index_search_poll(hr_index* h, int64_t ticket, int* state_out);
 /* Diagnostics of the pipelined search: out[0] = caller host time per submit (us), out[1] = host time
  * per batch of the busiest shard thread (us), out[2] = batches submitted. */
 int hr_index_host_us(hr_index* h, double* out);

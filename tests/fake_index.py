@@ -79,6 +79,8 @@ class AsyncOracleIndex(OracleIndex):
     def __init__(self, *a, delay=0.002, **kw):
         super().__init__(*a, **kw)
         self.delay, self.tickets, self.next_ticket, self.busy = delay, {}, 1, False
+        self.needs_fallback: set = set()  # tickets whose collect would run the exact fallback (poll -> 2)
+        self.collected: list = []
         self.devices = [0]
 
     def search_submit_host(self, q, k, notify_fd=-1):
@@ -87,10 +89,8 @@ class AsyncOracleIndex(OracleIndex):
 
         import hiprag._native as N
 
-        if self.busy:
+        if self.busy or len(self.tickets) >= 2:  # the library: any free slot of two, else HR_E_BUSY
             raise N.BusyError(N.E_BUSY, "handle busy")
-        if len(self.tickets) >= 2:
-            raise ValueError("two batches in flight: collect one first")
         if self.live.sum() == 0:
             raise NotImplementedError("empty index")
         t = self.next_ticket
@@ -100,5 +100,16 @@ class AsyncOracleIndex(OracleIndex):
             threading.Timer(self.delay, lambda: os.eventfd_write(notify_fd, 1)).start()
         return t
 
+    def search_poll(self, ticket):
+        import hiprag._native as N
+
+        if self.busy:
+            raise N.BusyError(N.E_BUSY, "handle busy")
+        if ticket not in self.tickets:
+            raise ValueError("unknown or collected ticket")
+        return 2 if ticket in self.needs_fallback else 1
+
     def search_collect(self, ticket, B, k):
+        self.needs_fallback.discard(ticket)
+        self.collected.append(ticket)
         return self.tickets.pop(ticket)

@@ -608,6 +608,44 @@ def test_sharded_merge_large_k(native):
     np.testing.assert_array_equal(sd.cpu().numpy()[ok], s_ref[ok].astype(np.float32))
 
 
+@pytest.mark.parametrize("dim", [256, 1024])
+def test_shard_search_f32_kc256_query_groups(native, dim):
+    """fp32 rows, 128 queries, kc = HR_MAX_KC = 256 (8 row parts: more than the 128-query FILTER's 7, so the
+    FILTER is k_scan<F32, QB = 2> with two query groups), through hr_index_search_shard + the merge: ids and
+    scores identical to the oracle wherever the guard holds, and the rest through the collect path of the
+    synchronous search."""
+    torch = pytest.importorskip("torch")
+    n, B, k, kc = 30_011, 128, 128, 256
+    raw = R.gen_rows(17, 0, n, dim)
+    q = np.concatenate([_planted_queries(raw, B // 2, np.random.default_rng(dim)),
+                        np.random.default_rng(dim + 1).standard_normal((B // 2, dim)).astype(np.float32)])
+    stored = R.process_rows(raw, "cosine", "f32")
+    s_ref, r_ref = oracle.c_search(stored, "f32", R.process_queries(q, "cosine"), k)
+    idx = native.NativeIndex(dim, "f32", "cosine")
+    idx.add(raw)
+    qd = torch.from_numpy(q).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    cand = torch.empty((1, B, kc, 2), dtype=torch.float64, device="cuda")
+    bounds = torch.empty((1, B), dtype=torch.float64, device="cuda")
+    w0 = idx.wide_launches()
+    idx.search_shard(qd.data_ptr(), B, k, kc, 0, cand[0].data_ptr(), bounds[0].data_ptr(), stream=st)
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    rd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kth = torch.empty(B, dtype=torch.float64, device="cuda")
+    fail = torch.empty(B, dtype=torch.int32, device="cuda")
+    native.merge_candidates(0, cand.data_ptr(), bounds.data_ptr(), 1, B, kc, k, sd.data_ptr(), rd.data_ptr(),
+                            kth.data_ptr(), fail.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert idx.wide_launches() == w0  # 8 parts: the query groups, not the 128-query FILTER
+    ok = fail.cpu().numpy() == 0
+    assert ok.mean() > 0.5
+    np.testing.assert_array_equal(rd.cpu().numpy()[ok], r_ref[ok])
+    np.testing.assert_array_equal(sd.cpu().numpy()[ok], s_ref[ok].astype(np.float32))
+    s, r = idx.search(q, k)
+    _check(s, r, s_ref, r_ref)
+    idx.close()
+
+
 def test_pool_normalize_matches_torch(native):
     torch = pytest.importorskip("torch")
     B, T, H, n_instr = 5, 37, 768, 6
@@ -869,7 +907,11 @@ def test_query_groups_vs_oracle(native, dim, dtype, n, B, k):
         np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))
 
 
-@pytest.mark.parametrize("dim,dtype,metric", [(1024, "bf16", "cosine"), (768, "f16", "cosine"), (1024, "bf16", "ip")])
+@pytest.mark.parametrize("dim,dtype,metric", [(1024, "bf16", "cosine"), (768, "f16", "cosine"), (1024, "bf16", "ip"),
+                                              # fp32 rows form query groups where the 128-query FILTER could take
+                                              # them; a tile list (selective mask) or k = 1 then falls back to
+                                              # k_scan<F32, QB = 2> with ng > 1
+                                              (256, "f32", "cosine"), (768, "f32", "cosine"), (1024, "f32", "ip")])
 def test_query_group_edges_vs_oracle(native, dim, dtype, metric):
     """Query groups (65..256 queries per corpus pass, k <= 32, D = 768 / 1024): fewer tiles than
     workgroups, ragged ranges, a selective filter (tile list), a removed stretch, and massive ties that
@@ -1004,3 +1046,54 @@ def test_query_groups_pipelined_vs_oracle(native):
     torch.cuda.synchronize()
     for (B, k), q, (s_o, r_o) in zip(plan, qs, outs):
         _check(s_o.cpu().numpy(), r_o.cpu().numpy(), *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), k))
+
+
+def test_async_slots_out_of_order_and_fallback_before_mutation(native):
+    """hr_index_search_submit_host / _collect (the store's event-loop path), ADVICE r03:
+    (1) two batches in flight are collected in any order and a submit takes whichever slot is free (a third
+    while both are busy raises BusyError, so the store takes its worker path);
+    (2) a batch whose guard failed (100 duplicates > kc) gets its exact fallback before a remove between
+    submit and collect: the answer is the corpus the batch was submitted against, and poll reports state 2
+    (ready, needs the fallback) before collect."""
+    dim, n = 128, 6000
+    raw = R.gen_rows(21, 0, n, dim)
+    dups = np.sort(np.random.default_rng(5).choice(n, 100, replace=False))
+    raw[dups] = raw[dups[0]]
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    stored = R.process_rows(raw, "cosine", "bf16")
+    rng = np.random.default_rng(6)
+    qs = [rng.standard_normal((B, dim)).astype(np.float32) for B in (7, 19, 33)]
+    refs = [oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10) for q in qs]
+    ta = idx.search_submit_host(qs[0], 10)
+    tb = idx.search_submit_host(qs[1], 10)
+    with pytest.raises(native.BusyError):
+        idx.search_submit_host(qs[2], 10)
+    _check(*idx.search_collect(tb, 19, 10), *refs[1])
+    tc = idx.search_submit_host(qs[2], 10)  # the slot B freed, while A is outstanding
+    _check(*idx.search_collect(tc, 33, 10), *refs[2])
+    _check(*idx.search_collect(ta, 7, 10), *refs[0])
+    # (2) the fallback runs against the rows at submit
+    q = np.concatenate([raw[dups[:1]], qs[0][:3]])
+    s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10)
+    g0 = idx.stats()["guard_failures"]
+    t = idx.search_submit_host(q, 10)
+    import time
+
+    for _ in range(2000):
+        st = idx.search_poll(t)
+        if st:
+            break
+        time.sleep(0.001)
+    assert st == 2
+    idx.remove(dups[:5])  # a mutation between submit and collect
+    s, r = idx.search_collect(t, len(q), 10)
+    _check(s, r, s_ref, r_ref)
+    np.testing.assert_array_equal(r[0], dups[:10])
+    assert idx.stats()["guard_failures"] > g0
+    # and a fresh search sees the removal
+    live = np.ones(n, bool)
+    live[dups[:5]] = False
+    s2, r2 = idx.search(q, 10)
+    _check(s2, r2, *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10, oracle.mask_from_bool(live)))
+    idx.close()

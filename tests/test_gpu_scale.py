@@ -67,12 +67,17 @@ def c3(native):
 @pytest.mark.parametrize("k", [10, 100])
 def test_c3_10M_bf16_vs_oracle(c3, k):
     idx, q, s_ref, r_ref = c3
-    before = idx.stats()
-    s, r = idx.search(q, k)  # 128 queries: two 64-query corpus passes
-    after = idx.stats()
+    before, w0 = idx.stats(), idx.wide_launches()
+    # 128 queries in ONE corpus pass: at k = 10 the 128-query FILTER (hr_wide.hip, one launch); at k = 100
+    # (kc 160: 5 row parts, more than the 16-bit 128-query FILTER takes) two query groups in one k_scan launch
+    s, r = idx.search(q, k)
+    after, w1 = idx.stats(), idx.wide_launches()
     print(f"\nC3 10Mx1024 bf16 k={k}: stats {after}, this search: "
           f"guard failures {after['guard_failures'] - before['guard_failures']}, "
-          f"exhaustive {after['exhaustive'] - before['exhaustive']}")
+          f"exhaustive {after['exhaustive'] - before['exhaustive']}, 128-query FILTER launches {w1 - w0}")
+    assert w1 - w0 == (1 if k == 10 else 0)
+    # one main pass (stats' main_passes counts FILTER passes; a collect fallback is not one)
+    assert after["main_passes"] - before["main_passes"] == 1
     _check(s[:64], r[:64], s_ref[:64, :k], r_ref[:64, :k])    # planted
     _check(s[64:], r[64:], s_ref[64:, :k], r_ref[64:, :k])    # isotropic
 
@@ -161,6 +166,42 @@ def test_c3_tombstones_and_filter_vs_oracle(c3):
             _check(s, r, s_ref, r_ref)
     finally:
         print(f"\nC3 filtered: stats {idx.stats()}")
+
+
+# ---------------------------------------------------------------- C3 on the store's default dtype: fp32 rows
+@pytest.fixture(scope="module")
+def c3_f32(native):
+    idx = native.NativeIndex(D3, "f32", "cosine")
+    idx.reserve(N3)
+    idx.add_synthetic(SEED3, 0, N3)
+    planted, iso = _queries(SEED3, N3, D3, 64, qseed=5151)
+    q = np.concatenate([planted, iso])
+    s_ref, r_ref = oracle.c_search_synthetic(SEED3, 0, N3, D3, "f32", "cosine", R.process_queries(q, "cosine"), 100)
+    yield idx, q, s_ref, r_ref
+    idx.close()
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_c3_10M_f32_vs_oracle(c3_f32, k):
+    """The drop-in store's default dtype (fp32 rows, the reference's: faiss_store.py:98, :148-154; Chroma
+    float32) at the headline size, 40.96 GB: fp32 rows reach the MFMA as f16 and rely on the exactness guard,
+    whose window is widest here (isotropic queries over 10M rows).  B = 64 runs k_scan; B = 128 the fp32
+    128-query FILTER (asserted through hr_index_wide_launches, row parts at k = 100).  Identical to the oracle's
+    exact fp32 answer; the guard counters are printed."""
+    idx, q, s_ref, r_ref = c3_f32
+    for B in (64, 128):
+        before, w0 = idx.stats(), idx.wide_launches()
+        if B == 64:
+            outs = [idx.search(q[:64], k), idx.search(q[64:], k)]
+            s, r = np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs])
+        else:
+            s, r = idx.search(q, k)
+        after, w1 = idx.stats(), idx.wide_launches()
+        print(f"\nC3 10Mx1024 f32 k={k} B={B}: 128-query FILTER launches {w1 - w0}, guard failures "
+              f"{after['guard_failures'] - before['guard_failures']}, exhaustive {after['exhaustive'] - before['exhaustive']}")
+        assert (w1 - w0 > 0) == (B == 128)
+        _check(s[:64], r[:64], s_ref[:64, :k], r_ref[:64, :k])    # planted
+        _check(s[64:], r[64:], s_ref[64:, :k], r_ref[64:, :k])    # isotropic
 
 
 # ---------------------------------------------------------------- C2: 1M x 768, f32 and bf16

@@ -360,3 +360,83 @@ def test_native_async_busy_handle_and_clear(tmp_path):
     assert s._batcher.native_launches == 2
     assert all(r == [] for r in out)
     s.close()
+
+
+def test_native_async_fallback_collected_off_loop(tmp_path):
+    """A batch whose collect would run the exact fallback (poll state 2: a synchronous corpus pass) is collected
+    in a worker thread, never on the event loop; every answer equals the sequential search."""
+    import threading
+    import time
+
+    s, holder = make_async_store(tmp_path, max_batch=8)
+    s.add_chunks_sync(chunks("a", 300))
+    idx = holder["idx"]
+    q = np.random.default_rng(13).standard_normal((32, 16)).astype(np.float32)
+    want = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q, 4)]
+    where = {}
+    submit0, collect0 = idx.search_submit_host, idx.search_collect
+
+    def submit(qq, k, fd=-1):
+        t = submit0(qq, k, fd)
+        if t == 1:
+            idx.needs_fallback.add(t)
+        return t
+
+    def collect(t, B, k):
+        where[t] = threading.get_ident()
+        if t in idx.needs_fallback:
+            time.sleep(0.05)  # the fallback's corpus pass
+        return collect0(t, B, k)
+
+    idx.search_submit_host, idx.search_collect = submit, collect
+
+    async def main():
+        where["loop"] = threading.get_ident()
+        return await asyncio.gather(*[s.search(query_embedding=x.tolist(), top_k=4) for x in q])
+
+    out = run(main())
+    assert [[(c.id, sc) for c, sc in r] for r in out] == want
+    assert s._batcher.native_launches == 4 and not idx.tickets
+    assert where[1] != where["loop"] and where[4] == where["loop"]
+    s.close()
+
+
+def test_native_async_collect_out_of_order_then_submit(tmp_path):
+    """The ADVICE r03 sequence: A and B in flight, B collected first (A's collect moved to a worker: a mutation
+    held the store), then a third batch is submitted while A is still outstanding -- it must take the free slot,
+    not fail; A is then collected (blocking) with its own answer."""
+    s, holder = make_async_store(tmp_path, max_batch=8)
+    s.add_chunks_sync(chunks("a", 200))
+    q = np.random.default_rng(14).standard_normal((3, 4, 16)).astype(np.float32)
+    want = [[[(c.id, sc) for c, sc in r] for r in s.search_batch(q[i], 5)] for i in range(3)]
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        b = s._batcher
+        ia = s._submit_native(s._prep_search(q[0], 5, None), b, loop)
+        ib = s._submit_native(s._prep_search(q[1], 5, None), b, loop)
+        import threading
+
+        held, release = threading.Event(), threading.Event()
+
+        def mutation():  # holds the store lock from another thread (the store's lock is re-entrant)
+            with s._lock:
+                held.set()
+                release.wait(5)
+
+        th = threading.Thread(target=mutation)
+        th.start()
+        held.wait(5)
+        assert s._collect_native(ia, blocking=False) is None  # A's non-blocking collect declines
+        release.set()
+        th.join()
+        rb = s._collect_native(ib, blocking=False)
+        ic = s._submit_native(s._prep_search(q[2], 5, None), b, loop)
+        assert ic is not None  # the freed slot, while A is outstanding
+        ra = await asyncio.to_thread(s._collect_native, ia, True)
+        rc = s._collect_native(ic, blocking=True)
+        return [s._assemble(s._prep_search(q[i], 5, None), r) for i, r in enumerate((ra, rb, rc))]
+
+    out = run(main())
+    assert [[[(c.id, sc) for c, sc in r] for r in o] for o in out] == want
+    s.close()

@@ -344,44 +344,36 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     if (scan_lds_bytes(h, QB) > 160 * 1024)
         return set_err(HR_E_UNSUPPORTED, "dim too large for the LDS-resident query tile (max 2560)");
     p->QB = QB;
-    // More than 64 queries: up to HIPRAG_MAX_GROUPS (default 4) groups of 64 share one corpus pass --
-    // each group's workgroups stream the same tiles on one XCD, the others reading them from L2
-    // (DESIGN.md "Query groups").  fp32 corpora (2 KiB k-steps) form groups only at the dims the 128-query FILTER
-    // takes (below); elsewhere they keep one group.
-    static const int mg_env = getenv("HIPRAG_MAX_GROUPS") ? atoi(getenv("HIPRAG_MAX_GROUPS")) : 4;
-    const int max_groups = std::max(1, std::min(8, mg_env));
+    // More than 64 queries: up to 4 groups of 64 share one corpus pass -- each group's workgroups stream the
+    // same tiles on one XCD, the others reading them from L2 (DESIGN.md "Query groups").  fp32 corpora (2 KiB
+    // k-steps) form groups only at the dims the 128-query FILTER takes (below); elsewhere they keep one group.
+    constexpr int max_groups = 4;
     // (fp32 rows form groups only where the 128-query FILTER takes them: its eight-wave form reads fp32 rows)
     p->NG = (QB == 2 && (h->dtype != F32 || wide_filter_ok(h->dtype, h->S))) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
     // D > 1280 (Youtu-Embedding's 2048 / 2304 dims) leaves LDS for one 32-query block only: a 64-query
-    // batch was two corpus passes; 32-query groups share one (HIPRAG_QB1_GROUPS=0: separate passes, A/B)
-    static const int qb1_env = getenv("HIPRAG_QB1_GROUPS") ? atoi(getenv("HIPRAG_QB1_GROUPS")) : 1;
-    if (QB == 1 && B > 32 && h->dtype != F32 && qb1_env) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
+    // batch was two corpus passes; 32-query groups share one (2M x 2304: 3.03 -> 1.98 ms/batch)
+    if (QB == 1 && B > 32 && h->dtype != F32) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
     // the 128-query FILTER (hr_wide.hip) serves query groups in pairs: round the group count up to even
     if (p->NG > 1 && QB == 2 && wide_filter_ok(h->dtype, h->S)) p->NG = (p->NG + 1) & ~1;
     p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
     const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
     p->P = (h->S % 16 == 0 && pmax >= 16) ? 16 : (h->S % 8 == 0 && pmax >= 8 ? 8 : 4);
-    static const int ring_env = getenv("HIPRAG_RING") ? atoi(getenv("HIPRAG_RING")) : 0;  // tuning experiments
-    if ((ring_env == 4 || ring_env == 8 || ring_env == 16) && ring_env <= pmax && h->S % ring_env == 0) p->P = ring_env;
     return HR_OK;
 }
 
 // the FILTER of this plan runs as the 128-query pass (hr_wide.hip): query groups in pairs, D a multiple of 256 up to
-// 1024, no tile list; row parts (kc > 32), euclidean scores and fp32 rows in the eight-wave form only
+// 1024, no tile list, row parts as below
 static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list) {
-    const bool eight = wide_waves() == 8;
     // Row parts: fp32 rows up to the LDS's 7 (10M x 1024, B = 128, pipelined: k = 20 / 50 / 100 at 20.0k / 19.0k /
     // 17.3k QPS vs the query groups' 16.2k / 16.0k / 15.7k); 16-bit rows up to 3 parts and one 128-query set
     // (bf16, k = 20 / 50: B = 128 31.9k / 29.6k vs 28.2k / 27.6k QPS, but B = 256 32.4k / 29.8k vs 33.0k / 32.2k,
     // and k = 100's 5 parts FILTER in 5.0 vs 4.5 ms: the appends of its slower-rising thresholds cost more than
-    // the L2 re-reads of the groups; profiles/r03_wide_parts_*).  HIPRAG_WIDE_PARTS: most parts it takes (A/B)
-    static const int parts_env = getenv("HIPRAG_WIDE_PARTS") ? atoi(getenv("HIPRAG_WIDE_PARTS")) : -1;
+    // the L2 re-reads of the groups; profiles/r03_wide_parts_*)
     const bool f32 = h->dtype == F32;
-    const int max_parts = std::max(1, std::min(parts_env >= 0 ? parts_env : (f32 ? 7 : 3), wide_max_parts(h->dtype)));
-    const bool parts_ok = eight && np <= max_parts && (f32 || pl.NG == 2 || parts_env >= 0);
-    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) &&
-           (eight || (h->metric != L2 && h->dtype != F32)) && wide_filter_ok(h->dtype, h->S);
+    const int max_parts = std::min(f32 ? 7 : 3, wide_max_parts(h->dtype));
+    const bool parts_ok = np <= max_parts && (f32 || pl.NG == 2);
+    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) && wide_filter_ok(h->dtype, h->S);
 }
 
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
@@ -426,11 +418,9 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
         sc.last_ng = ng;
         sc.last_capw = kCapW;
         h->last_scr = &sc;
-        // dynamic tail: the last dyn_frac of the units go out in runs from the counter, but only
-        // when every wave still gets a long static run (HIPRAG_DYN_PCT / HIPRAG_DYN_CHUNK: A/B)
-        static const int pct_env = getenv("HIPRAG_DYN_PCT") ? atoi(getenv("HIPRAG_DYN_PCT")) : -1;
-        static const int chunk_env = getenv("HIPRAG_DYN_CHUNK") ? atoi(getenv("HIPRAG_DYN_CHUNK")) : 0;
-        const int pct = pct_env >= 0 ? pct_env : 10;
+        // dynamic tail: the last 10 % of the units go out in 2-unit runs from the counter, but only when every
+        // wave still gets a long static run (DESIGN.md "Dynamic tail"; profiles/r03_shard1.25M_knob_sweep.log)
+        constexpr int pct = 10;
         const int64_t per_wave = a.n_units / W;
         args.dyn_start = a.n_units;
         if (pct > 0 && per_wave >= 8 && sc.dyn_q.p) {
@@ -438,7 +428,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
             const int64_t s_per = per_wave - std::max<int64_t>(2, per_wave * pct / 100);
             args.dyn_start = s_per * W;
             args.dyn_pct = pct;
-            args.dyn_chunk = std::max(2, chunk_env > 0 ? chunk_env : 2);
+            args.dyn_chunk = 2;
             args.dyn_q = sc.dyn_q.as<uint32_t>();
         }
     }
@@ -456,17 +446,15 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // the SAMPLE pass: its tiles are the same every batch (unit * stride), and the FILTER's
     // non-temporal stream does not evict them from the Infinity Cache, so after the first batch the
     // SAMPLE is served on-die instead of taking HBM time from the FILTER beside it
-    // (HIPRAG_SAMPLE_NT=1: non-temporal SAMPLE loads, for A/B)
-    static const bool sample_nt = getenv("HIPRAG_SAMPLE_NT") && atoi(getenv("HIPRAG_SAMPLE_NT")) != 0;
-    const bool dflt = pl.NG > 1 || (MODE == SCAN_SAMPLE && !sample_nt);
+    // (1.25M rows: 0.442 -> 0.437 ms/step, profiles/r02_sample_policy_ab.jsonl)
+    const bool dflt = pl.NG > 1 || MODE == SCAN_SAMPLE;
     // more than 64 queries (query groups) in a plain FILTER: the 128-query pass reads every tile once for
     // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
     if constexpr (MODE == SCAN_FILTER) {
-        if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups && !a.stamps) {
-            // waves: one candidate region per (group, wave); a wave takes a tile (8 waves) or a tile pair (4)
-            const int wpb = wide_waves();
-            const int64_t units = wpb == 8 ? a.n_units : (a.n_units + 1) / 2;
-            const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (units + wpb - 1) / wpb));
+        if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups) {
+            // waves: one candidate region per (group, wave); a wave takes one tile per round
+            constexpr int wpb = 8;
+            const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (a.n_units + wpb - 1) / wpb));
             const int64_t W = (int64_t)blocks * wpb;
             HIP_TRY(sc.pbuf.ensure((size_t)pl.NG * 64 * W * kCapW * sizeof(float2)));
             HIP_TRY(sc.pcnt.ensure((size_t)pl.NG * 64 * W * 4));
@@ -526,9 +514,7 @@ static int launch_scan(hr_index* h, Scratch& sc, int cus, const Plan& pl, const 
 // on 224 of the 256 CUs (measured: 6.85 vs 6.81 TB/s at 10M rows, 0.434 vs 0.427 ms at 1.25M),
 // so select/rescore, the RCCL all-gather and the merge of the previous batch run beside it
 static int tail_cus(const hr_index* h) {
-    static const int env = getenv("HIPRAG_TAIL_CUS") ? atoi(getenv("HIPRAG_TAIL_CUS")) : -1;
-    const int want = env >= 0 ? env : 32;
-    return std::max(0, std::min(want, h->n_cu - 8));
+    return std::max(0, std::min(32, h->n_cu - 8));
 }
 
 // error-bound constants for the approximate (MFMA) scores, see DESIGN.md "Exactness guard"
@@ -558,44 +544,35 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const bool piped = st_tail != st && mode == 0;
     if (!piped) st_tail = st;
     Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
-    static const int dbg = getenv("HIPRAG_SCAN_DEBUG") ? atoi(getenv("HIPRAG_SCAN_DEBUG")) : 0;
     const int64_t n_tiles = (h->n + 31) / 32;
-    // SAMPLE size for n units: n/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M)
-    static const int sdiv_env = getenv("HIPRAG_SAMPLE_DIV") ? atoi(getenv("HIPRAG_SAMPLE_DIV")) : 0;
-    static const int smin_env = getenv("HIPRAG_SAMPLE_MIN") ? atoi(getenv("HIPRAG_SAMPLE_MIN")) : 0;
-    // sample tiles: 2048 (or 1/128 of the shard if more).  HIPRAG_SAMPLE_FRAC=f caps it at 1/f of a small
-    // shard (>= 64 tiles): at 100k rows the fixed 2048 read 65 % of the shard again, yet capping it
-    // (which also turns on the early SAMPLE there) gained nothing -- 0.11-0.13 ms/step either way, the
-    // per-step host submission bounds such small collections -- so the default keeps 2048
-    static const int sfrac_env = getenv("HIPRAG_SAMPLE_FRAC") ? atoi(getenv("HIPRAG_SAMPLE_FRAC")) : 0;
+    // SAMPLE size for n units: n/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M).  (Capping it at a
+    // fraction of a small shard -- at 100k rows the fixed 2048 read 65 % of the shard again -- gained nothing:
+    // 0.11-0.13 ms/step either way, the per-step host submission bounds such small collections.)
     auto sample_target = [&](int64_t n) {
         // a shard sharing its GPU with other shards of a group samples 512 tiles: the co-located shards'
         // SAMPLEs add up (8 x 1.25M rows on one GPU: 3.387 / 3.308 / 3.297 ms per batch at 2048 / 1024 /
         // 512, profiles/r03_group_scan_streams.log)
-        const int64_t smin = smin_env > 0 ? smin_env : (h->shared_dev ? 512 : 2048);
-        const int64_t small = sfrac_env > 0 ? std::max<int64_t>(64, n / sfrac_env) : smin;
-        return std::max<int64_t>(std::min<int64_t>(smin, small), n / (sdiv_env > 0 ? sdiv_env : 128));
+        const int64_t smin = h->shared_dev ? 512 : 2048;
+        return std::max<int64_t>(smin, n / 128);
     };
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
     // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
     // large enough (>= 8 sample sizes, 524k rows) for the narrow SAMPLE to finish inside the previous
     // FILTER (A/B at 16: 1M x 768 0.355 vs 0.325 ms/step; at 4, 300k-row shards lose 10 %).
-    static const int early_env = getenv("HIPRAG_EARLY_SAMPLE") ? atoi(getenv("HIPRAG_EARLY_SAMPLE")) : 1;
-    static const int early_min = getenv("HIPRAG_EARLY_MIN") ? atoi(getenv("HIPRAG_EARLY_MIN")) : 8;  // A/B
+    constexpr int early_min = 8;
     // Not for a group shard sharing its GPU with other shards (dev_ids repeated): their early SAMPLEs on
     // high-priority streams then cut into each other's FILTERs -- 8 shards of 1.25M rows on one GPU
     // 4.87 ms/batch with, 3.76 without (profiles/r03_group_shared_gpu.log)
     // (not for the 128-query FILTER, which takes every CU: an early SAMPLE on the spare CUs would only start
     // when the previous FILTER ends, on 32 CUs instead of all of them)
-    // CUs the pipelined FILTER leaves to the tail stream and the early SAMPLE: tail_cus(h) for k_scan; none by
-    // default for the 128-query FILTER (HIPRAG_WIDE_TAIL_CUS), whose per-CU rate bounds it, so its SAMPLE is not
-    // early (it would only start when the previous FILTER ends, on the few spare CUs)
-    static const int wide_tail_env = getenv("HIPRAG_WIDE_TAIL_CUS") ? atoi(getenv("HIPRAG_WIDE_TAIL_CUS")) : 0;
+    // CUs the pipelined FILTER leaves to the tail stream and the early SAMPLE: tail_cus(h) for k_scan; none for the
+    // 128-query FILTER, whose per-CU rate bounds it (8 / 16 spare CUs: 3.66 / 3.65 vs 3.44 ms at B = 128,
+    // profiles/r03_wide_spare_cus_sample_ab.log), so its SAMPLE is not early
     const bool wide_likely = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, h->tl_n >= 0);
-    const int spare = wide_likely ? std::max(0, std::min(wide_tail_env, h->n_cu - 8)) : tail_cus(h);
-    const bool early = piped && q_ready && early_env && h->tl_n < 0 && !(dbg & 5) && spare > 0 &&
-                       !h->shared_dev && n_tiles >= early_min * sample_target(n_tiles);
+    const int spare = wide_likely ? 0 : tail_cus(h);
+    const bool early = piped && q_ready && h->tl_n < 0 && spare > 0 && !h->shared_dev &&
+                       n_tiles >= early_min * sample_target(n_tiles);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -604,8 +581,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             // sharing one with the scan stream would serialise the early SAMPLE behind the FILTER
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            static const int prio_env = getenv("HIPRAG_PRE_PRIO") ? atoi(getenv("HIPRAG_PRE_PRIO")) : 1;
-            HIP_TRY(hipStreamCreateWithPriority(&h->pre, hipStreamNonBlocking, prio_env ? hi : lo));
+            HIP_TRY(hipStreamCreateWithPriority(&h->pre, hipStreamNonBlocking, hi));
         }
         sp = h->pre;
     }
@@ -624,13 +600,12 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // row -- from the host-mask path (hr_index_search built h->tl), or built here for a device mask
     // (rocPRIM select on the prep stream; the count is read back, so a masked batch costs one host
     // wait for the prep stream).  A dense mask (more than half the tiles) keeps the full scan.
-    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
     const uint32_t* tl_ptr = nullptr;
     int64_t n_vis = n_tiles;
     if (h->tl_n >= 0) {
         tl_ptr = h->tl.as<uint32_t>();
         n_vis = h->tl_n;
-    } else if (h->tl_n == -1 && mask_dev && tl_env && n_tiles > 0) {  // (-2: the host already chose the full scan)
+    } else if (h->tl_n == -1 && mask_dev && n_tiles > 0) {  // (-2: the host already chose the full scan)
         HIP_TRY(sc.tl.ensure((size_t)n_tiles * 4 + 64));
         HIP_TRY(sc.tl_tmp.ensure(std::max<size_t>(64, tile_list_scratch_bytes(n_tiles))));
         uint32_t* list = sc.tl.as<uint32_t>();
@@ -651,16 +626,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // consecutive batches use different workspaces, so batch i+1's FILTER has no dependency on
     // batch i's and its workgroups take the CUs batch i's FILTER frees during its tail (measured
     // 0.482 -> 0.462 ms/step at 1.25M rows, 0.873 -> 0.835 at 2.5M, 1.625 -> 1.607 at 5M, no gain
-    // at 10M; A/B: HIPRAG_DUAL_SCAN=0 off, 2 at any size)
-    static const int dual_env = getenv("HIPRAG_DUAL_SCAN") ? atoi(getenv("HIPRAG_DUAL_SCAN")) : 1;
-    const bool dual = early && (dual_env == 2 || (dual_env == 1 && n_tiles <= 160 * 1024));
+    // at 10M)
+    const bool dual = early && n_tiles <= 160 * 1024;
     hipStream_t sf = st;  // stream of the FILTER scan
     if (dual) {
         if (!sc.scan) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            static const int prio_env = getenv("HIPRAG_SCAN_PRIO") ? atoi(getenv("HIPRAG_SCAN_PRIO")) : 1;
-            HIP_TRY(hipStreamCreateWithPriority(&sc.scan, hipStreamNonBlocking, prio_env ? hi : lo));
+            HIP_TRY(hipStreamCreateWithPriority(&sc.scan, hipStreamNonBlocking, hi));
         }
         sf = sc.scan;
     }
@@ -668,7 +641,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // workgroups' waves per SIMD (248 registers each) no tail kernel fits beside it anyway, and its per-CU rate,
     // not HBM, bounds it (10M x 1024, B = 128: 3.60 -> 3.43 ms per batch, B = 256: 7.19 -> 6.81 ms)
     const bool wide = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, tl_ptr != nullptr);
-    const int cus = piped ? h->n_cu - (wide ? std::max(0, std::min(wide_tail_env, h->n_cu - 8)) : tail_cus(h)) : h->n_cu;
+    const int cus = piped && !wide ? h->n_cu - tail_cus(h) : h->n_cu;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
     HIP_TRY(sc.qfrag.ensure((size_t)pl.NG * h->S * pl.QB * 1024));
     HIP_TRY(sc.qerr.ensure((size_t)Bp * 4 * 8));
@@ -685,7 +658,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     HIP_TRY(sc.dyn_q.ensure((size_t)std::max(4, pl.NG) * 64));
 
     const int MT = mfma_type(h);
-    float* fl = (mode == 0 && !(dbg & 1)) ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
+    float* fl = mode == 0 ? sc.floor_q.as<float>() : nullptr;  // else uploaded below
     if (MT == BF16)
         hipLaunchKernelGGL((k_prep_q<BF16>), dim3((Bp + 3) / 4), dim3(256), 0, sp, q_dev, B, Bp, h->dim, h->dpad,
                            h->S, pl.QB, h->metric, sc.q32.as<float>(), sc.qfrag.as<uint16_t>(), sc.qerr.as<double>(),
@@ -721,13 +694,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             h->floor_host[(size_t)b] = f;
         }
     }
-    // HIPRAG_SCAN_DEBUG (timing experiments only; results are wrong with bits 1/4 set):
-    // 1 = no candidate appends, 2 = no threshold refresh, 4 = no sample pass, 8 = refresh never publishes,
-    // 16 = publish with relaxed stores instead of atomicMax, 32 = the SAMPLE pass publishes nothing,
-    // 64 = FILTER appends compute their slots but store nothing
     if (!fl) {
-        if (dbg & 1)
-            for (auto& f : h->floor_host) f = INFINITY;
         HIP_TRY(hipMemcpyAsync(sc.floor_q.p, h->floor_host.data(), (size_t)Bp * 4, hipMemcpyHostToDevice, st));
     }
 
@@ -746,12 +713,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     a.cnt = sc.cnt.as<uint32_t>();
     a.buf = sc.buf.as<float2>();
     a.cap = kCap;
-    static const int refresh_env = getenv("HIPRAG_REFRESH") ? atoi(getenv("HIPRAG_REFRESH")) : 0;
-    a.publish = (dbg & 8) ? 0 : (dbg & 16) ? 2 : 1;
+    a.publish = 1;
     a.private_bufs = mode == 0 ? 1 : 0;
-    static const int wm_env = getenv("HIPRAG_WAVE_MAJOR") ? atoi(getenv("HIPRAG_WAVE_MAJOR")) : 1;
-    a.wave_major = wm_env;
-    static const int strided_env = getenv("HIPRAG_STRIDED") ? atoi(getenv("HIPRAG_STRIDED")) : 1;  // A/B: 0 = ranges
+    a.wave_major = 1;
     // round-robin units make the chip sweep the tiles in order, so with row parts (k > 32) the last part
     // would keep its SAMPLE-level group maxima until the sweep reaches it, and the threshold (min over all
     // parts) with them: 50M rows at k = 100 then appended 78k candidates per query, overflowed every
@@ -759,20 +723,15 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // deals in teams (ScanArgs::teams): team p = every np-th wave, dealing part p's tiles round-robin, so
     // every part is read from the start and each wave stays in its part; over a tile list (units are list
     // positions, not tiles) parts keep contiguous per-wave ranges, as does the SAMPLE pass.
-    // HIPRAG_PART_TEAMS=0: contiguous ranges for every row-part FILTER (A/B)
-    static const int teams_env = getenv("HIPRAG_PART_TEAMS") ? atoi(getenv("HIPRAG_PART_TEAMS")) : 1;
-    a.strided = strided_env;
-    a.teams = (teams_env && !tl_ptr) ? 1 : 0;
-    a.refresh_every = (dbg & 2) ? (1 << 30) : (refresh_env > 0 ? refresh_env : 4);
+    a.strided = 1;
+    a.teams = tl_ptr ? 0 : 1;
+    a.refresh_every = 4;
     // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
     // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->
-    // 3.05-3.07 ms (two alternating repeats on one box, tools/ab_env.sh), so big shards keep the
-    // epilogue loads.  HIPRAG_EARLY_REFRESH=0/1 forces either (A/B)
-    static const int early_refresh_env = getenv("HIPRAG_EARLY_REFRESH") ? atoi(getenv("HIPRAG_EARLY_REFRESH")) : -1;
-    a.diag_nostore = (dbg & 64) ? 1 : 0;
-    // ... and with 4+ row parts (k >= 75: a refresh then also reads the other parts' maxima), where the
+    // 3.05-3.07 ms (two alternating repeats on one box), so big shards keep the epilogue loads ...
+    // ... except with 4+ row parts (k >= 75: a refresh then also reads the other parts' maxima), where the
     // early loads pay at 10M too: k = 100 3.217 -> 3.190 ms (profiles/r03_rowpart_knobs_10M.log)
-    a.early_refresh = early_refresh_env >= 0 ? early_refresh_env : ((dual || np >= 4) ? 1 : 0);
+    a.early_refresh = (dual || np >= 4) ? 1 : 0;
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;
@@ -793,14 +752,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             ev.sampled = false;
             ev.early = early;
         }
-        if (groups && !(dbg & 4)) {
+        if (groups) {
             a.sample_stride = std::max<int64_t>(1, n_vis / s_target);
             a.n_units = (n_vis + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
-            const int pub = a.publish;
-            a.publish = (dbg & 32) ? 0 : 1;
             if (int rc = launch_scan(h, sc, early ? spare : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
-            a.publish = pub;
             ev.sampled = true;
             if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE
                 if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
@@ -821,25 +777,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         }
         h->isolate_next = dual && timed;
         if (timed) HIP_TRY(hipEventRecord(ev.e[1], sf));
-        // diagnostics: per-wave stamps of the 10th main FILTER launch, dumped to $HIPRAG_STAMPS
-        static const char* stamp_path = getenv("HIPRAG_STAMPS");
-        static int64_t stamp_launch = 0;
-        const bool stamp = stamp_path && groups && ++stamp_launch == 10;
-        if (stamp) {
-            HIP_TRY(h->stamp_buf.ensure((size_t)4 * 8 * 65536));
-            a.stamps = h->stamp_buf.as<unsigned long long>();
-        }
         if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, sf)) return rc;
-        if (stamp) {
-            a.stamps = nullptr;
-            std::vector<unsigned long long> hs((size_t)4 * sc.last_W);
-            HIP_TRY(hipStreamSynchronize(sf));
-            HIP_TRY(hipMemcpy(hs.data(), h->stamp_buf.p, hs.size() * 8, hipMemcpyDeviceToHost));
-            if (FILE* f = fopen(stamp_path, "wb")) {
-                fwrite(hs.data(), 8, hs.size(), f);
-                fclose(f);
-            }
-        }
         if (timed) {
             HIP_TRY(hipEventRecord(ev.e[3], sf));
             h->ev_pending.push_back(ev);
@@ -1175,6 +1113,7 @@ extern "C" int hr_index_search_finalize(hr_index* h, int64_t ticket) {
 }
 
 // ---- asynchronous host-query search (the drop-in store's event loop; include/hiprag.h)
+constexpr int kAsyncPresizeB = 256;  // queries the async slots are sized for at first use (the store's max_batch)
 static void notify_fd(void* p) {  // host function on the tail stream: one completion to the caller's eventfd
     const int fd = (int)(intptr_t)p;
     const uint64_t one = 1;
@@ -1184,9 +1123,36 @@ static void notify_fd(void* p) {  // host function on the tail stream: one compl
 
 // wait (host) for every asynchronous batch in flight: mutations must not run under a scan that reads the
 // rows (a growing corpus is reallocated); the results stay in pinned memory for collect
+// A batch whose guard failed for some queries gets its exact fallback HERE, before the mutation: the fallback
+// must see the corpus the batch was submitted against (rows removed in between could leave fewer than k rows
+// above its bound, rows added in between could be returned).  The slot's pinned flags are then cleared, so
+// collect copies the completed results.
+static int async_resolve_fallback(hr_index* h, hr_index::AsyncSlot& sl);
 static int async_drain(hr_index* h) {
     for (auto& sl : h->aslot)
-        if (sl.busy && sl.done) HIP_TRY(hipEventSynchronize(sl.done));
+        if (sl.busy && sl.done) {
+            HIP_TRY(hipEventSynchronize(sl.done));
+            if (int rc = async_resolve_fallback(h, sl)) return rc;
+        }
+    return HR_OK;
+}
+
+static int async_resolve_fallback(hr_index* h, hr_index::AsyncSlot& sl) {
+    const int B = sl.B, k = sl.k;
+    int32_t* fail = (int32_t*)(sl.pin + sl.off_f);
+    const double* kth = (const double*)(sl.pin + sl.off_k);
+    std::vector<int> failed;
+    for (int b = 0; b < B; ++b)
+        if (fail[b]) failed.push_back(b);
+    if (failed.empty()) return HR_OK;
+    // the exact collect fallback (rare), synchronous, into the slot's device results
+    if (int rc = search_fallback(h, sl.q.as<float>(), k, nullptr, sl.s.as<float>(), sl.r.as<int64_t>(), failed, kth,
+                                 h->stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_s, sl.s.p, (size_t)B * k * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(sl.pin + sl.off_r, sl.r.p, (size_t)B * k * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    for (int b : failed) fail[b] = 0;
     return HR_OK;
 }
 
@@ -1200,8 +1166,16 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "asynchronous host search: single-device handles");
     if (int rc = validate_search(h, B, k)) return rc;
     if (h->n_live == 0) return set_err(HR_E_UNSUPPORTED, "empty index: use hr_index_search");
-    auto& sl = h->aslot[h->anext];
-    if (sl.busy) return set_err(HR_E_INVALID, "two batches in flight: collect one first");
+    // any free slot (batches may be collected out of order: one collect can move to a worker thread while
+    // the other is collected on the loop); none free: HR_E_BUSY, so the caller takes its blocking path
+    hr_index::AsyncSlot* free_slot = nullptr;
+    for (auto& s : h->aslot)
+        if (!s.busy) {
+            free_slot = &s;
+            break;
+        }
+    if (!free_slot) return set_err(HR_E_BUSY, "two batches in flight: collect one first");
+    auto& sl = *free_slot;
     if (int rc = set_device(h)) return rc;
     if (!h->atail) HIP_TRY(hipStreamCreateWithFlags(&h->atail, hipStreamNonBlocking));
     if (!h->acopy) HIP_TRY(hipStreamCreateWithFlags(&h->acopy, hipStreamNonBlocking));
@@ -1213,8 +1187,12 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     sl.off_r = sl.off_s + up((size_t)B * k * 4);
     sl.off_f = sl.off_r + up((size_t)B * k * 8);
     sl.off_k = sl.off_f + up((size_t)B * 4);
-    const size_t need = sl.off_k + (size_t)B * 8;
-    if (need > sl.pin_bytes) {
+    // The slot's buffers are sized once, for kAsyncPresizeB queries at HR_MAX_K (or the batch, if larger): a
+    // later reallocation (hipHostFree / hipFree synchronise the device) would stall the event loop calling this
+    const int Bs = std::max(B, kAsyncPresizeB);
+    const size_t need = up((size_t)Bs * h->dim * 4) + up((size_t)Bs * HR_MAX_K * 4) + up((size_t)Bs * HR_MAX_K * 8) +
+                        up((size_t)Bs * 4) + (size_t)Bs * 8;
+    if (sl.off_k + (size_t)B * 8 > sl.pin_bytes) {
         if (sl.pin) HIP_TRY(hipHostFree(sl.pin));
         sl.pin = nullptr;
         sl.pin_bytes = 0;
@@ -1222,13 +1200,13 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
         sl.pin_bytes = need;
     }
     const int kc = hr_kc_for_k_dim(k, h->dim);
-    HIP_TRY(sl.q.ensure(qb));
-    HIP_TRY(sl.cand.ensure((size_t)B * kc * sizeof(Cand)));
-    HIP_TRY(sl.bound.ensure((size_t)B * 8));
-    HIP_TRY(sl.kth.ensure((size_t)B * 8));
-    HIP_TRY(sl.fail.ensure((size_t)B * 4));
-    HIP_TRY(sl.s.ensure((size_t)B * k * 4));
-    HIP_TRY(sl.r.ensure((size_t)B * k * 8));
+    HIP_TRY(sl.q.ensure((size_t)Bs * h->dim * 4));
+    HIP_TRY(sl.cand.ensure((size_t)Bs * std::max(kc, HR_MAX_KC) * sizeof(Cand)));
+    HIP_TRY(sl.bound.ensure((size_t)Bs * 8));
+    HIP_TRY(sl.kth.ensure((size_t)Bs * 8));
+    HIP_TRY(sl.fail.ensure((size_t)Bs * 4));
+    HIP_TRY(sl.s.ensure((size_t)Bs * HR_MAX_K * 4));
+    HIP_TRY(sl.r.ensure((size_t)Bs * HR_MAX_K * 8));
     // queries: host -> pinned -> device on a copy stream of their own, so the early query prep + SAMPLE
     // (ready by event) need not queue behind the previous batch's FILTER
     std::memcpy(sl.pin, q, qb);
@@ -1251,7 +1229,6 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     sl.B = B;
     sl.k = k;
     sl.ticket = h->aticket++;
-    h->anext ^= 1;
     *ticket_out = sl.ticket;
     return HR_OK;
 }
@@ -1271,20 +1248,28 @@ extern "C" int hr_index_search_collect(hr_index* h, int64_t ticket, float* score
     if (int rc = set_device(h)) return rc;
     HIP_TRY(hipEventSynchronize(sl.done));
     const int B = sl.B, k = sl.k;
-    const int32_t* fail = (const int32_t*)(sl.pin + sl.off_f);
-    const double* kth = (const double*)(sl.pin + sl.off_k);
-    std::vector<int> failed;
-    for (int b = 0; b < B; ++b)
-        if (fail[b]) failed.push_back(b);
-    if (!failed.empty()) {  // the exact collect fallback (rare), synchronous, into the slot's device results
-        if (int rc = search_fallback(h, sl.q.as<float>(), k, nullptr, sl.s.as<float>(), sl.r.as<int64_t>(), failed, kth,
-                                     h->stream))
-            return rc;
-        HIP_TRY(hipMemcpy(sl.pin + sl.off_s, sl.s.p, (size_t)B * k * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(sl.pin + sl.off_r, sl.r.p, (size_t)B * k * 8, hipMemcpyDeviceToHost));
-    }
+    if (int rc = async_resolve_fallback(h, sl)) return rc;
     std::memcpy(scores_out, sl.pin + sl.off_s, (size_t)B * k * 4);
     std::memcpy(rows_out, sl.pin + sl.off_r, (size_t)B * k * 8);
+    return HR_OK;
+}
+
+extern "C" int hr_index_search_poll(hr_index* h, int64_t ticket, int* state_out) {
+    if (!h || !state_out) return set_err(HR_E_INVALID, "null argument");
+    std::unique_lock<std::mutex> lk(h->mu, std::try_to_lock);
+    if (!lk.owns_lock()) return set_err(HR_E_BUSY, "handle busy");
+    hr_index::AsyncSlot* sp = nullptr;
+    for (auto& sl : h->aslot)
+        if (sl.busy && sl.ticket == ticket) sp = &sl;
+    if (!sp) return set_err(HR_E_INVALID, "unknown or collected ticket");
+    if (hipEventQuery(sp->done) != hipSuccess) {
+        *state_out = 0;
+        return HR_OK;
+    }
+    const int32_t* fail = (const int32_t*)(sp->pin + sp->off_f);
+    int any = 0;
+    for (int b = 0; b < sp->B; ++b) any |= fail[b];
+    *state_out = any ? 2 : 1;
     return HR_OK;
 }
 
@@ -1344,9 +1329,8 @@ int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_
 // filter that keeps one document's chunks reads that document's tiles, not the whole corpus.
 // mask_words: the host mask as one u32 per tile of this index.  Sets h->tl / h->tl_n (reset by the caller).
 int index_host_tile_list(hr_index* h, const uint32_t* mw, hipStream_t st) {
-    static const int tl_env = getenv("HIPRAG_TILE_LIST") ? atoi(getenv("HIPRAG_TILE_LIST")) : 1;  // A/B
     h->tl_n = -1;
-    if (!mw || !tl_env) return HR_OK;
+    if (!mw) return HR_OK;
     const int64_t n_tiles = (h->n + 31) / 32;
     const uint32_t* lw = h->live_host.data();
     // a dense mask (most tiles hold an allowed row) keeps the full scan: decided on every 64th
@@ -1750,7 +1734,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (h->pin) (void)hipHostFree(h->pin);
     for (DevBuf* b : {&h->q_in, &h->cand, &h->bound, &h->kth, &h->fail, &h->fb_cand, &h->fb_bound, &h->fb_q,
-                      &h->fb_out, &h->stage, &h->exh, &h->stamp_buf, &h->tl, &h->s_mask, &h->sync_out,
+                      &h->fb_out, &h->stage, &h->exh, &h->tl, &h->s_mask, &h->sync_out,
                       &h->ivf_coarse, &h->ivf_probe, &h->ivf_units, &h->ivf_uoff, &h->ivf_out})
         b->release();
     for (auto& sc : h->scr) sc.release_all();

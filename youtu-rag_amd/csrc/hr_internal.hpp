@@ -73,7 +73,6 @@ int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles,
 // hr_wide.hip: the 128-query FILTER (one workgroup per CU, 4 waves; pbuf / pcnt regions [2 groups][4 * cus][64])
 struct ScanArgs;
 bool wide_filter_ok(int dtype, int S);
-int wide_waves();  // 8 (one tile per wave, 512 threads) or 4 (tile pairs, 256 threads)
 int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st);
 // row parts of the eight-wave form (kc > 32): 32 groups per part, one 16 KiB key table each in LDS beside the two
 // streamed window buffers (2 x 32 KiB, or 2 x 16 KiB for fp32 rows): at most 5 (bf16 / f16) or 7 (fp32) parts,
@@ -138,7 +137,6 @@ struct hr_index {
     bool isolate_next = false;        // dual-stream mode: the next FILTER waits for a timed one
     int n_cu = 256;
     std::mutex mu;
-    DevBuf stamp_buf;  // diagnostics (HIPRAG_STAMPS)
     // tile list of the current selective-filter search (hr_index_search with a row mask that
     // leaves at most half the tiles): sorted tiles holding a live, allowed row; tl_n = -1: none
     // (a device mask builds its own), -2: the host evaluated the mask and chose the full scan
@@ -190,7 +188,6 @@ struct hr_index {
         DevBuf q, cand, bound, kth, fail, s, r;
         hipEvent_t q_ready = nullptr, done = nullptr;
     } aslot[2];
-    int anext = 0;
     int64_t aticket = 1;
     hipStream_t acopy = nullptr, atail = nullptr;
     // ---- multi-device handles (hr_index_create with n_dev > 1, hr_group.hip)

@@ -545,15 +545,12 @@ extern "C" int hr_ivf_search(hr_index* h, const float* centroids_dev, int nlist,
         hipLaunchKernelGGL(k_ivf_units, dim3(1), dim3(1024), 0, st, h->ivf_probe.as<Cand>(), bc, nprobe,
                            list_tiles_dev, h->ivf_units.as<uint32_t>(), h->ivf_uoff.as<int64_t>(), cap);
         HIP_TRY(hipGetLastError());
-        static const int bpc_env = getenv("HIPRAG_IVF_BPC") ? atoi(getenv("HIPRAG_IVF_BPC")) : 8;  // A/B timing
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * std::max(1, bpc_env),
-                                                                      (cap + 3) / 4));
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * 8, (cap + 3) / 4));
         int rc = dispatch_dt(h->dtype, [&](auto dt) -> int {
             constexpr int DT = decltype(dt)::value;
             // ring depth (chunks in flight per wave): fp32 rows 4 (8 KiB; deeper rings spill), 16-bit
-            // rows 16 where the k-steps allow it (HIPRAG_IVF_RING=4|8|16: A/B timing)
-            static const int ring_env = getenv("HIPRAG_IVF_RING") ? atoi(getenv("HIPRAG_IVF_RING")) : 16;
-            const int ring = DT == F32 ? 4 : (h->S % ring_env == 0 ? ring_env : (h->S % 8 == 0 ? 8 : 4));
+            // rows 16 where the k-steps allow it
+            const int ring = DT == F32 ? 4 : (h->S % 16 == 0 ? 16 : (h->S % 8 == 0 ? 8 : 4));
             auto kern = ring == 16 ? k_ivf_scan<DT, 16> : ring == 8 ? k_ivf_scan<DT, 8> : k_ivf_scan<DT, 4>;
             const size_t qbytes = (size_t)4 * dpad * sizeof(float);  // one query per wave
             static bool scan_attr[64][3] = {};

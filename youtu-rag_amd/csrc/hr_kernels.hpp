@@ -270,13 +270,10 @@ struct ScanArgs {
     uint32_t* dyn_q;
     // euclidean: approximate score 2 q̂.x - |x|^2 (fp32 |x|^2 per row); nullptr for cosine / ip
     const float* xnorm;
-    // diagnostics (HIPRAG_STAMPS): per-wave wall-clock stamps {entry, staged, end, tiles}, nullable
-    unsigned long long* stamps;
     // query groups (more than QB*32 queries per corpus pass): ng workgroups stream the same tile range,
     // each with its own QB*32 queries in LDS; per-query tables hold ng consecutive groups
     int ng;
-    int diag_nostore;        // timing diagnostics only (HIPRAG_SCAN_DEBUG & 64): appends skip their stores (wrong results)
-    int early_refresh;       // FILTER: a refresh's loads go out before the tile's k-loop (0: in its epilogue; A/B)
+    int early_refresh;       // FILTER: a refresh's loads go out before the tile's k-loop (0: in its epilogue)
     // FILTER with row parts (np > 1) and round-robin dealing: the waves form np teams, team p (waves with
     // wr % np == p) deals part p's tiles round-robin among its members with a dynamic tail of its own
     // (counter dyn_q[p]) -- every wave stays in one part, every part is read from the start, and the chip
@@ -470,7 +467,6 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
         const int64_t i = wave_uniform(t_off + u * stride);
         return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };
-    const unsigned long long t_entry = a.stamps ? wall_clock64() : 0ull;
 
     // first loads of the corpus stream go out before the query staging, so their HBM latency
     // overlaps it
@@ -485,7 +481,6 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
     // thread (a load->store loop pays one L2 round trip per 8 KiB)
     stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
     __syncthreads();
-    const unsigned long long t_staged = a.stamps ? wall_clock64() : 0ull;
 
     if (u0 >= u1 && FILTER) {
         if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = 0;
@@ -540,11 +535,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
             for (int i = 0; i < 16; ++i) {
                 key[qb][i] = key[qb][i] > HR_KEY_NEG_INF ? key[qb][i] : HR_KEY_NEG_INF;
                 if (publish && a.publish && gmax[qb][i] > key2f(key[qb][i])) {
-                    if (a.publish == 2)
-                        __hip_atomic_store(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    else
-                        atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
+                    atomicMax(gkq[qb] + 32 * ((i & 3) + 8 * (i >> 2)), f2key(gmax[qb][i]));
                     key[qb][i] = f2key(gmax[qb][i]);
                 }
             }
@@ -739,7 +730,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
                                 const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)mycnt, q);
                                 if (pass && half == h) {
                                     const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                                    if (pos < (uint32_t)a.capw && !a.diag_nostore)
+                                    if (pos < (uint32_t)a.capw)
                                         wave_buf[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
                                 }
                                 mycnt += (lane == q) ? (uint32_t)__builtin_popcount(mh) : 0u;
@@ -778,13 +769,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
     }
 
     if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = mycnt;
-    if (a.stamps && lane == 0) {
-        a.stamps[4 * wg] = t_entry;
-        a.stamps[4 * wg + 1] = t_staged;
-        a.stamps[4 * wg + 2] = wall_clock64();
-        a.stamps[4 * wg + 3] = (unsigned long long)done;
-    }
-    if (!FILTER && a.publish) {  // (publish == 0: timing experiments only)
+    if (!FILTER && a.publish) {
         // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope
         // atomics from 8 XCDs), where same-address atomics serialise, so the workgroup's 8 waves
         // first reduce in LDS (the query tile is no longer needed): one atomic per address per

@@ -4,47 +4,31 @@
 // 65-128 queries used to be two groups of workgroups streaming the same tiles, the second reading them from L2
 // (query groups): bounded by that access shape at 4.4-4.6 ms per 10M x 1024 batch, 1.13x the HBM
 // bytes.  Here ONE workgroup serves 128 queries and every tile is read from HBM once:
-//  * 4 waves (one per SIMD, up to 512 registers each); a wave scores two consecutive tiles at a time
-//    (a tile pair), so every query fragment read from LDS feeds two MFMAs;
+//  * 8 waves (two per SIMD), one tile per wave per round; each wave scores its tile against all 128 queries
+//    (4 MFMA blocks of 32 queries, 64 accumulators);
 //  * the queries' fragments do not fit in LDS (256 KiB at D = 1024), so they stream through it in depth
-//    windows of 8 k-steps (2 groups x 8 k-steps x 2 blocks x 1 KiB = 32 KiB, double-buffered) that the four
+//    windows of 8 k-steps (2 groups x 8 k-steps x 2 blocks x 1 KiB = 32 KiB, double-buffered) that the eight
 //    waves walk in lock step -- one barrier per window; each window is staged by LDS-DMA
-//    (buffer_load ... lds: L2 -> LDS with no registers and no ds_write) one window ahead;
-//  * the corpus streams through a 32-deep register ring (two halves of 2 tiles x 8 k-steps, non-temporal
-//    buffer loads, one V# per tile pair);
+//    (buffer_load ... lds: L2 -> LDS with no registers and no ds_write) one window ahead, and the first
+//    windows of every tile stay resident in LDS for the whole launch;
+//  * the corpus streams through a 16-deep register ring (two halves of 8 k-steps, non-temporal buffer loads,
+//    one V# per tile);
 //  * per-query thresholds live in LDS, and so do the group maxima: one table per workgroup raised with ds_max,
 //    only by scores at or above their query's threshold (nothing below the minimum over the groups can raise
-//    it, so these updates are as rare as the appends); at a refresh (every 2 pairs) wave w swaps query block
-//    w's maxima out, publishes them (atomicMax only where they beat the global key) and recomputes its 32
-//    thresholds.  The final keys may then sit below a group's true maximum, which only lowers k_select's
-//    threshold: the candidates still hold every row at or above the scan's highest threshold, and 32 of them
-//    (one per group) lie at or above it, so the kc-th best candidate bounds every dropped row;
+//    it, so these updates are as rare as the appends); at a refresh the waves swap their share of the table
+//    out, publish it (atomicMax only where it beats the global key) and recompute the thresholds.  The final
+//    keys may then sit below a group's true maximum, which only lowers k_select's threshold: the candidates
+//    still hold every row at or above the scan's highest threshold, and 32 of them (one per group) lie at or
+//    above it, so the kc-th best candidate bounds every dropped row;
 //  * candidates go to k_scan's private per-(group, wave) regions, so k_select reads them unchanged.
-// Timing prototype and its measurements: tools/q128_proto.hip (10M x 1024 bf16, 128 queries: 3.01 ms on 224
-// CUs against 2.92 ms with the staging switched off, 3.37 ms with one tile per wave, 3.77 ms with register
-// staging).
-// Scope: bf16 / f16 / fp32 corpora (fp32: the eight-wave form), D a multiple of 256 up to 1024 (S = 16, 32, 48, 64
-// k-steps), one row part (kc <= 32), cosine / inner product (and euclidean: the eight-wave form), no tile list --
-// every other FILTER keeps k_scan's query groups.
+// Timing prototype and its measurements: tools/q128_proto.hip.  (A four-wave tile-pair form was built in round 3
+// and measured slower, 4.0-4.2 vs 3.58 ms per 10M x 1024 pass: its epilogue ran on the only wave of its SIMD.)
+// Scope: bf16 / f16 / fp32 corpora, D a multiple of 256 up to 1024 (S = 16, 32, 48, 64 k-steps), row parts up to
+// wide_max_parts, cosine / inner product / euclidean, no tile list -- every other FILTER keeps k_scan's query groups.
 #include "hr_internal.hpp"
 #include "hr_kernels.hpp"
 
-// A/B timing builds only (0 = wrong results): HR_WIDE_APPEND (candidate appends), HR_WIDE_REFRESH (threshold refresh)
-#ifndef HR_WIDE_APPEND
-#define HR_WIDE_APPEND 1
-#endif
-#ifndef HR_WIDE_STAGGER
-#define HR_WIDE_STAGGER 1
-#endif
-#ifndef HR_WIDE_REFRESH
-#define HR_WIDE_REFRESH 1
-#endif
-#ifndef HR_WIDE_GMAX  // timing experiments only (0: no group maxima; wrong thresholds)
-#define HR_WIDE_GMAX 1
-#endif
 namespace hr {
-
-int wide_waves();
 
 namespace {
 
@@ -75,281 +59,13 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
                       __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
 }
 constexpr int kWN = 8;       // k-steps per query window
-constexpr int kRefreshPairs = 2;  // tile pairs between threshold refreshes (k_scan: every 4 tiles)
 // eight-wave form: depth windows kept resident in LDS for the whole launch (the rest stream): 2 x 32 KiB
 constexpr int kResidentWindows = 2;
 
-template <int MT, int DT, int S_>
-__global__ __launch_bounds__(256, 1) void k_filter_wide(ScanArgs a) {
-    static_assert(DT != F32, "1 KiB k-step chunks (bf16 / f16 corpora)");
-    static_assert(S_ % (2 * kWN) == 0, "an even number of windows per tile (the ring halves alternate by window)");
-    constexpr int NW = S_ / kWN;           // windows per tile
-    constexpr int WQ = kWN * 4 * 64;       // u32x4 per window buffer: [group][k-step][block][lane]
-    constexpr int PER = WQ / 256;          // LDS-DMA chunks per thread per window
-    __shared__ __attribute__((aligned(16))) u32x4 lb0[WQ];
-    __shared__ __attribute__((aligned(16))) u32x4 lb1[WQ];
-    __shared__ __attribute__((aligned(16))) float th_lds[128];
-    // the workgroup's group maxima since the last refresh, as keys (f2key: ordered like the scores):
-    // G[block][register][lane], raised with ds_max_u32 by every wave, swapped out by the block's owner at a refresh
-    __shared__ __attribute__((aligned(16))) uint32_t G[4][16][64];
-    // per-wave scratch of a tile's 64 score registers for the append loop: dump[wave][register][lane]
-    __shared__ __attribute__((aligned(16))) float dump[4][64][64];
-
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
-    const int64_t W = (int64_t)gridDim.x * 4;
-    const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;  // wave-major: a round's pairs spread over the CUs
-    const int64_t n_tiles = a.n_units;
-    const int64_t n_pairs = (n_tiles + 1) / 2;
-    const int64_t rounds = (n_pairs + W - 1) / W;  // the same for every wave: the waves of a workgroup stay in step
-    const int64_t full_rounds = n_pairs / W;
-    // pair of round u for this wave (-1: none -- the wave still walks the windows with the others, on a V# of
-    // zero records that reads zeros); full rounds are rotated by a hash of u as in k_scan (periodic clusters
-    // must not land in the same waves)
-    auto pair_at = [&](int64_t u) -> int64_t {
-        int64_t pos = wr;
-        if (HR_ROTATE_ROUNDS && u < full_rounds) {
-            pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
-            if (pos >= W) pos -= W;
-        }
-        const int64_t p = u * W + pos;
-        return wave_uniform(p < n_pairs ? p : -1);
-    };
-    auto rsrc = [&](int64_t p) {
-        const int64_t t0 = p < 0 ? 0 : 2 * p;
-        const int nt = p < 0 ? 0 : (int)std::min<int64_t>(2, n_tiles - t0);
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + t0 * (S_ * 1024)), (short)0, nt * S_ * 1024, 0x00020000);
-    };
-    const int voff = lane * 16;
-    auto ld = [&](__amdgpu_buffer_rsrc_t r, int chunk) -> u32x4 {
-        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, chunk * 1024, 2);  // non-temporal
-    };
-    // query fragments [group][S][2][64] (k_prep_q's layout, two groups); window w of group gq is one contiguous
-    // 16 KiB block.  Wave wv's j-th DMA moves the 1 KiB at buffer position j * 256 + wv * 64 (u32x4)
-    const __amdgpu_buffer_rsrc_t qr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 2 * S_ * 2 * 1024, 0x00020000);
-    auto stage = [&](int w, u32x4* buf) {
-        int vo = tid * 16;
-        asm volatile("" : "+v"(vo));  // (per call: keeps the offsets out of loop-invariant registers)
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int gq = j / (PER / 2), jj = j % (PER / 2);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 256 + wv * 64),
-                                                     16, vo, gq * S_ * 2048 + w * kWN * 2048 + jj * 4096, 0, 0);
-        }
-    };
-    // ring slot i of a half: tile (i >> 3) of the pair, k-step (i & 7) of the window
-    u32x4 ra[2 * kWN], rb[2 * kWN];
-    {
-        const auto r0 = rsrc(pair_at(0));
-#pragma unroll
-        for (int i = 0; i < 2 * kWN; ++i) ra[i] = ld(r0, (i >> 3) * S_ + (i & 7));
-#pragma unroll
-        for (int i = 0; i < 2 * kWN; ++i) rb[i] = ld(r0, (i >> 3) * S_ + kWN + (i & 7));
-    }
-    stage(0, lb0);
-
-    // this wave's query block for refreshes: block wv = group wv >> 1, queries (wv & 1) * 32 .. + 32 of it
-    uint32_t* const keys_w = a.mkeys + (wv * 32 + 4 * half) * 32 + g;  // + 32 * ((i & 3) + 8 (i >> 2))
-    auto qoff_i = [](int i) { return 32 * ((i & 3) + 8 * (i >> 2)); };
-    auto publish_refresh = [&](const float (&m)[16], const uint32_t (&key)[16], bool publish) {
-        float th16[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            uint32_t k = key[i] > HR_KEY_NEG_INF ? key[i] : HR_KEY_NEG_INF;
-            if (publish && a.publish && m[i] > key2f(k)) {
-                atomicMax(keys_w + qoff_i(i), f2key(m[i]));
-                k = f2key(m[i]);
-            }
-            float f = key2f(k);
-            f = half_min32(f);
-            th16[i] = f;
-        }
-        if (g == 0) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int q = wv * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
-                th_lds[q] = fmaxf(th_lds[q], fmaxf(th16[i], a.floor_q[q]));
-            }
-        }
-    };
-    // first thresholds (the SAMPLE's group maxima and the floors)
-    if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) th_lds[wv * 32 + i] = -__builtin_inff();
-    }
-    {
-        uint32_t key[16];
-        float m[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            key[i] = __hip_atomic_load(keys_w + qoff_i(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            m[i] = -__builtin_inff();
-        }
-        publish_refresh(m, key, false);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) G[wv][i][lane] = HR_KEY_NEG_INF;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    uint32_t mycnt[2] = {0u, 0u};  // lane q: candidates of query q of group 0 / 1 in this wave's regions
-    float2* const reg0 = a.pbuf + (wr * 64) * a.capw;        // region (group 0, wave wr)
-    float2* const reg1 = a.pbuf + ((W + wr) * 64) * a.capw;  // region (group 1, wave wr)
-
-    // the live / mask words of a pair (scalar loads), fetched one pair ahead: a scalar load still in flight at
-    // a window barrier would hold it (the barrier's lgkmcnt(0) waits for scalar loads too)
-    auto allow_words = [&](int64_t p, uint32_t& w0, uint32_t& w1) {
-        w0 = w1 = 0;
-        if (p < 0) return;
-        const int64_t t = 2 * p;
-        w0 = scalar_word(a.live, t);
-        if (a.mask) w0 &= scalar_word(a.mask, t);
-        if (t + 1 < n_tiles) {
-            w1 = scalar_word(a.live, t + 1);
-            if (a.mask) w1 &= scalar_word(a.mask, t + 1);
-        }
-    };
-    uint32_t next0, next1;
-    allow_words(pair_at(0), next0, next1);
-    for (int64_t u = 0; u < rounds; ++u) {
-        const int64_t p = pair_at(u), pn = pair_at(u + 1);
-        const auto rt = rsrc(p), rn = rsrc(pn);
-        const int64_t t0 = p < 0 ? 0 : 2 * p;
-        const uint32_t allow0 = next0, allow1 = next1;
-        allow_words(pn, next0, next1);
-        const bool refresh = HR_WIDE_REFRESH && u > 0 && (u % kRefreshPairs) == 0;  // workgroup-uniform
-        f32x16 acc[2][4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int qb = 0; qb < 4; ++qb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[h][qb][i] = 0.0f;
-        uint32_t key[16];
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            u32x4(&ring)[2 * kWN] = (w & 1) ? rb : ra;
-            if (w > 0 || u > 0) {
-                // window w's fragments are in LDS: this wave's DMA landed (every VMEM op issued after it -- the
-                // previous window's 16 ring refills at least -- may still be in flight), every wave's (barrier);
-                // every wave is also through the other buffer
-                asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-            stage((w + 1) % NW, (w & 1) ? lb0 : lb1);
-            if (refresh && w == NW - 1) {  // the global keys, applied after the epilogue: issued before this
-                // window's ring refills, they are in by the time the next window's barrier wait would be anyway
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    key[i] = __hip_atomic_load(keys_w + qoff_i(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            unsigned qo = (unsigned)lane;
-            asm volatile("" : "+v"(qo));  // (per window: fragment offsets fold into the ds_read immediates)
-            const u32x4* qs = ((w & 1) ? lb1 : lb0) + qo;
-            // fragment (k-step i, block qb) at [qb >> 1][i][qb & 1]; one k-step ahead of its MFMAs
-            auto qfrag = [&](int i, int qb) { return qs[((qb >> 1) * kWN * 2 + i * 2 + (qb & 1)) * 64]; };
-            u32x4 qf[2][4];
-#pragma unroll
-            for (int qb = 0; qb < 4; ++qb) qf[0][qb] = qfrag(0, qb);
-#pragma unroll
-            for (int i = 0; i < kWN; ++i) {
-                if (i + 1 < kWN) {
-#pragma unroll
-                    for (int qb = 0; qb < 4; ++qb) qf[(i + 1) & 1][qb] = qfrag(i + 1, qb);
-                }
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const u32x4 x = ring[h * kWN + i];
-                    ring[h * kWN + i] = (w + 2 < NW) ? ld(rt, h * S_ + (w + 2) * kWN + i) : ld(rn, h * S_ + (w + 2 - NW) * kWN + i);
-#pragma unroll
-                    for (int qb = 0; qb < 4; ++qb) acc[h][qb] = mfma32<MT>(qf[i & 1][qb], x, acc[h][qb]);
-                }
-                __builtin_amdgcn_sched_barrier(0);  // (keeps the next k-step's fragment reads ahead of these MFMAs)
-            }
-        }
-
-        // epilogue.  Fast test first: does any allowed row of either tile reach its query's threshold?
-        // acc - th >= 0 exactly when acc >= th (a flushed denormal difference can only add a false positive,
-        // which the exact compares below then reject; th = -inf gives +inf, a padded query's th = +inf gives
-        // -inf).  After the first rounds almost no tile does, and the pair costs 2 subtractions + 2 maxima per
-        // register.  (The full per-register compare and ballot of both tiles cost ~25 instructions per
-        // register on the one wave of its SIMD.)
-        const int rg0 = slot_row(t0, g), rg1 = slot_row(t0 + 1, g);
-        const bool ok0 = (allow0 >> rg0) & 1u, ok1 = (allow1 >> rg1) & 1u;
-        float d0 = -__builtin_inff(), d1 = -__builtin_inff();
-#pragma unroll
-        for (int qb = 0; qb < 4; ++qb) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const f32x4 t4 = *(const f32x4*)&th_lds[qb * 32 + 8 * r + 4 * half];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    d0 = fmaxf(d0, acc[0][qb][4 * r + c] - t4[c]);
-                    d1 = fmaxf(d1, acc[1][qb][4 * r + c] - t4[c]);
-                }
-            }
-        }
-        const bool hit0 = ok0 && d0 >= 0.0f, hit1 = ok1 && d1 >= 0.0f;
-        // Slow path, per tile with a hit: its 64 score registers (-inf where the row is not allowed) go to this
-        // wave's LDS scratch, and a compact loop over the registers does the exact compares, raises the group
-        // maxima (only scores at or above their query's threshold can raise it: the threshold is the minimum
-        // over the groups) and appends to the private regions
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!__ballot(h ? hit1 : hit0)) continue;
-            const bool ok = h ? ok1 : ok0;
-            const uint32_t row = (uint32_t)((t0 + h) * 32 + (h ? rg1 : rg0));
-#pragma unroll
-            for (int qb = 0; qb < 4; ++qb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) dump[wv][qb * 16 + i][lane] = ok ? acc[h][qb][i] : -__builtin_inff();
-            for (int b = 0; b < 64; ++b) {  // (not unrolled: rare, keep the loop body small)
-                const int qb = b >> 4, i = b & 15;
-                const float v = dump[wv][b][lane];
-                const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
-                // (a masked row holds -inf: it must not pass a threshold that is still -inf)
-                const bool pass = v > -__builtin_inff() && v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
-                const uint64_t msk = __ballot(pass);
-                if (!msk) continue;
-                if (HR_WIDE_GMAX && pass) atomicMax(&G[qb][i][lane], f2key(v));
-                if (!HR_WIDE_APPEND) continue;
-                const int gq = qb >> 1;
-                uint32_t cnt = gq ? mycnt[1] : mycnt[0];
-                float2* const reg = gq ? reg1 : reg0;
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const uint32_t mh = (uint32_t)(msk >> (32 * hh));
-                    if (!mh) continue;
-                    const int ql = ql0 + 4 * hh;
-                    const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
-                    if (pass && half == hh) {
-                        const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                        if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
-                    }
-                    cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
-                }
-                if (gq) mycnt[1] = cnt;
-                else mycnt[0] = cnt;
-            }
-        }
-        if (refresh) {  // block wv's maxima since the last refresh, swapped out of G (nothing raised meanwhile is lost)
-            float m[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                m[i] = key2f(__hip_atomic_exchange(&G[wv][i][lane], (uint32_t)HR_KEY_NEG_INF, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
-            publish_refresh(m, key, true);
-        }
-    }
-    a.pcnt[wr * 64 + lane] = mycnt[0];
-    a.pcnt[(W + wr) * 64 + lane] = mycnt[1];
-}
-
-// The eight-wave form: two waves per SIMD, one tile per wave per round.  Staging per tile is the same as the
-// four-wave pair form (each staged window serves eight tiles per workgroup), the registers per wave half, and a
+// Two waves per SIMD, one tile per wave per round: each staged window serves the workgroup's eight tiles, and a
 // wave's epilogue runs beside the other wave's MFMAs on its SIMD -- with 128 queries per tile a third of the tiles
-// hold a candidate (10M rows, k = 10), so the epilogue is no longer rare.  Group maxima, thresholds, refreshes
-// and appends as in k_filter_wide; a refresh splits each query block's 16 registers between two waves.
+// hold a candidate (10M rows, k = 10), so the epilogue is not rare.  A refresh splits each query block's 16
+// registers between two waves.
 template <int MT, int DT, int S_, bool PARTS = false>
 __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     // fp32 rows: 2 KiB k-step chunks (two 16-byte loads per lane, rounded to the MFMA type on use, as k_scan's
@@ -527,9 +243,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
         const auto rt = rsrc(t), rn = rsrc(tn);
         const uint32_t allow = next_allow;
         next_allow = allow_word(tn);
-        // workgroup-uniform; staggered over the workgroups (HR_WIDE_STAGGER), so each round a 1 / RT share of
-        // them publishes and reads fresh keys instead of all at once
-        const bool refresh = u > 0 && ((u + (HR_WIDE_STAGGER ? blockIdx.x : 0)) % RT) == 0;
+        // workgroup-uniform; staggered over the workgroups, so each round a 1 / RT share of them publishes and
+        // reads fresh keys instead of all at once (15-17 % fewer candidates at the same refresh rate)
+        const bool refresh = u > 0 && ((u + blockIdx.x) % RT) == 0;
         // the part whose keys the refresh prefetches (rotating; a refresh serves every part) and the part of this
         // wave's tile (its G table)
         const int pr = PARTS ? (int)((u / RT) % np) : 0;
@@ -591,7 +307,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
             }
         }
 
-        // epilogue: fast test (acc - th >= 0 exactly when acc >= th; see k_filter_wide), then, for a tile with a
+        // epilogue: fast test (acc - th >= 0 exactly when acc >= th, a flushed denormal difference only adds a
+        // false positive), then, for a tile with a
         // hit, the exact per-register compares, group maxima (ds_max, scores at or above their threshold
         // only) and appends
         const bool ok = (allow >> rg) & 1u;
@@ -643,8 +360,8 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
                 const int ql0 = (qb & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query within its group, half 0
                 const bool pass = ok && v >= th_lds[(qb >> 1) * 64 + ql0 + 4 * half];
                 const uint64_t msk = __ballot(pass);
-                if (HR_WIDE_GMAX && pass) atomicMax(&G[pt][qb][i][lane], f2key(v));
-                if (!HR_WIDE_APPEND || !msk) continue;
+                if (pass) atomicMax(&G[pt][qb][i][lane], f2key(v));
+                if (!msk) continue;
                 const int gq = qb >> 1;
                 uint32_t cnt = gq ? mycnt[1] : mycnt[0];
                 float2* const reg = gq ? reg1 : reg0;
@@ -688,29 +405,14 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
 
 template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
-    if (a.np > 1) {  // row parts: the eight-wave form only
-        hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_, true>), dim3((unsigned)cus), dim3(512), 0, st, a);
-    } else if constexpr (DT == F32) {  // (the tile-pair form is built for 1 KiB k-step chunks only)
-        hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
-    } else {
-        if (wide_waves() == 8) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((k_filter_wide<MT, DT, S_>), dim3((unsigned)cus), dim3(256), 0, st, a);
-    }
+    if (a.np > 1) hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_, true>), dim3((unsigned)cus), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((k_filter_wide8<MT, DT, S_>), dim3((unsigned)cus), dim3(512), 0, st, a);
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 
 }  // namespace
 
-// waves per workgroup of the 128-query FILTER: 8 (one tile per wave) or 4 (tile pairs); HIPRAG_WIDE_WAVES (A/B)
-int wide_waves() {
-    static const int env = getenv("HIPRAG_WIDE_WAVES") ? atoi(getenv("HIPRAG_WIDE_WAVES")) : 8;
-    return env == 4 ? 4 : 8;
-}
-
-bool wide_filter_ok(int dtype, int S) {
-    static const int env = getenv("HIPRAG_WIDE_FILTER") ? atoi(getenv("HIPRAG_WIDE_FILTER")) : 1;  // 0: query groups (A/B)
-    return env && (S == 16 || S == 32 || S == 48 || S == 64);
-}
+bool wide_filter_ok(int dtype, int S) { return S == 16 || S == 32 || S == 48 || S == 64; }
 
 int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st) {
 #define HR_WIDE_CASE(MTv, DTv, Sv) \

@@ -45,7 +45,7 @@ EXPORTS = [
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_index_wide_launches", "hr_kc_for_k_dim",
     "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
-    "hr_index_search_collect",
+    "hr_index_search_collect", "hr_index_search_poll",
 ]
 
 _lib = None
@@ -95,6 +95,7 @@ def load_library(path: str | None = None):
             "hr_index_host_us": [vp, vp],
             "hr_index_search_submit_host": [vp, vp, i32, i32, i32, vp],
             "hr_index_search_collect": [vp, i64, vp, vp],
+            "hr_index_search_poll": [vp, i64, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
@@ -293,8 +294,8 @@ class NativeIndex:
     def search_submit_host(self, q: np.ndarray, k: int, notify_fd: int = -1) -> int:
         """Asynchronous search of host queries (single-device handle, no mask): returns a ticket at once;
         when the batch's results reach host memory an 8-byte 1 is written to notify_fd (an eventfd).
-        At most two batches in flight.  Raises NotImplementedError where hr_index_search must serve
-        (empty index, multi-device handle)."""
+        At most two batches in flight, collected in any order (a third raises BusyError).  Raises
+        NotImplementedError where hr_index_search must serve (empty index, multi-device handle)."""
         q = np.ascontiguousarray(q, np.float32)
         if q.ndim != 2 or q.shape[1] != self.dim:
             raise ValueError(f"queries must be (B, {self.dim}) float32")
@@ -309,6 +310,14 @@ class NativeIndex:
         r = np.empty((B, k), np.int64)
         _check(self.lib.hr_index_search_collect(self._h, int(ticket), _ptr(s), _ptr(r)))
         return s, r
+
+    def search_poll(self, ticket: int) -> int:
+        """State of a submitted asynchronous batch, without waiting: 0 running, 1 ready, 2 ready but its
+        collect will run the exact fallback (a corpus pass: collect it off the event loop).  Raises
+        BusyError while another call holds the handle."""
+        st = ctypes.c_int(0)
+        _check(self.lib.hr_index_search_poll(self._h, int(ticket), ctypes.byref(st)))
+        return st.value
 
     def search_finalize(self, ticket: int) -> None:
         """Wait for a submitted batch's guard flags and run its exact fallback (no-op if already final)."""

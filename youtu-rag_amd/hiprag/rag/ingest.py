@@ -146,6 +146,11 @@ class GpuIngestor:
                         pending_docs = {c.document_id for c in pending}
                 await self._store(pending)
                 self._flush()
+        except BaseException:
+            # a failed ingest commits nothing later: drop the embedded batch still in flight (the next call
+            # would otherwise store it silently, after newer data)
+            self._inflight = None
+            raise
         finally:
             if paused:
                 gc.enable()

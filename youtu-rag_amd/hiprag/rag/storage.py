@@ -722,13 +722,22 @@ class HipVectorStore(BaseVectorStore):
 
     def _collect_native(self, info, blocking: bool):
         """(raw, tables) of a finished native launch, as _run_search returns them; None when not blocking
-        and the store lock is held (the caller then collects in a worker thread)."""
+        and the store lock is held, the handle is busy or the batch needs its exact fallback (the caller then
+        collects in a worker thread)."""
         idx, ticket, B, k, tables = info
         if not self._lock.acquire(blocking=blocking):
             return None
         try:
             if idx is not self._index or tables[2] != self._epoch:  # cleared / closed since: rows are gone
                 return None, tables
+            if not blocking and hasattr(idx, "search_poll"):
+                # a batch whose collect would run the exact fallback (a synchronous corpus pass) or a handle held
+                # by another call: collect in a worker thread, never on the event loop
+                try:
+                    if idx.search_poll(ticket) != 1:
+                        return None
+                except _native.BusyError:
+                    return None
             return idx.search_collect(ticket, B, k), tables
         finally:
             self._lock.release()

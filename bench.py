@@ -60,11 +60,15 @@ def parse():
     p.add_argument("--cpu-ref-rows", type=int, default=1_000_000, help="row sample of the reference-path CPU baseline")
     p.add_argument("--cpu-embed-preset", default="bge-large")
     p.add_argument("--recall-queries", type=int, default=64, help="planted and isotropic queries of the recall checks")
-    p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline and recall (quick runs)")
+    p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline, recall and the GPU embed leg (quick runs)")
+    p.add_argument("--no-embed", action="store_true", help="skip the GPU embed+search leg")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
     p.add_argument("--collective", action="store_true",
                    help="run the exchange through an RCCL process group even at --gpus 1 (world size 1): the timed "
                         "loop then includes the all-gather an 8-GPU node runs")
+    p.add_argument("--persist", type=int, default=1, choices=(0, 1, 2),
+                   help="persistent FILTER for the pipelined shard batches: 0 off (one FILTER launch per batch), "
+                        "1 shards up to 5.1M rows (default), 2 every shard size")
     p.add_argument("--single-process", action="store_true",
                    help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()
@@ -188,6 +192,72 @@ def cpu_reference_baseline(args, qbatches, N, D, K, B):
     except Exception as e:  # noqa: BLE001
         out["embed"] = {"error": repr(e)}
     return out
+
+
+def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> dict:
+    """The reference's query path on the GPU, beside cpu_baseline's CPU embed+search: ``embed_query`` then
+    ``search`` (base_retriever.py:57-62; the embedding server's encode, deploying-locally.mdx:81-116) -- B query
+    strings -> TorchRocmEmbedder (the same bge-large shape as the CPU leg, bf16, unpadded packed forward + K7
+    pooling) -> the exact scan over the resident corpus (this bench's searcher), timed end to end:
+    * ``sequential``: one batch at a time, embed -> search -> synchronise (a lone caller's latency);
+    * ``pipelined``: the embedder on a stream of its own, each batch's search submitted behind its queries' event,
+      two batches in flight (the throughput a serving process gets);
+    plus the embed alone and its MFMA rate (executed FLOPs of the forwards ÷ time, against the 2.5 PF bf16 peak).
+    Random-init weights (no checkpoint offline), so the vectors are not semantically meaningful: the figure is
+    the work's cost, not retrieval quality."""
+    import torch
+
+    from hiprag.rag.rocm_embedder import TorchRocmEmbedder
+
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from flops import EncoderFlops
+
+    emb = TorchRocmEmbedder(preset=args.cpu_embed_preset, dtype="bfloat16", batch_size=B, device=dev, seed=0)
+    if emb.dim != D:
+        return {"skipped": f"embedder dim {emb.dim} != corpus dim {D}"}
+    fl = EncoderFlops(emb.model, emb.unpadded)
+    texts = [[f"what does document {i * B + j} say about topic {(i * B + j) % 7} and its retrieval setup"
+              for j in range(B)] for i in range(n_batches + 2)]
+    for t in texts[:2]:  # warm: kernels, allocator, tokenizer caches
+        searcher.search(emb.embed_queries_device(t), K)
+    torch.cuda.synchronize()
+    fl.reset()
+    t0 = time.perf_counter()
+    for t in texts[2:]:
+        emb.embed_queries_device(t)
+    torch.cuda.synchronize()
+    t_embed = (time.perf_counter() - t0) / n_batches
+    flops = fl.totals()
+    t0 = time.perf_counter()
+    for t in texts[2:]:
+        searcher.search(emb.embed_queries_device(t), K)
+        torch.cuda.synchronize()
+    t_seq = (time.perf_counter() - t0) / n_batches
+    es = torch.cuda.Stream(dev)
+    s_out = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
+    r_out = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
+    keep = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, t in enumerate(texts[2:]):
+        with torch.cuda.stream(es):
+            q = emb.embed_queries_device(t)
+            ev = torch.cuda.Event()
+            ev.record(es)
+        keep.append((q, ev))
+        torch.cuda.current_stream(dev).wait_event(ev)  # (the scan stream's own order: prep runs behind the queries)
+        searcher.submit(q, K, s_out=s_out[i], r_out=r_out[i], q_ready=ev)
+    searcher.finalize_all()
+    torch.cuda.synchronize()
+    t_pipe = (time.perf_counter() - t0) / n_batches
+    tflops = flops["executed"] / n_batches / t_embed / 1e12
+    return {"model": f"{args.cpu_embed_preset} shape (random init), bf16, unpadded forward + K7", "batch": B,
+            "batches": n_batches, "tokens_per_batch": round(flops["tokens_real"] / n_batches, 1),
+            "embed_ms_per_batch": round(1000 * t_embed, 3), "embed_tflops": round(tflops, 1),
+            "embed_frac_of_bf16_peak": round(tflops / MFMA_PEAK_TFLOPS, 4),
+            "sequential": {"ms_per_batch": round(1000 * t_seq, 3), "qps": round(B / t_seq, 1)},
+            "pipelined": {"ms_per_batch": round(1000 * t_pipe, 3), "qps": round(B / t_pipe, 1)},
+            "path": "embed_query -> search (base_retriever.py:57-62), embedding + exact scan on the GPU"}
 
 
 def isotropic_queries(B: int, D: int, seed: int = 7) -> np.ndarray:
@@ -405,6 +475,7 @@ def main():
 
     t0 = time.time()
     index = _native.NativeIndex(D, args.dtype, "cosine", device=local)
+    index.set_persist(args.persist)
     index.reserve(n_local)
     index.add_synthetic(args.seed, start, n_local)
     torch.cuda.synchronize()
@@ -437,6 +508,7 @@ def main():
     # ~6 us bubble on the scan stream, so timing every launch would slow the steps being measured
     index.set_scan_timing(TIME_EVERY)
     wide0 = index.wide_launches()
+    persist0 = index.persist_stats()["batches"]
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -450,6 +522,10 @@ def main():
     elapsed = time.perf_counter() - t_start
     sample_ms, scan_ms = index.take_scan_times()
     wide_per_step = (index.wide_launches() - wide0) / args.steps  # 128-query FILTER launches per batch
+    pst = index.persist_stats()
+    if pst["error"]:
+        raise RuntimeError(f"persistent FILTER error {pst['error']}")
+    persist = pst["batches"] - persist0 == args.steps  # every timed batch went through the persistent FILTER
     # one untimed batch of isotropic queries (the worst case for ranking: no planted neighbour), for the
     # recall checks; every rank takes part (the merge is collective)
     q_iso = isotropic_queries(B, D)
@@ -496,7 +572,10 @@ def main():
                    "parallelism": f"rowshard{G}" + ("+rccl" if searcher.collective else ""),
                    "exchange": (f"RCCL all_gather_into_tensor ({dist.get_backend()})" if searcher.collective
                                 else "none (one shard: local copy)")},
-        "roofline": {"bound": "hbm", "kernel": "k_filter_wide8 (128-query FILTER)" if wide else "k_scan (FILTER pass)",
+        "roofline": {"bound": "hbm",
+                     "kernel": ("k_filter_wide8 (128-query FILTER)" if wide else
+                                "k_scan_persist (persistent FILTER; per-batch time = period between the device stamps "
+                                "of consecutive batches' last workgroup arrivals)" if persist else "k_scan_filter (FILTER pass)"),
                      "filter_launches_per_batch": passes, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "frac_of_measured_read_ceiling": round(achieved / HBM_READ_CEILING_GBS, 4),
@@ -554,6 +633,13 @@ def main():
         result.update(recall_checks(args, N, D, K, qs[args.warmup][:nq], r_dev[args.warmup, :nq].cpu().numpy(),
                                     s_dev[args.warmup, :nq].cpu().numpy(), q_iso[:nq],
                                     r_iso[:nq].cpu().numpy(), s_iso[:nq].cpu().numpy()))
+
+    # the reference's embed + search query path on the GPU (N = 1), beside cpu_baseline's CPU embed + search
+    if rank == 0 and G == 1 and not args.no_cpu and not args.no_embed:
+        try:
+            result["gpu_embed_plus_search"] = gpu_embed_plus_search(args, searcher, dev, D, K, B)
+        except Exception as e:  # report, never hide
+            result["gpu_embed_plus_search"] = {"error": repr(e)}
 
     # CPU baselines, rank 0, N=1 only: the reference's search path on the host cores (cpu_baseline),
     # the reference's per-query loop and the CPU query embedding beside it, and the exact fp64 oracle

@@ -220,13 +220,27 @@ int hr_hash_words(const char* text, const int64_t* offsets, int64_t n_texts, int
 int hr_add_layernorm(const void* x_dev, const void* r_dev, const void* gamma_dev, const void* beta_dev, void* out_dev,
                      int64_t rows, int H, float eps, int dtype, void* stream);
 
+/* The persistent FILTER (pipelined shard batches of <= 64 queries, k <= 16, no mask, early SAMPLE: the per-GPU
+ * step of a row-sharded node).  One long-lived launch streams the corpus batch after batch -- no per-batch launch
+ * ramp and tail; replaces the per-batch FILTER launch behind hr_index_search_shard_async_ev (same results).
+ * set_persist: 0 off, 1 shards up to 5.1M rows (default), 2 every shard size.  persist_close: no further batch
+ * for now (the running instance exits once through its batches instead of after its 300 us idle timeout).
+ * persist_stats: out[0] = batches served, out[1] = error word (a bounded wait gave up; 0 = none). */
+/* Diagnostics: tiles each wave of the most recent k_scan FILTER launch scanned ([query group][wave], blocking;
+ * up to cap counts, the number in n_out).  Every unit is scanned exactly once per group, so the counts sum to
+ * groups x units -- the invariant of the round-robin dealing, its rotation and the dynamic tail. */
+int hr_index_wave_tiles(hr_index* h, uint32_t* out, int cap, int* n_out);
+int hr_index_set_persist(hr_index* h, int mode);
+int hr_index_persist_close(hr_index* h);
+int hr_index_persist_stats(hr_index* h, int64_t out[2]);
 /* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
  * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
 int hr_index_set_scan_timing(hr_index* h, int every);
 /* Timing of the main-pass scans (ms, HIP events recorded on the search stream).
  * take_scan_times harvests, in launch order, every (SAMPLE, FILTER) pair launched since the
  * previous harvest (blocking on the pending events; up to cap entries; count in n_out);
- * last_scan_ms harvests everything and reports the most recent pair. */
+ * last_scan_ms harvests everything and reports the most recent pair.  A batch of the persistent FILTER reports
+ * as its FILTER time the period between its last workgroup arrival and the previous batch's (device clock). */
 int hr_index_take_scan_times(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n_out);
 int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms);
 int hr_device_count(int* n_out);

@@ -1097,3 +1097,33 @@ def test_async_slots_out_of_order_and_fallback_before_mutation(native):
     s2, r2 = idx.search(q, 10)
     _check(s2, r2, *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10, oracle.mask_from_bool(live)))
     idx.close()
+
+
+def test_every_tile_scanned_exactly_once(native):
+    """hr_index_wave_tiles: the tiles each wave of the last k_scan FILTER scanned sum to groups x units -- the
+    round-robin dealing (rotated per round), the dynamic tail (600k rows: every wave gets >= 8 static tiles, so the
+    last 10 % go out from the counter), row-part teams, query groups and tile lists each visit every unit exactly
+    once.  (Results are checked against the oracle elsewhere; this pins the dealing itself.)"""
+    n, dim = 600_011, 256
+    n_tiles = (n + 31) // 32
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    try:
+        idx.add_synthetic(4, 0, n)
+        rng = np.random.default_rng(1)
+        for B, k, groups in ((64, 10, 1), (40, 50, 1), (256, 100, 4)):
+            q = rng.standard_normal((B, dim)).astype(np.float32)
+            w0 = idx.wide_launches()
+            idx.search(q, k)
+            assert idx.wide_launches() == w0  # (k_scan, not the 128-query FILTER)
+            wt = idx.wave_tiles()
+            assert len(wt) % groups == 0 and len(wt) >= groups * 8
+            assert int(wt.sum()) == groups * n_tiles, (B, k, int(wt.sum()), groups * n_tiles)
+        # tile list: a few documents' contiguous rows -> only their tiles
+        sel = np.zeros(n, bool)
+        for lo in (1000, 300_000, 599_000):
+            sel[lo:lo + 5000] = True
+        idx.search(rng.standard_normal((64, dim)).astype(np.float32), 10, oracle.mask_from_bool(sel))
+        listed = len(np.unique(np.nonzero(sel)[0] // 32))
+        assert int(idx.wave_tiles().sum()) == listed
+    finally:
+        idx.close()

@@ -1,0 +1,48 @@
+"""CPU: register budget of the hot scan kernels in the built libhiprag.so (gfx950 code-object metadata, read by
+tools/kernel_resources.py -- no GPU needed).
+
+The FILTER kernels run two waves per SIMD and sit at (or near) the 256-VGPR limit, where the register allocator's
+choices flip with unrelated edits: in round 4 removing a few lines of diagnostics made k_scan_filter spill 42 VGPRs
+to scratch inside its tile loop and cost 9 % at 1.25M rows.  A VGPR spill in these kernels fails here, on the CPU,
+before it reaches a GPU.  (SGPR spills go to VGPR lanes and are not scratch traffic.)
+"""
+import os
+import re
+import shutil
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "youtu-rag_amd", "hiprag", "libhiprag.so")
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB) or not shutil.which("/opt/rocm/lib/llvm/bin/llvm-readelf"),
+                                reason="libhiprag.so or the ROCm LLVM tools are missing")
+
+# kernels that must not spill VGPRs at all, and the 128-query FILTER's known spills (not to grow)
+NO_SPILL = re.compile(r"k_scan_(filter|sample|collect|persist)")
+WIDE = re.compile(r"k_filter_wide8")
+
+
+@pytest.fixture(scope="module")
+def resources():
+    from kernel_resources import kernel_resources
+
+    return kernel_resources(LIB)
+
+
+def test_scan_kernels_do_not_spill(resources):
+    hot = {k: v for k, v in resources.items() if NO_SPILL.search(k)}
+    assert len(hot) >= 40, sorted(hot)  # every instantiation was found
+    spilled = {k: v["vgpr_spill_count"] for k, v in hot.items() if v.get("vgpr_spill_count", 0)}
+    assert not spilled, spilled
+    persist = [v for k, v in hot.items() if "k_scan_persist" in k]
+    assert len(persist) == 4
+
+
+def test_wide_filter_spills_bounded(resources):
+    wide = {k: v for k, v in resources.items() if WIDE.search(k)}
+    assert len(wide) == 32, sorted(wide)
+    worst = max(v.get("vgpr_spill_count", 0) for v in wide.values())
+    assert worst <= 35, worst

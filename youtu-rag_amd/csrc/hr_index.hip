@@ -12,6 +12,39 @@ int set_err(int code, const std::string& msg) {
 
 static int async_drain(hr_index* h);
 
+// ---------------------------------------------------------------- the persistent FILTER (hr_persist.hip)
+// Host state of an index's persistent FILTER: kPersistSlots per-batch workspaces whose buffers the instance reads
+// (query fragments, group-max keys, floors, candidate regions, dynamic-tail counters) sit at a constant stride in
+// one arena per kind, so an instance finds slot s's buffers as slot 0's + s * stride; the other per-batch buffers
+// (select / rescore) are the slots' own.  Configured for one corpus state and plan; re-configured after a quiesce.
+struct Persist {
+    int mode = 1;                      // hr_index_set_persist: 0 off, 1 small shards (default), 2 every shard size
+    bool ready = false;                // configured (for the key below)
+    int64_t key_n = -1;
+    const void* key_rows = nullptr;
+    int key_S = 0, key_P = 0, key_ncu = 0;
+    Scratch slot[kPersistSlots];       // qfrag / mkeys / floor_q / pbuf / pcnt / dyn_q are views into the arenas
+    DevBuf ar_qfrag, ar_mkeys, ar_floor, ar_pbuf, ar_pcnt, ar_dynq;
+    int64_t st_qfrag = 0, st_mkeys = 0, st_floor = 0, st_pbuf = 0, st_pcnt = 0, st_dynq = 0;
+    DevBuf ctl;                        // PersistCtl
+    uint32_t* host_err = nullptr;      // pinned mirror of PersistCtl::error
+    hipStream_t pst = nullptr;         // instances (one launch per batch, gated by the batch's post event)
+    hipEvent_t posted[kPersistSlots] = {};
+    uint32_t epoch = 0;                // last epoch assigned
+    bool active = false;               // an instance may be running (launched since the last quiesce)
+    int nwg = 0;                       // workgroups of every instance (n_cu - tail CUs): fixed, the tail's targets use it
+    uint32_t idle_ticks = 30000;       // 300 us of s_memrealtime (100 MHz) without a batch: the instance exits
+    void drop_views() {
+        for (auto& sc : slot)
+            for (DevBuf* b : {&sc.qfrag, &sc.mkeys, &sc.floor_q, &sc.pbuf, &sc.pcnt, &sc.dyn_q}) {
+                b->p = nullptr;
+                b->bytes = 0;
+            }
+    }
+};
+static int persist_quiesce(hr_index* h);  // blocking: every instance has exited (mutations, destroy)
+static int persist_close(hr_index* h);    // non-blocking: the running instance exits once through its batches
+
 // ---------------------------------------------------------------- create / grow
 extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
     if (!out) return set_err(HR_E_INVALID, "out is null");
@@ -376,6 +409,22 @@ static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list)
     return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) && wide_filter_ok(h->dtype, h->S);
 }
 
+// dynamic tail of a FILTER over W waves: the last 10 % of the units go out in 2-unit runs from the counter, but
+// only when every wave still gets a long static run (DESIGN.md "Dynamic tail"; profiles/r03_shard1.25M_knob_sweep.log)
+static void set_dyn_tail(ScanArgs& args, int64_t W, uint32_t* dyn_q) {
+    constexpr int pct = 10;
+    const int64_t per_wave = args.n_units / W;
+    args.dyn_start = args.n_units;
+    if (per_wave >= 8 && dyn_q) {
+        // static runs and dynamic runs are >= 2 units (the grab is issued one unit early)
+        const int64_t s_per = per_wave - std::max<int64_t>(2, per_wave * pct / 100);
+        args.dyn_start = s_per * W;
+        args.dyn_pct = pct;
+        args.dyn_chunk = 2;
+        args.dyn_q = dyn_q;
+    }
+}
+
 template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB = kScanThreads>
 static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, hipStream_t st, int lds) {
     const int ng = std::max(1, a.ng);
@@ -410,6 +459,9 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
         const int Bq = QB * 32;
         HIP_TRY(sc.pbuf.ensure((size_t)ng * Bq * W * kCapW * sizeof(float2)));
         HIP_TRY(sc.pcnt.ensure((size_t)ng * Bq * W * 4));
+        HIP_TRY(sc.wtiles.ensure((size_t)ng * W * 4));
+        args.wave_tiles = sc.wtiles.as<uint32_t>();
+        sc.wtiles_valid = true;
         args.pbuf = sc.pbuf.as<float2>();
         args.pcnt = sc.pcnt.as<uint32_t>();
         args.capw = kCapW;
@@ -418,19 +470,7 @@ static int launch_scan_t(hr_index* h, Scratch& sc, int cus, const ScanArgs& a, h
         sc.last_ng = ng;
         sc.last_capw = kCapW;
         h->last_scr = &sc;
-        // dynamic tail: the last 10 % of the units go out in 2-unit runs from the counter, but only when every
-        // wave still gets a long static run (DESIGN.md "Dynamic tail"; profiles/r03_shard1.25M_knob_sweep.log)
-        constexpr int pct = 10;
-        const int64_t per_wave = a.n_units / W;
-        args.dyn_start = a.n_units;
-        if (pct > 0 && per_wave >= 8 && sc.dyn_q.p) {
-            // static runs and dynamic runs are >= 2 units (the grab is issued one unit early)
-            const int64_t s_per = per_wave - std::max<int64_t>(2, per_wave * pct / 100);
-            args.dyn_start = s_per * W;
-            args.dyn_pct = pct;
-            args.dyn_chunk = 2;
-            args.dyn_q = sc.dyn_q.as<uint32_t>();
-        }
+        set_dyn_tail(args, W, sc.dyn_q.as<uint32_t>());
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)(blocks * ng)), dim3(TPB), lds, st, args);
     HIP_TRY(hipGetLastError());
@@ -462,6 +502,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
             sc.last_Bp = 64;
             sc.last_ng = pl.NG;
             sc.last_capw = kCapW;
+            sc.wtiles_valid = false;
             h->last_scr = &sc;
             for (int set = 0; set < pl.NG / 2; ++set) {  // two groups per launch
                 ScanArgs b = a;
@@ -517,6 +558,128 @@ static int tail_cus(const hr_index* h) {
     return std::max(0, std::min(32, h->n_cu - 8));
 }
 
+// ---- persistent FILTER: configuration, quiesce, close
+static int persist_quiesce(hr_index* h) {
+    Persist* ps = h->ps;
+    if (!ps || !ps->active) return HR_OK;
+    if (int rc = set_device(h)) return rc;
+    PersistCtl* c = ps->ctl.as<PersistCtl>();
+    if (int rc = launch_persist_close(c, h->pre)) return rc;  // behind every post (same stream)
+    HIP_TRY(hipStreamSynchronize(h->pre));
+    HIP_TRY(hipStreamSynchronize(ps->pst));                   // every instance has exited
+    HIP_TRY(hipMemsetAsync(&c->stop, 0, 4, ps->pst));
+    HIP_TRY(hipStreamSynchronize(ps->pst));
+    ps->active = false;
+    if (ps->host_err && *(volatile uint32_t*)ps->host_err)
+        return set_err(HR_E_HIP, "persistent FILTER: a bounded wait gave up (results of the batches in flight are invalid)");
+    return HR_OK;
+}
+
+static int persist_close(hr_index* h) {
+    Persist* ps = h->ps;
+    if (!ps || !ps->active) return HR_OK;
+    if (int rc = set_device(h)) return rc;
+    if (int rc = launch_persist_close(ps->ctl.as<PersistCtl>(), h->pre)) return rc;
+    // the next batch finds the gate closed and starts an instance of its own, which reopens it (stop is cleared
+    // first, on the instances' stream, behind the running instance)
+    HIP_TRY(hipMemsetAsync(&ps->ctl.as<PersistCtl>()->stop, 0, 4, ps->pst));
+    ps->active = false;
+    return HR_OK;
+}
+
+static void persist_free(hr_index* h) {
+    Persist* ps = h->ps;
+    if (!ps) return;
+    (void)persist_quiesce(h);
+    ps->drop_views();
+    for (auto& sc : ps->slot) sc.release_all();
+    for (DevBuf* b : {&ps->ar_qfrag, &ps->ar_mkeys, &ps->ar_floor, &ps->ar_pbuf, &ps->ar_pcnt, &ps->ar_dynq, &ps->ctl})
+        b->release();
+    for (auto& e : ps->posted)
+        if (e) (void)hipEventDestroy(e);
+    if (ps->pst) (void)hipStreamDestroy(ps->pst);
+    if (ps->host_err) (void)hipHostFree(ps->host_err);
+    delete ps;
+    h->ps = nullptr;
+}
+
+// The persistent FILTER serves this pipelined batch?  Unmasked, one 64-query tile (one group, one row part: k <= 16),
+// not the 128-query FILTER, a plan it is built for, early-SAMPLE conditions met, a single-device index (not a group
+// shard), and (mode 1) a shard in the dual-FILTER range (<= 160k tiles = 5.1M rows: 1.25M rows at G = 8).
+static bool persist_wanted(hr_index* h, const Plan& pl, int np, bool early, const uint64_t* mask_dev, int64_t n_tiles) {
+    const int mode = h->ps ? h->ps->mode : 1;
+    if (mode == 0 || !early || mask_dev || np != 1 || pl.NG != 1 || pl.QB != 2 || h->stripe_G != 1) return false;
+    if (!(h->dtype != F32 ? pl.P == 16 : pl.P == 4)) return false;
+    return mode == 2 || n_tiles <= 160 * 1024;
+}
+
+// (re)configure for the current corpus and plan: arenas sized for one 64-query tile per slot
+static int persist_configure(hr_index* h, const Plan& pl) {
+    if (!h->ps) h->ps = new Persist();
+    Persist& ps = *h->ps;
+    const int64_t n_tiles = (h->n + 31) / 32;
+    const int nwg = h->n_cu - tail_cus(h);
+    if (ps.ready && ps.key_n == h->n && ps.key_rows == h->rows && ps.key_S == h->S && ps.key_P == pl.P &&
+        ps.key_ncu == h->n_cu)
+        return HR_OK;
+    if (int rc = persist_quiesce(h)) return rc;
+    if ((n_tiles + 7) / 8 < nwg) return set_err(HR_E_UNSUPPORTED, "shard too small for the persistent FILTER");
+    if (!ps.pst) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&ps.pst, hipStreamNonBlocking, hi));
+        for (auto& e : ps.posted) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc((void**)&ps.host_err, 64));
+        *ps.host_err = 0;
+        HIP_TRY(ps.ctl.ensure(sizeof(PersistCtl)));
+        PersistCtl init{};
+        init.gate = 0x80000000u;  // closed: the first batch starts an instance of its own
+        init.next_epoch = 1;
+        HIP_TRY(hipMemcpy(ps.ctl.p, &init, sizeof init, hipMemcpyHostToDevice));
+    }
+    auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    const int64_t W = (int64_t)nwg * (kScanThreads / 64);
+    ps.st_qfrag = up((int64_t)h->S * pl.QB * 1024);
+    ps.st_mkeys = up((int64_t)pl.Bp * 32 * 4);
+    ps.st_floor = up((int64_t)pl.Bp * 4);
+    ps.st_pbuf = up((int64_t)pl.Bp * W * kCapW * (int64_t)sizeof(float2));
+    ps.st_pcnt = up((int64_t)pl.Bp * W * 4);
+    ps.st_dynq = 256;
+    ps.drop_views();
+    const int R = kPersistSlots;
+    HIP_TRY(ps.ar_qfrag.ensure((size_t)(R * ps.st_qfrag)));
+    HIP_TRY(ps.ar_mkeys.ensure((size_t)(R * ps.st_mkeys)));
+    HIP_TRY(ps.ar_floor.ensure((size_t)(R * ps.st_floor)));
+    HIP_TRY(ps.ar_pbuf.ensure((size_t)(R * ps.st_pbuf)));
+    HIP_TRY(ps.ar_pcnt.ensure((size_t)(R * ps.st_pcnt)));
+    HIP_TRY(ps.ar_dynq.ensure((size_t)(R * ps.st_dynq)));
+    for (int s = 0; s < R; ++s) {
+        Scratch& sc = ps.slot[s];
+        auto view = [&](DevBuf& v, DevBuf& ar, int64_t st) {
+            v.p = (uint8_t*)ar.p + s * st;
+            v.bytes = (size_t)st;
+        };
+        view(sc.qfrag, ps.ar_qfrag, ps.st_qfrag);
+        view(sc.mkeys, ps.ar_mkeys, ps.st_mkeys);
+        view(sc.floor_q, ps.ar_floor, ps.st_floor);
+        view(sc.pbuf, ps.ar_pbuf, ps.st_pbuf);
+        view(sc.pcnt, ps.ar_pcnt, ps.st_pcnt);
+        view(sc.dyn_q, ps.ar_dynq, ps.st_dynq);
+        sc.last_W = W;
+        sc.last_Bp = pl.Bp;
+        sc.last_ng = 1;
+        sc.last_capw = kCapW;
+    }
+    ps.nwg = nwg;
+    ps.key_n = h->n;
+    ps.key_rows = h->rows;
+    ps.key_S = h->S;
+    ps.key_P = pl.P;
+    ps.key_ncu = h->n_cu;
+    ps.ready = true;
+    return HR_OK;
+}
+
 // error-bound constants for the approximate (MFMA) scores, see DESIGN.md "Exactness guard"
 static double acc_gamma(const hr_index* h) { return (double)(h->dpad + 64) * std::ldexp(1.0, -23); }
 static double storage_u(const hr_index* h) {
@@ -543,7 +706,6 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const int Bp = pl.Bp;
     const bool piped = st_tail != st && mode == 0;
     if (!piped) st_tail = st;
-    Scratch& sc = piped ? h->scr[h->flip] : h->scr[kSyncSet];
     const int64_t n_tiles = (h->n + 31) / 32;
     // SAMPLE size for n units: n/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M).  (Capping it at a
     // fraction of a small shard -- at 100k rows the fixed 2048 read 65 % of the shard again -- gained nothing:
@@ -573,6 +735,19 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     const int spare = wide_likely ? 0 : tail_cus(h);
     const bool early = piped && q_ready && h->tl_n < 0 && spare > 0 && !h->shared_dev &&
                        n_tiles >= early_min * sample_target(n_tiles);
+    // the persistent FILTER (hr_persist.hip) takes this batch: its FILTER runs in the instance streaming the
+    // batches one after another; prep, SAMPLE, select and rescore are this function's as for any pipelined batch
+    const bool persist = mode == 0 && !wide_likely && persist_wanted(h, pl, (kc + 31) / 32, early, mask_dev, n_tiles);
+    uint32_t pepoch = 0;
+    int pslot = 0;
+    if (persist) {
+        if (int rc = persist_configure(h, pl)) return rc;
+        pepoch = ++h->ps->epoch;
+        pslot = (int)((pepoch - 1) % kPersistSlots);
+    } else if (piped && h->ps && h->ps->active) {
+        if (int rc = persist_close(h)) return rc;  // another kind of batch: let the running instance go
+    }
+    Scratch& sc = persist ? h->ps->slot[pslot] : (piped ? h->scr[h->flip] : h->scr[kSyncSet]);
     hipStream_t sp = st;  // stream of query prep + SAMPLE
     if (early) {
         if (!h->pre) {
@@ -586,7 +761,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
         sp = h->pre;
     }
     if (piped) {
-        h->flip ^= 1;
+        if (!persist) h->flip ^= 1;
         if (!sc.scanned) HIP_TRY(hipEventCreateWithFlags(&sc.scanned, hipEventDisableTiming));
         if (!sc.released) HIP_TRY(hipEventCreateWithFlags(&sc.released, hipEventDisableTiming));
         if (early && !sc.sampled) HIP_TRY(hipEventCreateWithFlags(&sc.sampled, hipEventDisableTiming));
@@ -627,7 +802,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // batch i's and its workgroups take the CUs batch i's FILTER frees during its tail (measured
     // 0.482 -> 0.462 ms/step at 1.25M rows, 0.873 -> 0.835 at 2.5M, 1.625 -> 1.607 at 5M, no gain
     // at 10M)
-    const bool dual = early && n_tiles <= 160 * 1024;
+    const bool dual = early && !persist && n_tiles <= 160 * 1024;
     hipStream_t sf = st;  // stream of the FILTER scan
     if (dual) {
         if (!sc.scan) {
@@ -731,7 +906,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     // 3.05-3.07 ms (two alternating repeats on one box), so big shards keep the epilogue loads ...
     // ... except with 4+ row parts (k >= 75: a refresh then also reads the other parts' maxima), where the
     // early loads pay at 10M too: k = 100 3.217 -> 3.190 ms (profiles/r03_rowpart_knobs_10M.log)
-    a.early_refresh = (dual || np >= 4) ? 1 : 0;
+    a.early_refresh = (dual || persist || np >= 4) ? 1 : 0;
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;
@@ -751,6 +926,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             }
             ev.sampled = false;
             ev.early = early;
+            ev.pepoch = pepoch;
         }
         if (groups) {
             a.sample_stride = std::max<int64_t>(1, n_vis / s_target);
@@ -760,8 +936,10 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             ev.sampled = true;
             if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE
                 if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
-                HIP_TRY(hipEventRecord(sc.sampled, sp));
-                HIP_TRY(hipStreamWaitEvent(sf, sc.sampled, 0));
+                if (!persist) {
+                    HIP_TRY(hipEventRecord(sc.sampled, sp));
+                    HIP_TRY(hipStreamWaitEvent(sf, sc.sampled, 0));
+                }
             }
         }
         a.sample_stride = 1;
@@ -776,10 +954,44 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             if (other.armed && other.scanned) HIP_TRY(hipStreamWaitEvent(sf, other.scanned, 0));
         }
         h->isolate_next = dual && timed;
-        if (timed) HIP_TRY(hipEventRecord(ev.e[1], sf));
-        if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, sf)) return rc;
+        if (persist) {
+            // post the batch (admits it to a running instance), then an instance behind it on the instances'
+            // stream: it runs only if the running one has exited before admitting this batch (else it exits at once)
+            Persist& ps = *h->ps;
+            PersistLaunch pa{};
+            pa.a = a;
+            pa.a.qfrag = ps.ar_qfrag.as<uint16_t>();  // slot 0's buffers; slot s = + s * stride
+            pa.a.mkeys = ps.ar_mkeys.as<uint32_t>();
+            pa.a.floor_q = ps.ar_floor.as<float>();
+            pa.a.pbuf = ps.ar_pbuf.as<float2>();
+            pa.a.pcnt = ps.ar_pcnt.as<uint32_t>();
+            pa.a.capw = kCapW;
+            pa.a.ng = 1;
+            set_dyn_tail(pa.a, (int64_t)ps.nwg * (kScanThreads / 64), ps.ar_dynq.as<uint32_t>());
+            pa.st_qfrag = ps.st_qfrag;
+            pa.st_mkeys = ps.st_mkeys;
+            pa.st_floor = ps.st_floor;
+            pa.st_pbuf = ps.st_pbuf;
+            pa.st_pcnt = ps.st_pcnt;
+            pa.st_dynq = ps.st_dynq;
+            pa.ctl = ps.ctl.as<PersistCtl>();
+            pa.host_err = ps.host_err;
+            pa.e0 = pepoch;
+            pa.idle_ticks = ps.idle_ticks;
+            if (int rc = launch_persist_post(pa.ctl, pepoch, sp)) return rc;
+            HIP_TRY(hipEventRecord(ps.posted[pslot], sp));
+            HIP_TRY(hipStreamWaitEvent(ps.pst, ps.posted[pslot], 0));
+            if (int rc = launch_persist(mfma_type(h), h->dtype, pl.P, ps.nwg, pa, scan_lds_bytes(h, pl.QB), ps.pst))
+                return rc;
+            ps.active = true;
+            sc.wtiles_valid = false;
+            h->last_scr = &sc;
+        } else {
+            if (timed) HIP_TRY(hipEventRecord(ev.e[1], sf));
+            if (int rc = launch_scan(h, sc, cus, pl, a, groups ? SCAN_FILTER : SCAN_COLLECT, sf)) return rc;
+        }
         if (timed) {
-            HIP_TRY(hipEventRecord(ev.e[3], sf));
+            if (!persist) HIP_TRY(hipEventRecord(ev.e[3], sf));
             h->ev_pending.push_back(ev);
             while (h->ev_pending.size() > 4096) {  // nobody is harvesting: recycle the oldest
                 h->ev_free.push_back(h->ev_pending.front());
@@ -787,7 +999,11 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             }
         }
     }
-    if (piped) {  // the tail stream picks the batch up once its FILTER is done
+    if (persist) {  // the tail picks the batch up once every workgroup of the instance is through it
+        Persist& ps = *h->ps;
+        const uint32_t target = (uint32_t)ps.nwg * ((pepoch - 1) / kPersistSlots + 1);
+        if (int rc = launch_persist_wait(ps.ctl.as<PersistCtl>(), pslot, target, ps.host_err, st_tail)) return rc;
+    } else if (piped) {  // the tail stream picks the batch up once its FILTER is done
         HIP_TRY(hipEventRecord(sc.scanned, sf));
         HIP_TRY(hipStreamWaitEvent(st_tail, sc.scanned, 0));
     }
@@ -1085,6 +1301,7 @@ extern "C" int hr_index_search_device(hr_index* h, const float* q_dev, int B, in
     if (!h || !q_dev || !scores_out_dev || !rows_out_dev) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this search
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
     if (h->G > 1) return group_search_device(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
     return search_device_impl(h, q_dev, B, k, row_mask_dev, scores_out_dev, rows_out_dev, st);
@@ -1098,6 +1315,7 @@ extern "C" int hr_index_search_submit(hr_index* h, const float* q_dev, int B, in
     if (!h || !q_dev || !scores_out_dev || !rows_out_dev || !ticket_out) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this search
     if (int rc = validate_search(h, B, k)) return rc;
     hipStream_t st = (hipStream_t)stream;
     *ticket_out = 0;
@@ -1129,6 +1347,7 @@ static void notify_fd(void* p) {  // host function on the tail stream: one compl
 // collect copies the completed results.
 static int async_resolve_fallback(hr_index* h, hr_index::AsyncSlot& sl);
 static int async_drain(hr_index* h) {
+    if (int rc = persist_quiesce(h)) return rc;  // a running instance reads the rows too
     for (auto& sl : h->aslot)
         if (sl.busy && sl.done) {
             HIP_TRY(hipEventSynchronize(sl.done));
@@ -1177,6 +1396,7 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     if (!free_slot) return set_err(HR_E_BUSY, "two batches in flight: collect one first");
     auto& sl = *free_slot;
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;
     if (!h->atail) HIP_TRY(hipStreamCreateWithFlags(&h->atail, hipStreamNonBlocking));
     if (!h->acopy) HIP_TRY(hipStreamCreateWithFlags(&h->acopy, hipStreamNonBlocking));
     if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
@@ -1360,6 +1580,7 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
     if (!h || !q || !scores_out || !rows_out) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this search
     if (B <= 0) return set_err(HR_E_INVALID, "B must be positive");
     if (k <= 0) return set_err(HR_E_INVALID, "k must be positive");
     if (h->G > 1) return group_search_host(h, q, B, k, row_mask, scores_out, rows_out);
@@ -1440,6 +1661,7 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
     std::lock_guard<std::mutex> lk(h->mu);
     if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this search
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
@@ -1476,6 +1698,7 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
     std::lock_guard<std::mutex> lk(h->mu);
     if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
     if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this search
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
     std::vector<double> kth((size_t)B);
     HIP_TRY(hipMemcpyAsync(kth.data(), kth_dev, (size_t)B * 8, hipMemcpyDeviceToHost, st));
@@ -1724,6 +1947,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
         return;
     }
     (void)hipSetDevice(h->device);
+    persist_free(h);  // every persistent FILTER instance exits before the rows go
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rows) (void)hipFree(h->rows);
     if (h->live) (void)hipFree(h->live);
@@ -1762,10 +1986,25 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
     while (!h->ev_pending.empty() && k < cap) {
         hr_index::ScanEvents ev = h->ev_pending.front();
         h->ev_pending.pop_front();
-        HIP_TRY(hipEventSynchronize(ev.e[3]));
         float a = 0.f, b = 0.f;
-        if (ev.sampled) HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.early ? ev.e[2] : ev.e[1]));
-        HIP_TRY(hipEventElapsedTime(&b, ev.e[1], ev.e[3]));
+        if (ev.pepoch) {
+            // persistent FILTER: the SAMPLE by events; the FILTER's time per batch = the period between the device
+            // stamps of the last workgroup arrivals of this batch and the one before it (s_memrealtime, 100 MHz)
+            HIP_TRY(hipEventSynchronize(ev.e[2]));
+            HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.e[2]));
+            const PersistCtl* c = h->ps->ctl.as<PersistCtl>();
+            unsigned long long t1 = 0, t0 = 0;
+            for (int i = 0; i < 100000 && !t1; ++i) {  // (the batch is normally through already)
+                HIP_TRY(hipMemcpy(&t1, &c->t_end[ev.pepoch % kPersistRing], 8, hipMemcpyDeviceToHost));
+                if (!t1) usleep(10);
+            }
+            if (ev.pepoch > 1) HIP_TRY(hipMemcpy(&t0, &c->t_end[(ev.pepoch - 1) % kPersistRing], 8, hipMemcpyDeviceToHost));
+            b = (t1 && t0 && t1 > t0) ? (float)((double)(t1 - t0) * 1e-5) : 0.f;
+        } else {
+            HIP_TRY(hipEventSynchronize(ev.e[3]));
+            if (ev.sampled) HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.early ? ev.e[2] : ev.e[1]));
+            HIP_TRY(hipEventElapsedTime(&b, ev.e[1], ev.e[3]));
+        }
         if (sample_ms) sample_ms[k] = a;
         if (filter_ms) filter_ms[k] = b;
         h->last_sample_ms = a;
@@ -1774,6 +2013,36 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
         ++k;
     }
     if (n) *n = k;
+    return HR_OK;
+}
+
+// persistent FILTER (hr_persist.hip) of pipelined small-shard batches: 0 off, 1 shards up to 5.1M rows (default),
+// 2 every shard size; a change lets every running instance exit first
+extern "C" int hr_index_set_persist(hr_index* h, int mode) {
+    if (!h || mode < 0 || mode > 2) return set_err(HR_E_INVALID, "mode must be 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "the persistent FILTER serves single-device indexes");
+    if (int rc = persist_quiesce(h)) return rc;
+    if (!h->ps) h->ps = new Persist();
+    h->ps->mode = mode;
+    return HR_OK;
+}
+
+// no further batch for now: a running persistent FILTER instance exits once through the batches it was given
+// (instead of after its idle timeout); returns at once
+extern "C" int hr_index_persist_close(hr_index* h) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return HR_OK;
+    return persist_close(h);
+}
+
+// persistent FILTER diagnostics: out[0] = batches it served, out[1] = error word (0: none)
+extern "C" int hr_index_persist_stats(hr_index* h, int64_t out[2]) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    out[0] = h->ps ? (int64_t)h->ps->epoch : 0;
+    out[1] = (h->ps && h->ps->host_err) ? (int64_t)*(volatile uint32_t*)h->ps->host_err : 0;
     return HR_OK;
 }
 
@@ -1808,6 +2077,23 @@ extern "C" int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filte
     return HR_OK;
 }
 
+
+// diagnostics: tiles each wave of the most recent k_scan FILTER launch scanned ([group][wave]; blocking).  Every
+// tile is scanned exactly once per query group: the counts sum to groups x units (tiles, or tile-list entries)
+extern "C" int hr_index_wave_tiles(hr_index* h, uint32_t* out, int cap, int* n_out) {
+    if (!h || !out || !n_out || cap < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "single-device indexes");
+    const Scratch* sc = h->last_scr;
+    *n_out = 0;
+    if (!sc || !sc->wtiles.p || !sc->wtiles_valid) return HR_OK;
+    if (int rc = set_device(h)) return rc;
+    const int n = (int)std::min<int64_t>(cap, (int64_t)sc->last_ng * sc->last_W);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, sc->wtiles.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    *n_out = n;
+    return HR_OK;
+}
 
 // diagnostics: candidates appended by the last FILTER scan (sum and max over queries)
 extern "C" int hr_index_stats(hr_index* h, int64_t out[3]) {

@@ -78,6 +78,13 @@ int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hip
 // streamed window buffers (2 x 32 KiB, or 2 x 16 KiB for fp32 rows): at most 5 (bf16 / f16) or 7 (fp32) parts,
 // kc <= 160 / 224
 constexpr int wide_max_parts(int dtype) { return dtype == F32 ? 7 : 5; }
+// hr_persist.hip: the persistent FILTER (plans with 64-query tiles: P = 16 for 16-bit rows, 4 for fp32 rows)
+struct PersistCtl;
+struct PersistLaunch;
+int launch_persist(int mt, int dtype, int P, int cus, const PersistLaunch& pa, int lds, hipStream_t st);
+int launch_persist_post(PersistCtl* c, uint32_t e, hipStream_t st);
+int launch_persist_close(PersistCtl* c, hipStream_t st);
+int launch_persist_wait(PersistCtl* c, int s, uint32_t target, uint32_t* host_err, hipStream_t st);
 }  // namespace hr
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
@@ -89,10 +96,12 @@ static constexpr int kScanThreads = 512;
 // i+1's scan on the scan stream); a third serves the synchronous and collect paths.
 struct Scratch {
     DevBuf q32, qfrag, qerr, mkeys, floor_q, cnt, buf, sel_rows, sel_cnt, bound_approx, overflow, pbuf, pcnt, dyn_q,
-        tl, tl_tmp;  // device-mask tile list (+ its count after the list) and its rocPRIM scratch
+        tl, tl_tmp,  // device-mask tile list (+ its count after the list) and its rocPRIM scratch
+        wtiles;      // diagnostics: tiles each wave of the most recent FILTER launch scanned (ScanArgs::wave_tiles)
     int64_t last_W = 0, last_Bp = 0;  // waves (per query group) and queries per group of the most recent FILTER
     int last_ng = 1;                  // query groups of that launch
     int last_capw = kCapW;            // candidate slots per (region, query) of that launch
+    bool wtiles_valid = false;        // that launch was a k_scan FILTER (it wrote wtiles)
     hipEvent_t scanned = nullptr;     // scan stream: this set's FILTER is done
     hipEvent_t released = nullptr;    // tail stream: this set's select/rescore are done
     hipEvent_t sampled = nullptr;     // pre stream: this set's early query prep + SAMPLE are done
@@ -100,7 +109,7 @@ struct Scratch {
     bool armed = false;               // `released` has been recorded at least once
     void release_all() {
         for (DevBuf* b : {&q32, &qfrag, &qerr, &mkeys, &floor_q, &cnt, &buf, &sel_rows, &sel_cnt, &bound_approx,
-                          &overflow, &pbuf, &pcnt, &dyn_q, &tl, &tl_tmp})
+                          &overflow, &pbuf, &pcnt, &dyn_q, &tl, &tl_tmp, &wtiles})
             b->release();
         if (scanned) (void)hipEventDestroy(scanned);
         if (released) (void)hipEventDestroy(released);
@@ -128,6 +137,7 @@ struct hr_index {
     struct ScanEvents {
         hipEvent_t e[4];  // SAMPLE start, FILTER start (= SAMPLE end unless early), early SAMPLE end, FILTER end
         bool sampled, early;
+        uint32_t pepoch;  // persistent FILTER: the batch's epoch (its FILTER time comes from the device's stamps)
     };
     std::vector<ScanEvents> ev_free;
     std::deque<ScanEvents> ev_pending;
@@ -205,6 +215,7 @@ struct hr_index {
     hipEvent_t g_ev_q = nullptr;      // group: queries ready on the primary stream
     std::vector<char> g_peer;         // group: shard s's device has peer access with the primary
     struct GroupPipe* pipe = nullptr; // group: pipelined search (submit / finalize, hr_group.hip)
+    struct Persist* ps = nullptr;     // persistent FILTER state (hr_index.hip; created on first use)
 };
 
 // group-handle entry points (hr_group.hip); each public hr_index_* call forwards here when h->G > 1

@@ -270,6 +270,8 @@ struct ScanArgs {
     uint32_t* dyn_q;
     // euclidean: approximate score 2 q̂.x - |x|^2 (fp32 |x|^2 per row); nullptr for cosine / ip
     const float* xnorm;
+    // diagnostics (nullable): tiles each wave scanned, [group wave] -- every tile exactly once over a FILTER's waves
+    uint32_t* wave_tiles;
     // query groups (more than QB*32 queries per corpus pass): ng workgroups stream the same tile range,
     // each with its own QB*32 queries in LDS; per-query tables hold ng consecutive groups
     int ng;
@@ -282,6 +284,28 @@ struct ScanArgs {
     int dyn_pct;             // dynamic-tail percentage the host used (teams recompute their split)
 };
 
+
+// ---- the persistent FILTER (hr_persist.hip): control words of the instances and one instance's launch
+constexpr int kPersistSlots = 3;    // batches in flight between the host and an instance (workspace sets)
+constexpr int kPersistRing = 4096;  // per-epoch completion stamps
+struct PersistCtl {                 // device memory; initialised once per index
+    uint32_t gate;                  // admitted-through epoch (low 31 bits); bit 31: closed (no further admissions)
+    uint32_t posted;                // highest epoch whose query prep + SAMPLE are complete
+    uint32_t next_epoch;            // first epoch no instance has processed (written by an exiting instance)
+    uint32_t stop;                  // a quiesce asked the instances to stop admitting
+    uint32_t error;                 // a bounded wait gave up (1: instance, 2: tail)
+    uint32_t pad[3];
+    uint32_t done[4];               // per slot: workgroup arrivals, monotonic (target = workgroups x epochs of the slot)
+    unsigned long long t_end[kPersistRing];  // s_memrealtime of the last arrival of epoch e (index e % ring)
+};
+struct PersistLaunch {              // kernel argument of one instance
+    ScanArgs a;                     // the FILTER of slot 0's workspace; slot s: every per-batch pointer + s * its stride
+    int64_t st_qfrag, st_mkeys, st_floor, st_pbuf, st_pcnt, st_dynq;  // slot strides (bytes)
+    PersistCtl* ctl;
+    uint32_t* host_err;             // pinned host word mirroring PersistCtl::error (nullable)
+    uint32_t e0;                    // the epoch the instance was launched for
+    uint32_t idle_ticks;            // s_memrealtime ticks without an admission before the instance exits
+};
 
 template <int MT>
 __device__ inline f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c) {
@@ -381,12 +405,32 @@ enum { SCAN_SAMPLE = 0, SCAN_FILTER = 1, SCAN_COLLECT = 2 };
 // query-group launches and was slower (B = 128 at 10M rows: 5.7 / 6.3 ms vs 4.6 ms), so it is not built.
 // The body is shared; each MODE is its own kernel symbol (k_scan_sample / k_scan_filter / k_scan_collect,
 // below), so profiles tell the passes apart by name rather than by grid size or duration.
-template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB>
+// LEAN (the persistent FILTER, hr_persist.hip): one query group, one row part, no mask or tile list, round-robin
+// units -- fixed at compile time, which frees the scalar registers those cases take (the persistent loop around the
+// body needs a few of its own, and this body is at the 256-VGPR limit with SGPRs spilled to VGPR lanes).
+template <int MT, int DT, int QB, int P, int MODE, bool NT, int TPB, bool LEAN = false>
 __device__ __forceinline__ void scan_body(ScanArgs a) {
     constexpr bool FILTER = MODE != SCAN_SAMPLE;
     constexpr bool priv = MODE == SCAN_FILTER;
+    static_assert(!LEAN || MODE == SCAN_FILTER, "the lean body is a FILTER");
+    if constexpr (LEAN) {
+        a.ng = 1;
+        a.np = 1;
+        a.part_tiles = (int64_t)1 << 62;
+        a.mask = nullptr;
+        a.tile_list = nullptr;
+        a.strided = 1;
+        a.wave_major = 1;
+        a.teams = 0;
+        a.use_groups = 1;
+        a.publish = 1;
+    }
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int tid = threadIdx.x;
+    int tid_ = threadIdx.x;
+    // the persistent loop runs this body once per batch: lane-derived values are recomputed each time instead of
+    // being hoisted out of the loop into registers held across it (the body is at the 256-VGPR limit)
+    if constexpr (LEAN) asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
     const int lane = tid & 63;
     const int half = lane >> 5;
     const int g = lane & 31;
@@ -616,7 +660,8 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
         return u < n_units ? u : -1;
     };
     uint32_t rkey[QB][16];  // group-max keys of the refresh due in the current tile's epilogue
-    const bool early_refresh = a.early_refresh != 0;
+    // (LEAN: never -- the 32 keys held across the k-loop cost the registers the persistent loop needs)
+    const bool early_refresh = !LEAN && a.early_refresh != 0;
     int64_t u = u0, u_end = u1, pend = -1, done = 0;
     uint32_t graw = 0;
     bool issued = false;  // this run's grab is in flight (exactly one grab per run)
@@ -769,6 +814,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
     }
 
     if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = mycnt;
+    if (a.wave_tiles && lane == 0) a.wave_tiles[wg] = (uint32_t)done;
     if (!FILTER && a.publish) {
         // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope
         // atomics from 8 XCDs), where same-address atomics serialise, so the workgroup's 8 waves

@@ -45,7 +45,8 @@ EXPORTS = [
     "hr_gen_rows_device", "hr_ivf_search", "hr_topk_records", "hr_index_search_shard_async_ev", "hr_index_stats",
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_index_wide_launches", "hr_kc_for_k_dim",
     "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
-    "hr_index_search_collect", "hr_index_search_poll",
+    "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
+    "hr_index_persist_stats", "hr_index_wave_tiles",
 ]
 
 _lib = None
@@ -96,6 +97,10 @@ def load_library(path: str | None = None):
             "hr_index_search_submit_host": [vp, vp, i32, i32, i32, vp],
             "hr_index_search_collect": [vp, i64, vp, vp],
             "hr_index_search_poll": [vp, i64, vp],
+            "hr_index_set_persist": [vp, i32],
+            "hr_index_persist_close": [vp],
+            "hr_index_persist_stats": [vp, vp],
+            "hr_index_wave_tiles": [vp, vp, i32, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
@@ -381,6 +386,27 @@ class NativeIndex:
         out = ctypes.c_int64(0)
         _check(self.lib.hr_index_wide_launches(self._h, ctypes.byref(out)))
         return out.value
+
+    def wave_tiles(self, cap: int = 1 << 16) -> np.ndarray:
+        """Tiles each wave of the most recent k_scan FILTER launch scanned ([group][wave], hr_index_wave_tiles)."""
+        out = np.zeros(cap, np.uint32)
+        n = ctypes.c_int(0)
+        _check(self.lib.hr_index_wave_tiles(self._h, _ptr(out), int(cap), ctypes.byref(n)))
+        return out[: n.value].copy()
+
+    def set_persist(self, mode: int) -> None:
+        """Persistent FILTER of pipelined shard batches: 0 off, 1 shards up to 5.1M rows (default), 2 any size."""
+        _check(self.lib.hr_index_set_persist(self._h, int(mode)))
+
+    def persist_close(self) -> None:
+        """No further batch for now: a running persistent FILTER exits once through its batches."""
+        _check(self.lib.hr_index_persist_close(self._h))
+
+    def persist_stats(self) -> dict:
+        """Persistent FILTER diagnostics: batches served, error word (0 = none)."""
+        out = (ctypes.c_int64 * 2)()
+        _check(self.lib.hr_index_persist_stats(self._h, out))
+        return {"batches": out[0], "error": out[1]}
 
     def graph_replays(self) -> int:
         """hr_index_search calls answered by a captured HIP graph (hr_index_graph_replays)."""

@@ -248,6 +248,9 @@ class ShardedSearch:
             slot = self.slots[(self._next + i) % len(self.slots)]
             if slot.ticket is not None:
                 self.finalize(slot)
+        close = getattr(self.index, "persist_close", None)
+        if close is not None:  # no batch behind these: a running persistent FILTER may exit now
+            close()
 
     def search(self, q, k: int, s_out=None, r_out=None, mask_ptr: int = 0, src_rank: int | None = None):
         """Synchronous search of one batch.  Returns (scores, rows) device tensors.  src_rank: the batch

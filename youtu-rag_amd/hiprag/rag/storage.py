@@ -280,6 +280,12 @@ class HipVectorStore(BaseVectorStore):
         self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)), int(params.get("search_depth", 2)))
         # unfiltered batches launched from the event loop through the asynchronous native entry point
         self.native_async = bool(params.get("native_async", True))
+        # after a bulk load (>= gc_freeze_rows rows since the last freeze) the process's tracked objects move to
+        # the collector's permanent generation (gc.freeze); see _after_bulk_load.  index_params gc_freeze: false
+        # leaves the collector alone
+        self.gc_freeze = bool(params.get("gc_freeze", True))
+        self.gc_freeze_rows = int(params.get("gc_freeze_rows", 100_000))
+        self._rows_since_freeze = 0
         self._lock = threading.RLock()
         self._paths = P.Paths(config.persist_directory, config.collection_name)
         self._gen = 0
@@ -393,6 +399,8 @@ class HipVectorStore(BaseVectorStore):
             self._defer -= 1
             if self._defer == 0 and self._dirty:
                 self.flush()
+            if self._defer == 0:
+                self._after_bulk_load()
 
     def flush(self):
         """Write a new snapshot generation now (folds the journal in)."""
@@ -484,6 +492,9 @@ class HipVectorStore(BaseVectorStore):
             live[: len(self._live)] = self._live
             self._live = live
         self._live[first:n] = [rec is not None for rec in records]
+        self._rows_since_freeze += len(records)
+        if self._defer == 0:
+            self._after_bulk_load()
         if self.keep_embeddings:
             if self._raw is None or len(self._raw) < n:
                 raw = np.zeros((max(n, 2 * (0 if self._raw is None else len(self._raw)), 1024), self.dim), np.float32)
@@ -492,6 +503,24 @@ class HipVectorStore(BaseVectorStore):
                 self._raw = raw
             if vectors is not None:
                 self._raw[first:n] = vectors
+
+    def _after_bulk_load(self):
+        """gc.freeze() once a bulk load is in (>= gc_freeze_rows rows appended since the last freeze).
+
+        Every search hit is a new Chunk and a (Chunk, score) tuple -- tracked objects, by the API's types -- that
+        live until the caller drops them, so they reach the collector's oldest generation, and each full collection
+        then walks the whole process heap: 84 ms over a serving process's ~190k long-lived objects (torch alone is
+        ~170k), several times a second at 20k queries/s (profiles/r03_async_store_10M_gc.jsonl: 12.5k QPS at 256
+        clients, 20.2k with the application calling gc.freeze()).  Freezing moves the objects alive now (imports,
+        the loaded collection) into the permanent generation, so full collections walk only what was allocated
+        since: the standard serving recipe, done here once per bulk load so an unmodified application gets it.
+        Garbage cycles alive at the freeze are kept (not collected); index_params gc_freeze: false opts out."""
+        if not self.gc_freeze or self._rows_since_freeze < self.gc_freeze_rows:
+            return
+        import gc
+
+        gc.freeze()
+        self._rows_since_freeze = 0
 
     def _register(self, fresh: list[Chunk], first: int, vectors: np.ndarray | None):
         records = [self._record(c) for c in fresh]

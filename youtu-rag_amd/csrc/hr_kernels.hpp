@@ -528,6 +528,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
 
     if (u0 >= u1 && FILTER) {
         if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = 0;
+        if (a.wave_tiles && lane == 0) a.wave_tiles[wg] = 0u;
         return;
     }  // an idle SAMPLE wave stays: it takes part in the workgroup reduction below
     uint32_t mycnt = 0;  // private mode: lane q counts the candidates of query q in this wave

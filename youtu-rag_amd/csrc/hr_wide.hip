@@ -98,7 +98,9 @@ __global__ __launch_bounds__(512, 1) void k_filter_wide8(ScanArgs a) {
     __shared__ __attribute__((aligned(16))) float pmin[KP][128];
     const int np = PARTS ? a.np : 1;
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = lane >> 5, g = lane & 31;
+    // wv: wave-uniform (readfirstlane), so every per-wave base below (candidate regions, tile positions) is a scalar
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5,
+              g = lane & 31;
     const int64_t W = (int64_t)gridDim.x * 8;
     const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;
     const int64_t n_tiles = a.n_units;

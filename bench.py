@@ -526,6 +526,18 @@ def main():
     if pst["error"]:
         raise RuntimeError(f"persistent FILTER error {pst['error']}")
     persist = pst["batches"] - persist0 == args.steps  # every timed batch went through the persistent FILTER
+    persist_timeline = None
+    if persist:  # where the period goes (device stamps, us): medians over the timed batches
+        tr = index.persist_trace(args.steps)
+        if len(tr) > 2:
+            post, s0, s1, e0, e1 = (tr[:, j] for j in range(5))
+            med = lambda x: round(float(np.median(x)), 2)  # noqa: E731
+            persist_timeline = {
+                "period_us": med(np.diff(e1)), "busy_us": med(e1 - s0),
+                "start_spread_us": med(s1 - s0), "end_spread_us": med(e1 - e0),
+                "post_before_prev_end_us": med(e1[:-1] - post[1:]),
+                "first_start_after_prev_first_end_us": med(s0[1:] - e0[:-1]),
+                "instances_run": int(pst["runs"])}
     # one untimed batch of isotropic queries (the worst case for ranking: no planted neighbour), for the
     # recall checks; every rank takes part (the merge is collective)
     q_iso = isotropic_queries(B, D)
@@ -582,6 +594,7 @@ def main():
                      "read_ceiling_source": "profiles/r02_stream_ceiling.jsonl", "traffic": None,
                      "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg / passes, 4),
                      "sample_pass_ms": round(sample_avg, 4)},
+        **({"persist_timeline": persist_timeline} if persist_timeline else {}),
         # the Q·Xᵀ contraction of the same launch on the MFMA pipe (bf16 dense peak, MI355X_MICROARCH.md)
         "mfma": {"achieved": round(mfma_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                  "frac": round(mfma_tflops / MFMA_PEAK_TFLOPS, 4), "flops_per_launch": mfma_flops},

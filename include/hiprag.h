@@ -225,14 +225,17 @@ int hr_add_layernorm(const void* x_dev, const void* r_dev, const void* gamma_dev
  * ramp and tail; replaces the per-batch FILTER launch behind hr_index_search_shard_async_ev (same results).
  * set_persist: 0 off, 1 shards up to 5.1M rows (default), 2 every shard size.  persist_close: no further batch
  * for now (the running instance exits once through its batches instead of after its 300 us idle timeout).
- * persist_stats: out[0] = batches served, out[1] = error word (a bounded wait gave up; 0 = none). */
+ * persist_stats: out[0] = batches served, out[1] = error word (a bounded wait gave up; 0 = none), out[2] =
+ * instances that ran.  persist_trace: per epoch of the last n (oldest first), 5 device stamps in us relative to the
+ * first one's post -- post, first / last workgroup start, first / last workgroup arrival (blocking). */
 /* Diagnostics: tiles each wave of the most recent k_scan FILTER launch scanned ([query group][wave], blocking;
  * up to cap counts, the number in n_out).  Every unit is scanned exactly once per group, so the counts sum to
  * groups x units -- the invariant of the round-robin dealing, its rotation and the dynamic tail. */
 int hr_index_wave_tiles(hr_index* h, uint32_t* out, int cap, int* n_out);
 int hr_index_set_persist(hr_index* h, int mode);
 int hr_index_persist_close(hr_index* h);
-int hr_index_persist_stats(hr_index* h, int64_t out[2]);
+int hr_index_persist_stats(hr_index* h, int64_t out[3]);
+int hr_index_persist_trace(hr_index* h, int n, double* out, int* n_out);
 /* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
  * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
 int hr_index_set_scan_timing(hr_index* h, int every);

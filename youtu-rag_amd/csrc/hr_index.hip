@@ -2037,12 +2037,49 @@ extern "C" int hr_index_persist_close(hr_index* h) {
     return persist_close(h);
 }
 
-// persistent FILTER diagnostics: out[0] = batches it served, out[1] = error word (0: none)
-extern "C" int hr_index_persist_stats(hr_index* h, int64_t out[2]) {
+// persistent FILTER diagnostics: out[0] = batches it served, out[1] = error word (0: none), out[2] = instances that
+// ran (a batch admitted to a running instance adds none; an idle exit makes the next batch's instance run)
+extern "C" int hr_index_persist_stats(hr_index* h, int64_t out[3]) {
     if (!h || !out) return set_err(HR_E_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
     out[0] = h->ps ? (int64_t)h->ps->epoch : 0;
     out[1] = (h->ps && h->ps->host_err) ? (int64_t)*(volatile uint32_t*)h->ps->host_err : 0;
+    out[2] = 0;
+    if (h->ps && h->ps->ctl.p) {
+        if (int rc = set_device(h)) return rc;
+        uint32_t runs = 0;
+        HIP_TRY(hipMemcpy(&runs, &h->ps->ctl.as<PersistCtl>()->runs, 4, hipMemcpyDeviceToHost));
+        out[2] = runs;
+    }
+    return HR_OK;
+}
+
+// persistent FILTER timeline of the last n epochs (through the latest submitted one; n <= 4096), 5 stamps each in
+// microseconds relative to the first returned post: post, first workgroup start, last workgroup start, first
+// arrival, last arrival (0 where not stamped yet); returns the epochs written in *n_out.  Blocking (device copies).
+extern "C" int hr_index_persist_trace(hr_index* h, int n, double* out, int* n_out) {
+    if (!h || !out || !n_out || n < 0) return set_err(HR_E_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *n_out = 0;
+    if (!h->ps || !h->ps->ctl.p || h->ps->epoch == 0) return HR_OK;
+    if (int rc = set_device(h)) return rc;
+    const int64_t last = (int64_t)h->ps->epoch;
+    const int m = (int)std::min<int64_t>({(int64_t)n, last, (int64_t)kPersistRing});
+    std::vector<PersistCtl> c(1);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(c.data(), h->ps->ctl.p, sizeof(PersistCtl), hipMemcpyDeviceToHost));
+    const unsigned long long base = c[0].t_post[(last - m + 1) % kPersistRing];
+    auto rel = [&](unsigned long long t) { return (t == 0ull || t == ~0ull) ? 0.0 : ((double)t - (double)base) * 1e-2; };
+    for (int i = 0; i < m; ++i) {
+        const int r = (int)((last - m + 1 + i) % kPersistRing);
+        double* o = out + 5 * (size_t)i;
+        o[0] = rel(c[0].t_post[r]);
+        o[1] = rel(c[0].t_start0[r]);
+        o[2] = rel(c[0].t_start1[r]);
+        o[3] = rel(c[0].t_end0[r]);
+        o[4] = rel(c[0].t_end[r]);
+    }
+    *n_out = m;
     return HR_OK;
 }
 

@@ -294,9 +294,13 @@ struct PersistCtl {                 // device memory; initialised once per index
     uint32_t next_epoch;            // first epoch no instance has processed (written by an exiting instance)
     uint32_t stop;                  // a quiesce asked the instances to stop admitting
     uint32_t error;                 // a bounded wait gave up (1: instance, 2: tail)
-    uint32_t pad[3];
+    uint32_t runs;                  // instances that ran (did not find their batch processed already)
+    uint32_t pad[2];
     uint32_t done[4];               // per slot: workgroup arrivals, monotonic (target = workgroups x epochs of the slot)
-    unsigned long long t_end[kPersistRing];  // s_memrealtime of the last arrival of epoch e (index e % ring)
+    // per-epoch s_memrealtime stamps (index e % ring; the post resets them): the last arrival (the tail's timing),
+    // and for hr_index_persist_trace the post, the first and last workgroup start and the first arrival
+    unsigned long long t_end[kPersistRing];
+    unsigned long long t_post[kPersistRing], t_start0[kPersistRing], t_start1[kPersistRing], t_end0[kPersistRing];
 };
 struct PersistLaunch {              // kernel argument of one instance
     ScanArgs a;                     // the FILTER of slot 0's workspace; slot s: every per-batch pointer + s * its stride

@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
     __syncthreads();
     if (!cmd) return;
     if (leader) {
+        __hip_atomic_fetch_add(&c->runs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // open the gate for this instance: every batch posted so far is ready (its post followed its SAMPLE); with a
         // close requested (quiesce), keep it closed -- this instance then serves its own batch only
         const uint32_t p = ld_agent(&c->posted);
@@ -101,6 +102,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
             if (tid == 0) cmd = wait_admission(c, e, leader, pa.idle_ticks, pa.host_err);
             __syncthreads();
             if (!cmd) break;
+        }
+        if (tid == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_fetch_min(&c->t_start0[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max(&c->t_start1[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         {
             ScanArgs a = pa.a;
@@ -120,8 +126,9 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_fetch_add(&c->done[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_max(&c->t_end[e % kPersistRing], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_fetch_max(&c->t_end[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_min(&c->t_end0[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         ++e;
     }
@@ -131,6 +138,13 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
 // behind batch e's query prep + SAMPLE on the pre stream: batch e is ready; admit it to a running instance
 __global__ void k_persist_post(PersistCtl* c, uint32_t e) {
     if (threadIdx.x == 0) {
+        const int r = (int)(e % kPersistRing);  // the epoch's stamps (its previous use, e - ring, is long through)
+        c->t_end[r] = 0ull;
+        c->t_start1[r] = 0ull;
+        c->t_start0[r] = ~0ull;
+        c->t_end0[r] = ~0ull;
+        c->t_post[r] = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_max(&c->posted, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t expect = e - 1;
         __hip_atomic_compare_exchange_strong(&c->gate, &expect, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,

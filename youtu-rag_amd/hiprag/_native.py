@@ -46,7 +46,7 @@ EXPORTS = [
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_index_wide_launches", "hr_kc_for_k_dim",
     "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
     "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
-    "hr_index_persist_stats", "hr_index_wave_tiles",
+    "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles",
 ]
 
 _lib = None
@@ -100,6 +100,7 @@ def load_library(path: str | None = None):
             "hr_index_set_persist": [vp, i32],
             "hr_index_persist_close": [vp],
             "hr_index_persist_stats": [vp, vp],
+            "hr_index_persist_trace": [vp, ctypes.c_int, vp, vp],
             "hr_index_wave_tiles": [vp, vp, i32, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
@@ -403,10 +404,18 @@ class NativeIndex:
         _check(self.lib.hr_index_persist_close(self._h))
 
     def persist_stats(self) -> dict:
-        """Persistent FILTER diagnostics: batches served, error word (0 = none)."""
-        out = (ctypes.c_int64 * 2)()
+        """Persistent FILTER diagnostics: batches served, error word (0 = none), instances that ran."""
+        out = (ctypes.c_int64 * 3)()
         _check(self.lib.hr_index_persist_stats(self._h, out))
-        return {"batches": out[0], "error": out[1]}
+        return {"batches": out[0], "error": out[1], "runs": out[2]}
+
+    def persist_trace(self, n: int = 64) -> np.ndarray:
+        """[epochs, 5] device stamps (us, from the first returned post) of the last n persistent batches: post,
+        first / last workgroup start, first / last workgroup arrival."""
+        out = np.zeros((max(0, int(n)), 5), np.float64)
+        m = ctypes.c_int(0)
+        _check(self.lib.hr_index_persist_trace(self._h, int(n), out.ctypes.data, ctypes.byref(m)))
+        return out[: m.value].copy()
 
     def graph_replays(self) -> int:
         """hr_index_search calls answered by a captured HIP graph (hr_index_graph_replays)."""

@@ -68,7 +68,7 @@ def parse():
                         "loop then includes the all-gather an 8-GPU node runs")
     p.add_argument("--persist", type=int, default=1, choices=(0, 1, 2),
                    help="persistent FILTER for the pipelined shard batches: 0 off (one FILTER launch per batch), "
-                        "1 shards up to 5.1M rows (default), 2 every shard size")
+                        "1 shards of 4.2M-5.1M rows (default: where it measured faster), 2 every shard size")
     p.add_argument("--single-process", action="store_true",
                    help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()

@@ -223,7 +223,8 @@ int hr_add_layernorm(const void* x_dev, const void* r_dev, const void* gamma_dev
 /* The persistent FILTER (pipelined shard batches of <= 64 queries, k <= 16, no mask, early SAMPLE: the per-GPU
  * step of a row-sharded node).  One long-lived launch streams the corpus batch after batch -- no per-batch launch
  * ramp and tail; replaces the per-batch FILTER launch behind hr_index_search_shard_async_ev (same results).
- * set_persist: 0 off, 1 shards up to 5.1M rows (default), 2 every shard size.  persist_close: no further batch
+ * set_persist: 0 off, 1 shards of 4.2M-5.1M rows (default: where it measured faster than per-batch launches),
+ * 2 every shard size.  persist_close: no further batch
  * for now (the running instance exits once through its batches instead of after its 300 us idle timeout).
  * persist_stats: out[0] = batches served, out[1] = error word (a bounded wait gave up; 0 = none), out[2] =
  * instances that ran.  persist_trace: per epoch of the last n (oldest first), 5 device stamps in us relative to the

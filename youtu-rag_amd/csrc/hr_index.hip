@@ -18,7 +18,7 @@ static int async_drain(hr_index* h);
 // one arena per kind, so an instance finds slot s's buffers as slot 0's + s * stride; the other per-batch buffers
 // (select / rescore) are the slots' own.  Configured for one corpus state and plan; re-configured after a quiesce.
 struct Persist {
-    int mode = 1;                      // hr_index_set_persist: 0 off, 1 small shards (default), 2 every shard size
+    int mode = 1;                      // hr_index_set_persist: 0 off, 1 where it measured faster (default), 2 always
     bool ready = false;                // configured (for the key below)
     int64_t key_n = -1;
     const void* key_rows = nullptr;
@@ -605,12 +605,17 @@ static void persist_free(hr_index* h) {
 
 // The persistent FILTER serves this pipelined batch?  Unmasked, one 64-query tile (one group, one row part: k <= 16),
 // not the 128-query FILTER, a plan it is built for, early-SAMPLE conditions met, a single-device index (not a group
-// shard), and (mode 1) a shard in the dual-FILTER range (<= 160k tiles = 5.1M rows: 1.25M rows at G = 8).
+// shard), and (mode 1) a shard where it measured faster than per-batch launches: 128k-160k tiles (4.2M-5.1M rows: the
+// 5M-row shard of a 10M corpus at G = 2, 1.532-1.558 vs 1.581-1.606 ms/step on two boxes).  Below that the dual
+// FILTER streams already hide each launch's ramp and tail and the instance's per-batch hand-off costs more (1.25M
+// rows: 0.435 ms device period vs 0.427-0.432 ms/step; 2.5M: 0.794 vs 0.805; 625k: the SAMPLE chain bounds both),
+// and the single-stream 10M launch equals it (2.992 vs 3.003 ms; profiles/r04_persist_vs_launches_shard_sweep.jsonl,
+// r04_persist_sc1_shard_sweep.jsonl).
 static bool persist_wanted(hr_index* h, const Plan& pl, int np, bool early, const uint64_t* mask_dev, int64_t n_tiles) {
     const int mode = h->ps ? h->ps->mode : 1;
     if (mode == 0 || !early || mask_dev || np != 1 || pl.NG != 1 || pl.QB != 2 || h->stripe_G != 1) return false;
     if (!(h->dtype != F32 ? pl.P == 16 : pl.P == 4)) return false;
-    return mode == 2 || n_tiles <= 160 * 1024;
+    return mode == 2 || (n_tiles >= 128 * 1024 && n_tiles <= 160 * 1024);
 }
 
 // (re)configure for the current corpus and plan: arenas sized for one 64-query tile per slot
@@ -1988,8 +1993,10 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
         h->ev_pending.pop_front();
         float a = 0.f, b = 0.f;
         if (ev.pepoch) {
-            // persistent FILTER: the SAMPLE by events; the FILTER's time per batch = the period between the device
-            // stamps of the last workgroup arrivals of this batch and the one before it (s_memrealtime, 100 MHz)
+            // persistent FILTER: the SAMPLE by events; the FILTER's time per batch = from the later of the previous
+            // batch's last workgroup arrival and this batch's first workgroup start to this batch's last arrival
+            // (device stamps, s_memrealtime at 100 MHz): the period in a steady stream, the batch's own span after a
+            // gap (an idle instance is not charged to the batch)
             HIP_TRY(hipEventSynchronize(ev.e[2]));
             HIP_TRY(hipEventElapsedTime(&a, ev.e[0], ev.e[2]));
             const PersistCtl* c = h->ps->ctl.as<PersistCtl>();
@@ -1999,6 +2006,9 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
                 if (!t1) usleep(10);
             }
             if (ev.pepoch > 1) HIP_TRY(hipMemcpy(&t0, &c->t_end[(ev.pepoch - 1) % kPersistRing], 8, hipMemcpyDeviceToHost));
+            unsigned long long ts = 0;
+            HIP_TRY(hipMemcpy(&ts, &c->t_start0[ev.pepoch % kPersistRing], 8, hipMemcpyDeviceToHost));
+            if (ts != ~0ull && ts > t0) t0 = ts;
             b = (t1 && t0 && t1 > t0) ? (float)((double)(t1 - t0) * 1e-5) : 0.f;
         } else {
             HIP_TRY(hipEventSynchronize(ev.e[3]));
@@ -2016,7 +2026,8 @@ static int harvest(hr_index* h, float* sample_ms, float* filter_ms, int cap, int
     return HR_OK;
 }
 
-// persistent FILTER (hr_persist.hip) of pipelined small-shard batches: 0 off, 1 shards up to 5.1M rows (default),
+// persistent FILTER (hr_persist.hip) of pipelined shard batches: 0 off, 1 shards of 4.2M-5.1M rows (default: where it
+// measured faster),
 // 2 every shard size; a change lets every running instance exit first
 extern "C" int hr_index_set_persist(hr_index* h, int mode) {
     if (!h || mode < 0 || mode > 2) return set_err(HR_E_INVALID, "mode must be 0, 1 or 2");

@@ -531,7 +531,12 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
     __syncthreads();
 
     if (u0 >= u1 && FILTER) {
-        if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = 0;
+        if (priv && lane < QB * 32) {
+            if constexpr (LEAN)
+                __hip_atomic_store(&a.pcnt[wg * (QB * 32) + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                a.pcnt[wg * (QB * 32) + lane] = 0;
+        }
         if (a.wave_tiles && lane == 0) a.wave_tiles[wg] = 0u;
         return;
     }  // an idle SAMPLE wave stays: it takes part in the workgroup reduction below
@@ -780,8 +785,14 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
                                 const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)mycnt, q);
                                 if (pass && half == h) {
                                     const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
-                                    if (pos < (uint32_t)a.capw)
-                                        wave_buf[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                                    if (pos < (uint32_t)a.capw) {
+                                        if constexpr (LEAN)  // write-through (sc1): no release fence per batch
+                                            __hip_atomic_store((uint64_t*)&wave_buf[q * a.capw + pos],
+                                                               ((uint64_t)row << 32) | __builtin_bit_cast(uint32_t, v),
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                        else
+                                            wave_buf[q * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                                    }
                                 }
                                 mycnt += (lane == q) ? (uint32_t)__builtin_popcount(mh) : 0u;
                             } else if (!priv && mh) {
@@ -818,7 +829,12 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
         }
     }
 
-    if (priv && lane < QB * 32) a.pcnt[wg * (QB * 32) + lane] = mycnt;
+    if (priv && lane < QB * 32) {
+        if constexpr (LEAN)
+            __hip_atomic_store(&a.pcnt[wg * (QB * 32) + lane], mycnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            a.pcnt[wg * (QB * 32) + lane] = mycnt;
+    }
     if (a.wave_tiles && lane == 0) a.wave_tiles[wg] = (uint32_t)done;
     if (!FILTER && a.publish) {
         // SAMPLE: publish the group maxima.  The table lives at the memory side (device-scope

@@ -1,12 +1,15 @@
 // hr_persist.hip -- the persistent FILTER: one long-lived launch streams the corpus for consecutive batches.
 //
-// A pipelined small shard (the per-GPU step of a row-sharded node: 1.25M rows at G = 8) pays each FILTER launch's
-// ramp and tail -- waves of one launch end tens of microseconds apart, and the next launch's workgroups only take a
-// CU once the previous one frees it -- on a 0.42 ms step (0.75 of 8 TB/s, against 0.86 for one 10M
-// launch).  Here an INSTANCE of k_scan_persist (one workgroup per CU on the CUs the tail stream leaves free) runs
-// batch after batch: a workgroup that is through its share of batch e's tiles restages batch e+1's queries into its
-// LDS and goes on, so the chip keeps reading while the last tiles of batch e finish elsewhere -- the stream is as
-// continuous as one long launch.
+// A pipelined shard pays each FILTER launch's ramp and tail -- waves of one launch end tens of microseconds apart,
+// and the next launch's workgroups only take a CU once the previous one frees it (the 1.25M-row step at
+// 0.75 of 8 TB/s, against 0.86 for one 10M launch).  Here an INSTANCE of k_scan_persist (one workgroup per CU on the
+// CUs the tail stream leaves free) runs batch after batch: a workgroup that is through its share of batch e's tiles
+// restages batch e+1's queries into its LDS and goes on, so the chip keeps reading while the last tiles of batch e
+// finish elsewhere -- the stream is as continuous as one long launch (device stamps: a workgroup starts batch e+1
+// within ~1 us of finishing batch e; every workgroup's start and end spread over ~23 us).
+// Measured ("Persistent FILTER"): faster than per-batch launches for 4.2M-5.1M-row shards (5M rows:
+// 1.53 vs 1.58 ms/step), not below, where the dual FILTER streams already overlap consecutive launches -- so the
+// default (mode 1) takes it in that range only.
 //
 // Hand-offs (all inside one device; MI355X_MICROARCH.md "inter-workgroup visibility" / cdna_hip_programming.md
 // Guideline 16 -- agent-scope atomics on the control words, a release before every signal, one acquire after every
@@ -22,8 +25,8 @@
 //    behind every batch on the persist stream, gated by that batch's post event; it starts after the running instance
 //    has exited, finds from `next_epoch` whether its batch was processed, and processes it (and the batches admitted
 //    after it) if not -- otherwise it exits at once;
-//  * instance -> tail: each workgroup, through a batch, drains its stores, releases (buffer_wbl2) and adds 1 to the
-//    slot's `done` counter; a one-lane kernel on the tail stream (k_persist_wait) polls it up to the batch's target
+//  * instance -> tail: each workgroup, through a batch, drains its write-through (sc1) candidate and count stores
+//    and adds 1 to the slot's `done` counter; a one-lane kernel on the tail stream (k_persist_wait) polls it up to the batch's target
 //    and the tail's select / rescore follow it in stream order (a kernel boundary: their own acquire).
 // Every wait is bounded (an exit condition every wave reaches): the instance's non-leader polls give up after
 // kHardTicks, the tail wait after kHardTicks too; either sets `error` (and the host's pinned error word) instead of
@@ -119,12 +122,12 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
             a.dyn_q = at(a.dyn_q, pa.st_dynq);
             scan_body<MT, DT, 2, P, SCAN_FILTER, true, kScanThreads, true>(a);
         }
-        // through batch e: every wave's candidate stores drained, then one release and the slot's arrival
+        // through batch e: the lean body stores its candidates and counts write-through (sc1, Guideline 16 R1), so
+        // every wave drains them, the workgroup meets, and one lane adds the slot's arrival -- no release fence
+        // (an L2 writeback per workgroup per batch: 28 per XCD every batch)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_fetch_add(&c->done[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long t = __builtin_amdgcn_s_memrealtime();
             __hip_atomic_fetch_max(&c->t_end[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

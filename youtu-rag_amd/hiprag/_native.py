@@ -396,7 +396,7 @@ class NativeIndex:
         return out[: n.value].copy()
 
     def set_persist(self, mode: int) -> None:
-        """Persistent FILTER of pipelined shard batches: 0 off, 1 shards up to 5.1M rows (default), 2 any size."""
+        """Persistent FILTER of pipelined shard batches: 0 off, 1 shards of 4.2M-5.1M rows (default), 2 any size."""
         _check(self.lib.hr_index_set_persist(self._h, int(mode)))
 
     def persist_close(self) -> None:

@@ -197,8 +197,9 @@ def cpu_reference_baseline(args, qbatches, N, D, K, B):
 def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> dict:
     """The reference's query path on the GPU, beside cpu_baseline's CPU embed+search: ``embed_query`` then
     ``search`` (base_retriever.py:57-62; the embedding server's encode, deploying-locally.mdx:81-116) -- B query
-    strings -> TorchRocmEmbedder (the same bge-large shape as the CPU leg, bf16, unpadded packed forward + K7
-    pooling) -> the exact scan over the resident corpus (this bench's searcher), timed end to end:
+    strings -> TorchRocmEmbedder (the same bge-large shape as the CPU leg, bf16, unpadded packed forward replayed
+    from HIP graphs + K7 pooling) -> the exact scan over the resident corpus (this bench's searcher), timed end to
+    end:
     * ``sequential``: one batch at a time, embed -> search -> synchronise (a lone caller's latency);
     * ``pipelined``: the embedder on a stream of its own, each batch's search submitted behind its queries' event,
       two batches in flight (the throughput a serving process gets);
@@ -218,7 +219,9 @@ def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> 
     fl = EncoderFlops(emb.model, emb.unpadded)
     texts = [[f"what does document {i * B + j} say about topic {(i * B + j) % 7} and its retrieval setup"
               for j in range(B)] for i in range(n_batches + 2)]
-    for t in texts[:2]:  # warm: kernels, allocator, tokenizer caches
+    # warm: kernels, allocator, tokenizer caches and the embed's HIP graphs -- one per packed shape (a serving
+    # process's steady state: query batches fall into a few shapes, each captured once; encoder.GraphedForward)
+    for t in texts:
         searcher.search(emb.embed_queries_device(t), K)
     torch.cuda.synchronize()
     fl.reset()
@@ -254,6 +257,7 @@ def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> 
     return {"model": f"{args.cpu_embed_preset} shape (random init), bf16, unpadded forward + K7", "batch": B,
             "batches": n_batches, "tokens_per_batch": round(flops["tokens_real"] / n_batches, 1),
             "embed_ms_per_batch": round(1000 * t_embed, 3), "embed_tflops": round(tflops, 1),
+            "embed_graphs": len(emb.graphed.graphs) if emb.graphed is not None else 0,
             "embed_frac_of_bf16_peak": round(tflops / MFMA_PEAK_TFLOPS, 4),
             "sequential": {"ms_per_batch": round(1000 * t_seq, 3), "qps": round(B / t_seq, 1)},
             "pipelined": {"ms_per_batch": round(1000 * t_pipe, 3), "qps": round(B / t_pipe, 1)},
@@ -509,6 +513,7 @@ def main():
     index.set_scan_timing(TIME_EVERY)
     wide0 = index.wide_launches()
     persist0 = index.persist_stats()["batches"]
+    fb0 = searcher.fallback_queries
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -526,6 +531,7 @@ def main():
     if pst["error"]:
         raise RuntimeError(f"persistent FILTER error {pst['error']}")
     persist = pst["batches"] - persist0 == args.steps  # every timed batch went through the persistent FILTER
+    fallback_queries = searcher.fallback_queries - fb0  # guard failures in the timed region (collect fallback)
     persist_timeline = None
     if persist:  # where the period goes (device stamps, us): medians over the timed batches
         tr = index.persist_trace(args.steps)
@@ -593,7 +599,7 @@ def main():
                      "frac_of_measured_read_ceiling": round(achieved / HBM_READ_CEILING_GBS, 4),
                      "read_ceiling_source": "profiles/r02_stream_ceiling.jsonl", "traffic": None,
                      "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg / passes, 4),
-                     "sample_pass_ms": round(sample_avg, 4)},
+                     "sample_pass_ms": round(sample_avg, 4), "guard_fallback_queries": fallback_queries},
         **({"persist_timeline": persist_timeline} if persist_timeline else {}),
         # the Q·Xᵀ contraction of the same launch on the MFMA pipe (bf16 dense peak, MI355X_MICROARCH.md)
         "mfma": {"achieved": round(mfma_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -195,3 +195,33 @@ def test_ingest_pauses_the_cyclic_gc_and_restores_it(tmp_path):
     seen.clear()
     run(GpuIngestor(store, GcProbe(), pause_gc=False).ingest(docs[:1]))
     assert seen and all(seen) and gc.isenabled()
+
+
+def test_pack_pad_sequence_changes_no_real_row():
+    """UnpaddedEncoder.pack(granule=64): one extra sequence of 1..64 pad tokens makes the token count a multiple of
+    64 (the shapes graph replays are captured for); every sequence attends only to itself, so the real tokens'
+    hidden states equal the unpadded pack's (fp32, CPU, SDPA per sequence), and `lengths` keeps the real ones."""
+    import numpy as np
+    import torch
+
+    from hiprag.rag.encoder import UnpaddedEncoder
+    from hiprag.rag.rocm_embedder import build_random_bert
+
+    model = build_random_bert("tiny", seed=3).eval()
+    enc = UnpaddedEncoder(model, use_varlen=False)
+    rng = np.random.default_rng(0)
+    lens = rng.integers(1, 20, 9)
+    ids = np.zeros((9, 20), np.int64)
+    mask = np.zeros((9, 20), np.int64)
+    for i, n in enumerate(lens):
+        ids[i, :n] = rng.integers(1, 30000, n)
+        mask[i, :n] = 1
+    with torch.inference_mode():
+        p0 = enc.pack(ids, mask, device="cpu")
+        p1 = enc.pack(ids, mask, device="cpu", granule=64)
+        h0, h1 = enc.forward_packed(p0), enc.forward_packed(p1)
+    n = int(lens.sum())
+    assert int(p1.cu_host[-1]) % 64 == 0 and 1 <= int(p1.cu_host[-1]) - n <= 64
+    np.testing.assert_array_equal(p1.lengths, lens)
+    np.testing.assert_array_equal(p1.cu_host[:-1], p0.cu_host)
+    torch.testing.assert_close(h1[:n], h0, rtol=1e-5, atol=1e-5)

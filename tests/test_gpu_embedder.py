@@ -205,3 +205,25 @@ def test_unpadded_embedder_matches_padded(dtype):
     z = a.encode_passages(texts)
     torch.testing.assert_close(z, x, rtol=0, atol=2e-2)
     assert float((z * x).sum(1).min()) > 0.9999
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_graph_replayed_forward_matches_eager(dtype):
+    """Query batches replayed from HIP graphs (encoder.GraphedForward: packed with a pad sequence up to a multiple
+    of 64 tokens, the flash kernel's maximum length rounded up) vs the eager packed forward of the same model:
+    every pooled embedding within half-precision rounding (the pad changes the GEMMs' row count, hence possibly
+    their kernels), cosine >= 0.9999; batches of one shape reuse one graph; a forward above max_tokens runs
+    eagerly."""
+    texts = [f"query {i}: " + " ".join(f"w{(i * 7 + j) % 211}" for j in range(1 + 5 * (i % 7))) for i in range(96)]
+    a = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=32, max_length=256, seed=8)
+    b = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=32, max_length=256, seed=8, cuda_graphs=False)
+    assert a.graphed is not None and b.graphed is None
+    for lo in (0, 32, 64, 0, 32):  # three shapes, each seen twice
+        x, y = a.encode_queries(texts[lo:lo + 32]), b.encode_queries(texts[lo:lo + 32])
+        torch.testing.assert_close(x, y, rtol=0, atol=2e-2)
+        assert float((x * y).sum(1).min()) > 0.9999
+    assert a.graphed.replays == 5 and 1 <= len(a.graphed.graphs) <= 3
+    a.graphed.max_tokens = 64  # every batch now exceeds it: eager
+    n = a.graphed.replays
+    torch.testing.assert_close(a.encode_queries(texts[:32]), b.encode_queries(texts[:32]), rtol=0, atol=2e-2)
+    assert a.graphed.replays == n

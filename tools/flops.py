@@ -16,7 +16,8 @@ from __future__ import annotations
 
 class EncoderFlops:
     """Counts the forwards of `model`; pass `unpadded` (the embedder's / reranker's UnpaddedEncoder, which
-    bypasses model.forward) to count those too -- there the executed FLOPs ARE the useful ones."""
+    bypasses model.forward) to count those too -- there the executed FLOPs are the useful ones, plus the pad
+    sequence a graph-replayed forward carries (encoder.GraphedForward)."""
 
     def __init__(self, model, unpadded=None):
         cfg = model.config
@@ -27,7 +28,7 @@ class EncoderFlops:
         self.unpadded = []  # host length arrays of unpadded forwards
         self.handle = model.register_forward_pre_hook(self._hook, with_kwargs=True)
         if unpadded is not None:
-            unpadded.observers.append(lambda B, T, lengths: self.unpadded.append(lengths.copy()))
+            unpadded.observers.append(lambda B, T, lengths, pad=0: self.unpadded.append((lengths.copy(), int(pad))))
 
     def _hook(self, module, args, kwargs):
         m = kwargs.get("attention_mask")
@@ -56,12 +57,12 @@ class EncoderFlops:
             ns += B
             ex += L * (B * T * dense + B * 4 * T * T * H)
             us += L * (float(lens.sum()) * dense + float((lens * lens).sum()) * 4 * H)
-        for lens in self.unpadded:  # real tokens only: executed = useful
+        for lens, pad in self.unpadded:  # real tokens (+ a graph replay's pad sequence: executed, not useful)
             n, sq = float(lens.sum()), float((lens.astype("float64") ** 2).sum())
             f = L * (n * dense + sq * 4 * H)
-            ex += f
+            ex += f + L * (pad * dense + pad * pad * 4 * H)
             us += f
-            tp += int(n)
+            tp += int(n) + pad
             tr += int(n)
             ns += len(lens)
         return {"executed": float(ex), "useful": float(us), "tokens_padded": tp, "tokens_real": tr, "sequences": ns}

@@ -423,7 +423,7 @@ static int group_search_impl(hr_index* g, const float* q_dev, int B, int k, cons
             HIP_TRY(hipMemcpyAsync(sh->cand.p, c.data(), c.size() * sizeof(Cand), hipMemcpyHostToDevice, sh->stream));
             HIP_TRY(hipMemcpyAsync(sh->bound.p, b.data(), b.size() * 8, hipMemcpyHostToDevice, sh->stream));
             HIP_TRY(hipStreamSynchronize(sh->stream));
-        } else if (int rc = index_shard_search(sh, qs, B, kc, mdev[(size_t)s], sh->cand.as<Cand>(),
+        } else if (int rc = index_shard_search(sh, qs, B, kc, hr_rank_for(k, kc, g->dim), mdev[(size_t)s], sh->cand.as<Cand>(),
                                                sh->bound.as<double>(), sh->stream)) {
             return rc;
         }
@@ -650,7 +650,9 @@ static int pipe_shard(hr_index* g, int s, GroupPipe::Slot& sl) {
             HIP_TRY(hipStreamWaitEvent(scan, ready, 0));  // the scan stream's prep reads them
         }
         if (!local && scan != sh->stream) HIP_TRY(hipStreamWaitEvent(scan, ready, 0));
-        if (int rc = index_shard_search_async(sh, qs, sl.B, sl.kc, cand, bound, scan, tail, ready)) return rc;
+        if (int rc = index_shard_search_async(sh, qs, sl.B, sl.kc, hr_rank_for(sl.k, sl.kc, g->dim), cand, bound, scan,
+                                              tail, ready))
+            return rc;
         if (!local) {
             HIP_TRY(hipMemcpyPeerAsync(sl.cand.as<Cand>() + (size_t)s * sl.B * sl.kc, g->device, cand, sh->device, cb,
                                        tail));

@@ -702,7 +702,7 @@ static double storage_u(const hr_index* h) {
 // st_tail: stream of select + rescore (the outputs are ready in its order).  st_tail != st:
 // pipelined (mode 0 only) -- ping-pong scratch set, the scan leaves tail_cus() CUs free and the
 // tail waits for this batch's FILTER by event; st_tail == st: one stream, the synchronous set.
-static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
+static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, const uint64_t* mask_dev, int64_t row_offset,
                        const double* kth_dev_host /* mode 1: host array of kth, B */, int mode, int cap_out,
                        Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail,
                        hipEvent_t q_ready = nullptr) {
@@ -938,6 +938,13 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
             a.n_units = (n_vis + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
             if (int rc = launch_scan(h, sc, early ? spare : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
+            // one row part and a strided sample: start the thresholds at the kj-th largest sampled group maximum
+            // (k_floor_kth; a sample of every tile -- small shards -- leaves the floor)
+            if (kj > 0 && np == 1 && a.sample_stride > 1) {
+                hipLaunchKernelGGL(k_floor_kth, dim3((Bp + 3) / 4), dim3(256), 0, sp, sc.mkeys.as<uint32_t>(),
+                                   sc.floor_q.as<float>(), Bp, kj);
+                HIP_TRY(hipGetLastError());
+            }
             ev.sampled = true;
             if (early) {  // the FILTER (scan stream) waits for the early prep + SAMPLE
                 if (timed) HIP_TRY(hipEventRecord(ev.e[2], sp));
@@ -1071,14 +1078,14 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, const uin
     return HR_OK;
 }
 
-static int shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, int64_t row_offset,
+static int shard_search(hr_index* h, const float* q_dev, int B, int kc, int kj, const uint64_t* mask_dev, int64_t row_offset,
                         Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail,
                         hipEvent_t q_ready = nullptr) {
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     for (int b0 = 0; b0 < B; b0 += pl.Bp) {
         const int bc = std::min(pl.Bp, B - b0);
-        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, kc, mask_dev, row_offset, nullptr, 0, 0,
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, kc, kj, mask_dev, row_offset, nullptr, 0, 0,
                                  cand_out + (int64_t)b0 * kc, bound_out + b0, st, st_tail, q_ready))
             return rc;
     }
@@ -1119,7 +1126,8 @@ static int search_main(hr_index* h, const float* q_dev, int B, int k, const uint
     HIP_TRY(h->bound.ensure((size_t)B * 8));
     HIP_TRY(h->kth.ensure((size_t)B * 8));
     HIP_TRY(h->fail.ensure((size_t)B * 4));
-    if (int rc = shard_search(h, q_dev, B, kc, mask_dev, 0, h->cand.as<Cand>(), h->bound.as<double>(), st, st))
+    if (int rc = shard_search(h, q_dev, B, kc, hr_rank_for(k, kc, h->dim), mask_dev, 0, h->cand.as<Cand>(),
+                              h->bound.as<double>(), st, st))
         return rc;
     return launch_merge(h->device, h->cand.as<Cand>(), h->bound.as<double>(), 1, B, kc, k, s_out, r_out,
                         h->kth.as<double>(), h->fail.as<int32_t>(), st);
@@ -1149,7 +1157,7 @@ static int search_fallback(hr_index* h, const float* q_dev, int k, const uint64_
     if (int rc = make_plan(h, nf, &pl)) return rc;
     for (int b0 = 0; b0 < nf; b0 += pl.Bp) {
         const int bc = std::min(pl.Bp, nf - b0);
-        if (int rc = shard_chunk(h, h->fb_q.as<float>() + (int64_t)b0 * h->dim, bc, kc2, mask_dev, 0, &kf[(size_t)b0], 1,
+        if (int rc = shard_chunk(h, h->fb_q.as<float>() + (int64_t)b0 * h->dim, bc, kc2, 0, mask_dev, 0, &kf[(size_t)b0], 1,
                                  kc2, h->fb_cand.as<Cand>() + (int64_t)b0 * kc2, h->fb_bound.as<double>() + b0, st, st))
             return rc;
     }
@@ -1438,7 +1446,8 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     HIP_TRY(hipMemcpyAsync(sl.q.p, sl.pin, qb, hipMemcpyHostToDevice, h->acopy));
     HIP_TRY(hipEventRecord(sl.q_ready, h->acopy));
     if (hipEventQuery(sl.q_ready) != hipSuccess) HIP_TRY(hipStreamWaitEvent(h->stream, sl.q_ready, 0));
-    if (int rc = shard_search(h, sl.q.as<float>(), B, kc, nullptr, 0, sl.cand.as<Cand>(), sl.bound.as<double>(),
+    if (int rc = shard_search(h, sl.q.as<float>(), B, kc, hr_rank_for(k, kc, h->dim), nullptr, 0, sl.cand.as<Cand>(),
+                              sl.bound.as<double>(),
                               h->stream, h->atail, sl.q_ready))
         return rc;
     if (int rc = launch_merge(h->device, sl.cand.as<Cand>(), sl.bound.as<double>(), 1, B, kc, k, sl.s.as<float>(),
@@ -1636,14 +1645,14 @@ extern "C" int hr_index_search(hr_index* h, const float* q, int B, int k, const 
 }
 
 // one shard's exact candidates (group handles, hr_group.hip)
-int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
+int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, int kj, const uint64_t* mask_dev, Cand* cand_out,
                        double* bound_out, hipStream_t st) {
-    return shard_search(h, q_dev, B, kc, mask_dev, 0, cand_out, bound_out, st, st);
+    return shard_search(h, q_dev, B, kc, kj, mask_dev, 0, cand_out, bound_out, st, st);
 }
 
-int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, Cand* cand_out, double* bound_out,
+int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, int kj, Cand* cand_out, double* bound_out,
                              hipStream_t st, hipStream_t st_tail, hipEvent_t q_ready) {
-    return shard_search(h, q_dev, B, kc, nullptr, 0, cand_out, bound_out, st, st_tail, q_ready);
+    return shard_search(h, q_dev, B, kc, kj, nullptr, 0, cand_out, bound_out, st, st_tail, q_ready);
 }
 
 int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,
@@ -1652,7 +1661,7 @@ int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kt
     if (int rc = make_plan(h, B, &pl)) return rc;
     for (int b0 = 0; b0 < B; b0 += pl.Bp) {  // one collect scan per chunk of queries
         const int bc = std::min(pl.Bp, B - b0);
-        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, mask_dev, 0, kth_host + b0, 1, cap,
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, 0, mask_dev, 0, kth_host + b0, 1, cap,
                                  cand_out + (int64_t)b0 * cap, bound_out + b0, st, st))
             return rc;
     }
@@ -1670,7 +1679,8 @@ extern "C" int hr_index_search_shard(hr_index* h, const float* q_dev, int B, int
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch's default)
-    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev, st, st);
+    return shard_search(h, q_dev, B, kc, hr_rank_for(k, kc, h->dim), row_mask_dev, row_offset, (Cand*)cand_out_dev,
+                        bound_out_dev, st, st);
 }
 
 extern "C" int hr_index_search_shard_async_ev(hr_index* h, const float* q_dev, int B, int k, int kc,
@@ -1684,8 +1694,8 @@ extern "C" int hr_index_search_shard_async_ev(hr_index* h, const float* q_dev, i
     if (int rc = set_device(h)) return rc;
     if (int rc = validate_search(h, B, k)) return rc;
     if (kc < k || kc > HR_MAX_KC) return set_err(HR_E_INVALID, "kc must be in [k, HR_MAX_KC]");
-    return shard_search(h, q_dev, B, kc, row_mask_dev, row_offset, (Cand*)cand_out_dev, bound_out_dev,
-                        (hipStream_t)scan_stream, (hipStream_t)tail_stream, (hipEvent_t)q_ready_event);
+    return shard_search(h, q_dev, B, kc, hr_rank_for(k, kc, h->dim), row_mask_dev, row_offset, (Cand*)cand_out_dev,
+                        bound_out_dev, (hipStream_t)scan_stream, (hipStream_t)tail_stream, (hipEvent_t)q_ready_event);
 }
 
 extern "C" int hr_index_search_shard_async(hr_index* h, const float* q_dev, int B, int k, int kc,
@@ -1713,7 +1723,7 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
     if (int rc = make_plan(h, B, &pl)) return rc;
     for (int b0 = 0; b0 < B; b0 += pl.Bp) {  // one collect scan per chunk of queries
         const int bc = std::min(pl.Bp, B - b0);
-        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, row_mask_dev, row_offset, &kth[(size_t)b0], 1,
+        if (int rc = shard_chunk(h, q_dev + (int64_t)b0 * h->dim, bc, cap, 0, row_mask_dev, row_offset, &kth[(size_t)b0], 1,
                                  cap, out + (int64_t)b0 * cap, bound_out_dev + b0, st, st))
             return rc;
     }
@@ -2209,6 +2219,11 @@ extern "C" int hr_abi_version(void) { return 2; }
 
 extern "C" int hr_kc_for_k(int k) { return hr_kc_for_k_dim(k, 0); }
 
+static int kc_margin(int k, int dim) {
+    const int wide = (dim + 63) / 64 * 64 >= 2048 ? 2 : 1;
+    return std::max(wide == 2 ? 20 : 16, wide * k / 2);  // (20: k = 16 lacked margin at 2304 dims)
+}
+
 extern "C" int hr_kc_for_k_dim(int k, int dim) {
     // margin beyond k: max(16, k/2), for every k; max(20, k) from 2048 dims on (Youtu-Embedding's
     // 2048 / 2304): the guard's window widens against the score spread (sigma ~ 1/sqrt(D)), and at
@@ -2217,7 +2232,19 @@ extern "C" int hr_kc_for_k_dim(int k, int dim) {
     // collect fallback (5.3 ms/batch at 6.25M rows), k/2 sends almost none (2.8 ms).  kc = 32 for every
     // k <= 32 left no margin at k = 32 (every query of a 10M batch failed the guard: 7.2 vs 3.3 ms) and
     // HR_MAX_KC = 160 only 32 rows at k = 128 (83 % failures, 8.2 ms; tools/diag_k.py)
-    const int wide = (dim + 63) / 64 * 64 >= 2048 ? 2 : 1;
-    const int margin = std::max(wide == 2 ? 20 : 16, wide * k / 2);  // (20: k = 16 lacked margin at 2304 dims)
-    return std::min(HR_MAX_KC, (k + margin + 31) / 32 * 32);
+    return std::min(HR_MAX_KC, (k + kc_margin(k, dim) + 31) / 32 * 32);
+}
+
+// The order statistic of a query's 32 group maxima that starts the FILTER's threshold and sets k_select's
+// (ScanArgs::kj): with one row part (kc <= 32) at least kc rows must lie at or above the threshold, and kc is
+// k + margin rounded UP to 32 -- the smallest group maximum, the 32nd largest.  The (k + margin)-th largest
+// leaves the guard the margin it was sized for and starts higher: the rows above the smallest of 32 group maxima
+// number ~32 H(32) = 130 of the rows seen, above the 26th largest (k = 10) ~32 ln(32 / 6) = 54 -- fewer candidates
+// appended while the SAMPLE's keys are the threshold (the first tiles of every wave).  Exactness is unchanged:
+// every key is the score of a row of its group, so j groups hold a row at or above the j-th largest key, and that
+// key only grows (exactness guard).  0: the smallest (row parts, or k + margin >= 32).
+int hr_rank_for(int k, int kc, int dim) {
+    if (kc > 32) return 0;
+    const int j = std::min(kc, k + kc_margin(k, dim));
+    return j < 32 ? j : 0;
 }

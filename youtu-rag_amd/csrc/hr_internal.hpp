@@ -248,14 +248,16 @@ int index_add_synthetic(hr_index* h, uint64_t seed, int64_t gen_base, int64_t n)
 int index_remove_local(hr_index* h, const int64_t* rows, int64_t n);
 int index_get_rows(hr_index* h, const int64_t* rows, int64_t n, float* out);
 int index_update_row_norms(hr_index* h, int64_t r0, int64_t n);
+// the group-max order statistic of the FILTER's starting threshold and k_select (ScanArgs::kj; hr_index.hip)
+int hr_rank_for(int k, int kc, int dim);
 int index_finish_load(hr_index* h);
 // one batch of queries (device, on this shard's device) through the exact search of one shard:
 // candidates (global rows) + bounds into cand_out / bound_out on `st`
-int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, const uint64_t* mask_dev, Cand* cand_out,
+int index_shard_search(hr_index* h, const float* q_dev, int B, int kc, int kj, const uint64_t* mask_dev, Cand* cand_out,
                        double* bound_out, hipStream_t st);
 // the same, pipelined: scan on st, select + rescore on st_tail (outputs ready in st_tail order), the
 // queries ready once q_ready completes (see hr_index_search_shard_async_ev)
-int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, Cand* cand_out, double* bound_out,
+int index_shard_search_async(hr_index* h, const float* q_dev, int B, int kc, int kj, Cand* cand_out, double* bound_out,
                              hipStream_t st, hipStream_t st_tail, hipEvent_t q_ready);
 int index_shard_collect(hr_index* h, const float* q_dev, int B, const double* kth_host, int cap,
                         const uint64_t* mask_dev, Cand* cand_out, double* bound_out, hipStream_t st);

@@ -399,6 +399,44 @@ struct XFrag<MT, F32, NT> {
 // query index held by accumulator register i of block qb in this lane's half
 __device__ inline int acc_query(int qb, int i, int half) { return qb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half; }
 
+// Cross-lane reductions without LDS round trips (a __shfl_xor is a ds_bpermute, and a 5-step reduction waited for
+// each: 40 serialised LDS round trips per refresh): DPP within each row of 16 lanes (xor 1, xor 2, half-mirror,
+// mirror), then a ds_swizzle (xor 16 within 32 lanes) or four readlanes across the rows
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+// min over the 32 lanes of each half-wave, in every lane
+__device__ __forceinline__ float half_min32(float f) {
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 1,0,3,2
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 2,3,0,1
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, f))));  // row_half_mirror
+    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x140>(__builtin_bit_cast(uint32_t, f))));  // row_mirror
+    return fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, f), 0x401F)));
+}
+// OR over the wave's 64 lanes, wave-uniform
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= dpp_u32<0xB1>(x);
+    x |= dpp_u32<0x4E>(x);
+    x |= dpp_u32<0x141>(x);
+    x |= dpp_u32<0x140>(x);
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) | __builtin_amdgcn_readlane((int)x, 16) |
+                      __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
+}
+// the j-th largest of the 32 values of each half-wave (1 <= j <= 32; j wave-uniform), in every lane: the smallest
+// is dropped 32 - j times -- one lane per round even among equal values (the lowest such lane of the half), so
+// exactly 32 - j values go -- then the minimum of the rest
+__device__ __forceinline__ float half_kth_largest(float f, int j) {
+    const int lane = __lane_id();
+    for (int r = 0; r < 32 - j; ++r) {
+        const float m = half_min32(f);
+        const uint64_t b = __ballot(f == m);
+        const uint32_t bh = lane >= 32 ? (uint32_t)(b >> 32) : (uint32_t)b;
+        if ((lane & 31) == __builtin_ctz(bh)) f = __builtin_inff();
+    }
+    return half_min32(f);
+}
+
 // MODE: SCAN_SAMPLE (group maxima only), SCAN_FILTER (threshold + private per-wave
 // candidate regions, no atomics on the append path), SCAN_COLLECT (floor-only threshold,
 // shared per-query buffer with atomic slot reservation; the exact fallback)
@@ -618,6 +656,8 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
         for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
+                // (a ds_bpermute chain: the DPP + ds_swizzle form of half_min32 measured 0.5 % slower at 10M rows,
+                // 1.1 % at k = 100, 0.6 % faster at 1.25M -- same box, profiles/r04_kscan_dpp_refresh_ab.jsonl)
                 float f = key2f(key[qb][i]);
 #pragma unroll
                 for (int off = 16; off >= 1; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
@@ -955,6 +995,22 @@ __device__ inline void block_bitonic_desc(uint64_t* s, int n) {  // n power of t
             __syncthreads();
         }
     }
+}
+
+// After the SAMPLE, one row part: raise each query's floor to the kj-th largest of its 32 group maxima (one wave per
+// query).  The FILTER takes th = max(floor, min over the groups) and k_select thr = max(floor, min over the final
+// groups), so this starts every wave's threshold at the kj-th largest sampled group maximum instead of the smallest
+// (hr_rank_for: kj = k + margin < 32).  Exact: each key is the score of a row of its group, so kj rows lie at or
+// above the floor; with thr = max(floor, min_final) every row at or above thr is appended (th never exceeds thr),
+// and at least kj of them (the floor's rows, or one row per group) are candidates -- the guard's premise.
+static __global__ __attribute__((unused)) __launch_bounds__(256) void k_floor_kth(const uint32_t* __restrict__ mkeys,
+                                                                                   float* __restrict__ floor_q, int B,
+                                                                                   int kj) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= B) return;  // (wave-uniform)
+    const uint32_t k = mkeys[(int64_t)q * 32 + (threadIdx.x & 31)];
+    const float t = half_kth_largest(key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF), kj);
+    if ((threadIdx.x & 63) == 0) floor_q[q] = fmaxf(floor_q[q], t);
 }
 
 constexpr int kRankMax = 1024;  // candidate sets up to this size are ranked by counting, larger ones sorted

@@ -34,30 +34,6 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Cross-lane reductions without LDS round trips (a __shfl_xor is a ds_bpermute, and a 5-step reduction waited for
-// each: 40 serialised LDS round trips per refresh): DPP within each row of 16 lanes (xor 1, xor 2, half-mirror,
-// mirror), then a ds_swizzle (xor 16 within 32 lanes) or four readlanes across the rows
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
-}
-// min over the 32 lanes of each half-wave, in every lane
-__device__ __forceinline__ float half_min32(float f) {
-    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 1,0,3,2
-    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, f))));   // quad_perm 2,3,0,1
-    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, f))));  // row_half_mirror
-    f = fminf(f, __builtin_bit_cast(float, dpp_u32<0x140>(__builtin_bit_cast(uint32_t, f))));  // row_mirror
-    return fminf(f, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, f), 0x401F)));
-}
-// OR over the wave's 64 lanes, wave-uniform
-__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
-    x |= dpp_u32<0xB1>(x);
-    x |= dpp_u32<0x4E>(x);
-    x |= dpp_u32<0x141>(x);
-    x |= dpp_u32<0x140>(x);
-    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) | __builtin_amdgcn_readlane((int)x, 16) |
-                      __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
-}
 constexpr int kWN = 8;       // k-steps per query window
 // eight-wave form: depth windows kept resident in LDS for the whole launch (the rest stream): 2 x 32 KiB
 constexpr int kResidentWindows = 2;

@@ -108,6 +108,7 @@ class ShardedSearch:
         if force_collective and not dist.is_initialized():
             raise ValueError("force_collective needs an initialised process group")
         self.collective = self.G > 1 or bool(force_collective)  # the exchange goes through the process group
+        self.fallback_queries = 0  # queries whose guard failed (collect fallback), cumulative
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
         # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
         self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k, int(getattr(index, "dim", 0)))
@@ -236,6 +237,7 @@ class ShardedSearch:
             slot.event.synchronize()
         failed = self._failed_queries(slot, B)
         if len(failed):
+            self.fallback_queries += len(failed)
             self._fallback(q, k, failed, slot.kth[:B], s_out, r_out, mask_ptr)
         return s_out, r_out
 

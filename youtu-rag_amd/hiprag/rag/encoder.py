@@ -98,11 +98,13 @@ class UnpaddedEncoder:
             pos += int(self.emb.padding_idx) + 1
         return pos
 
-    def pack(self, input_ids, attention_mask, token_type_ids=None, device=None):
+    def pack(self, input_ids, attention_mask, token_type_ids=None, device=None, granule: int = 0):
         """Host-side packing of right-padded tokenizer batches (host tensors / arrays (B, T), or lists of
         them -- several batches become one packed batch): the real tokens' ids, token types and
         positions plus the cumulative lengths, uploaded with ONE pinned asynchronous copy.  Returns the
-        Packed batch forward_packed() takes."""
+        Packed batch forward_packed() takes.  granule > 0 (graph replay, GraphedForward): one more sequence of
+        1..granule pad tokens (id 0) makes the token count a multiple of granule; its rows are computed and
+        ignored (every sequence attends only to itself), and `lengths` keeps the real sequences only."""
         torch = self.torch
         many = isinstance(input_ids, (list, tuple))
         parts = zip(input_ids, attention_mask, token_type_ids if token_type_ids is not None else [None] * len(input_ids)) \
@@ -118,6 +120,13 @@ class UnpaddedEncoder:
             types_l.append(np.asarray(types)[keep] if types is not None else None)
             lens_l.append(lengths)
         lengths = np.concatenate(lens_l) if lens_l else np.zeros(0, np.int64)
+        real = lengths
+        if granule > 0:
+            n_real = int(lengths.sum())
+            pad = granule - n_real % granule  # 1..granule: the pad sequence is never empty
+            ids_l.append(np.zeros(pad, np.int64))
+            types_l.append(None)
+            lengths = np.concatenate([lengths, [pad]]).astype(np.int64)
         B = len(lengths)
         cu = np.zeros(B + 1, np.int64)
         cu[1:] = np.cumsum(lengths)
@@ -135,14 +144,14 @@ class UnpaddedEncoder:
         if dev.type == "cuda":
             t = t.pin_memory()
         t = t.to(dev, non_blocking=dev.type == "cuda")
-        return Packed(t[:n], t[n:2 * n], t[2 * n:3 * n], t[3 * n:].to(torch.int32), cu, lengths,
+        return Packed(t[:n], t[n:2 * n], t[2 * n:3 * n], t[3 * n:].to(torch.int32), cu, real,
                       int(lengths.max()) if B else 0)
 
     def forward_packed(self, pk: "Packed"):
         """Last hidden state of the packed real tokens, (N, H) (row cu[b] + t is token t of sequence b)."""
         n = int(pk.cu_host[-1])
-        for f in self.observers:
-            f(len(pk.lengths), pk.max_len, pk.lengths)
+        for f in self.observers:  # (the pad sequence of a graph-shaped pack: executed, not real)
+            f(len(pk.lengths), pk.max_len, pk.lengths, n - int(pk.lengths.sum()))
         x = self.emb(input_ids=pk.ids[None], token_type_ids=pk.types[None], position_ids=pk.pos[None])[0]
         return self._layers(x, pk.cu, pk.cu_host, pk.max_len, n)
 
@@ -185,6 +194,78 @@ class UnpaddedEncoder:
         seq = h.new_zeros(B * T, h.shape[-1])
         seq.index_copy_(0, idx, h)
         return seq.view(B, T, -1)
+
+
+class GraphedForward:
+    """forward_packed() replayed from HIP graphs: a query batch's forward is ~300 small kernels (24 layers at
+    bge-large shape) whose host dispatch, not the GPU, bounds it (64 queries, ~900 tokens: 4.2 ms of host time
+    for 4.0 ms of GPU time by events, 2.06 ms replayed; profiles/r04_embed_probe_bge-large_b64.json).  One graph
+    per (sequences, tokens, max length) shape: batches are packed with a pad sequence up to a multiple of
+    `granule` tokens (UnpaddedEncoder.pack) and the flash kernel's maximum length is rounded up to a power of two,
+    so a stream of query batches falls into a few shapes.  Each graph is captured once (two warm-up forwards on a
+    side stream first) into one shared memory pool; a call copies the packed ids / types / positions /
+    offsets into the graph's static inputs on the current stream and replays it there.  The returned (N, H)
+    hidden state is the graph's static output: valid until the next call on that stream.  Forwards above
+    max_tokens run eagerly."""
+
+    def __init__(self, enc: "UnpaddedEncoder", granule: int = 64, max_tokens: int = 8192, max_graphs: int = 64):
+        self.enc = enc
+        self.torch = enc.torch
+        self.granule = int(granule)
+        self.max_tokens = int(max_tokens)
+        self.max_graphs = int(max_graphs)
+        self.graphs: dict = {}
+        self.pool = None
+        self.replays = 0
+
+    @staticmethod
+    def _bucket_len(m: int) -> int:
+        b = 32
+        while b < m:
+            b <<= 1
+        return b
+
+    def __call__(self, pk: "Packed"):
+        n = int(pk.cu_host[-1])
+        ml = self._bucket_len(pk.max_len)
+        key = (len(pk.cu_host) - 1, n, ml)
+        ent = self.graphs.get(key)
+        if ent is None:
+            if n > self.max_tokens or not pk.ids.is_cuda or len(self.graphs) >= self.max_graphs:
+                return self.enc.forward_packed(pk)
+            ent = self.graphs[key] = self._capture(pk, ml)
+        for f in self.enc.observers:  # (a replay runs no Python forward: report the shape here)
+            f(len(pk.lengths), pk.max_len, pk.lengths, n - int(pk.lengths.sum()))
+        ids, types, pos, cu, g, out = ent
+        ids.copy_(pk.ids, non_blocking=True)
+        types.copy_(pk.types, non_blocking=True)
+        pos.copy_(pk.pos, non_blocking=True)
+        cu.copy_(pk.cu, non_blocking=True)
+        g.replay()
+        self.replays += 1
+        return out
+
+    def _capture(self, pk: "Packed", ml: int):
+        torch = self.torch
+        dev = pk.ids.device
+        ids, types, pos, cu = (x.clone() for x in (pk.ids, pk.types, pk.pos, pk.cu))
+        spk = Packed(ids, types, pos, cu, pk.cu_host, pk.lengths, ml)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        obs, self.enc.observers = self.enc.observers, []  # (warm-up and capture are not forwards of a batch)
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.enc.forward_packed(spk)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self.enc.forward_packed(spk)
+        finally:
+            self.enc.observers = obs
+        if self.pool is None:
+            self.pool = g.pool()
+        return ids, types, pos, cu, g, out
 
 
 class Packed(NamedTuple):

@@ -188,7 +188,7 @@ class TorchRocmEmbedder(BaseEmbedder):
                  batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
                  trust_remote_code: bool = False, fused_layernorm: bool | None = None, unpadded: bool | None = None,
-                 forward_tokens: int | None = None, **_ignored):
+                 forward_tokens: int | None = None, cuda_graphs: bool | None = None, **_ignored):
         import torch
 
         self.torch = torch
@@ -225,6 +225,11 @@ class TorchRocmEmbedder(BaseEmbedder):
             unpadded = _enc._ENV and self.device.type == "cuda" and self.dtype_name != "float32"
         self.unpadded = _enc.UnpaddedEncoder(self.model) if (unpadded and _enc.UnpaddedEncoder.supported(self.model)) \
             else None
+        # packed forwards up to 8192 tokens (query batches) replayed from HIP graphs (encoder.GraphedForward): their
+        # ~300 kernel launches per forward, not the GPU, bound them; cuda_graphs=False runs them eagerly
+        if cuda_graphs is None:
+            cuda_graphs = self.unpadded is not None
+        self.graphed = _enc.GraphedForward(self.unpadded) if (cuda_graphs and self.unpadded is not None) else None
         max_pos = getattr(getattr(model, "config", None), "max_position_embeddings", None)
         self.max_length = min(int(max_length), int(max_pos)) if max_pos else int(max_length)
         self.batch_size = int(batch_size)
@@ -282,9 +287,13 @@ class TorchRocmEmbedder(BaseEmbedder):
         """Unpadded forward of one or more tokenizer batches as ONE packed batch -> (sum B, H) float32."""
         torch = self.torch
         with torch.inference_mode():
+            gf = self.graphed
+            ntok = sum(int(b["attention_mask"].sum()) for b in batches)
+            if gf is not None and ntok + gf.granule > gf.max_tokens:
+                gf = None
             pk = self.unpadded.pack([b["input_ids"] for b in batches], [b["attention_mask"] for b in batches],
-                                    [b.get("token_type_ids") for b in batches])
-            hidden = self.unpadded.forward_packed(pk)
+                                    [b.get("token_type_ids") for b in batches], granule=gf.granule if gf else 0)
+            hidden = gf(pk) if gf is not None else self.unpadded.forward_packed(pk)
             if hidden.dtype != getattr(torch, self.dtype_name):
                 hidden = hidden.to(getattr(torch, self.dtype_name))
             hidden = hidden.contiguous()

@@ -78,7 +78,8 @@ def main(port: int, q_path: str, out_path: str, rows: int, dim: int) -> None:
     ff.search(qd[1], k, s_out=s[5], r_out=r[5])
     torch.cuda.synchronize()
     np.savez(out_path, s=s.cpu().numpy(), r=r.cpu().numpy(), backend=np.array(backend),
-             ag=np.array(counts["all_gather_into_tensor"]), bc=np.array(counts["broadcast"]))
+             ag=np.array(counts["all_gather_into_tensor"]), bc=np.array(counts["broadcast"]),
+             persist=np.array(idx.persist_stats()["batches"]))
     dist.destroy_process_group()
 
 

@@ -6,7 +6,8 @@ test uses gloo.  This test executes the production branch itself: a world-size-1
 force_collective=True)`` so the packed candidate records go through ``all_gather_into_tensor`` on the
 tail stream, a src_rank batch through ``broadcast`` on the scan stream, and a forced collect fallback
 through the second all-gather -- at C3's size (10M x 1024 bf16, 64-query batches, k = 10), every batch
-identical to the CPU oracle over all 10M rows.  Anchor: the one-process-many-collections deployment the
+identical to the CPU oracle over all 10M rows -- and at 5M rows (the per-GPU shard of a 10M corpus at G = 2),
+where the pipelined batches run through the persistent FILTER with the all-gather behind its tail wait.  Anchor: the one-process-many-collections deployment the
 exchange serves, /root/reference/utu/rag/rag_tools/base_toolkit.py:79-91.
 """
 import os
@@ -23,7 +24,7 @@ from oracle import ref_numpy as R
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-N, D, B, K = 10_000_000, 1024, 64, 10
+D, B, K = 1024, 64, 10
 
 
 def _free_port():
@@ -33,7 +34,8 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_rccl_world1_exchange_c3_vs_oracle(tmp_path):
+@pytest.mark.parametrize("N", [10_000_000, 5_000_000])
+def test_rccl_world1_exchange_c3_vs_oracle(tmp_path, N):
     from hiprag import synth
 
     planted, _ = synth.planted_queries(0, N, D, B, qseed=4343)
@@ -51,6 +53,8 @@ def test_rccl_world1_exchange_c3_vs_oracle(tmp_path):
     # 4 pipelined batches + 1 broadcast batch: one all-gather each; the forced fallback batch: two (the
     # merge's gather, then the collect records'); one broadcast
     assert int(got["ag"]) == 7 and int(got["bc"]) == 1, (int(got["ag"]), int(got["bc"]))
+    if N == 5_000_000:  # the persistent FILTER's range (hr_index_set_persist mode 1): the 4 pipelined batches
+        assert int(got["persist"]) >= 4, int(got["persist"])
     s_ref, r_ref = oracle.c_search_synthetic(0, 0, N, D, "bf16", "cosine",
                                              R.process_queries(q.reshape(2 * B, D), "cosine"), K)
     s_ref = s_ref.astype(np.float32).reshape(2, B, K)

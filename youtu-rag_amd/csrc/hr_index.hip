@@ -912,6 +912,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     // ... except with 4+ row parts (k >= 75: a refresh then also reads the other parts' maxima), where the
     // early loads pay at 10M too: k = 100 3.217 -> 3.190 ms (profiles/r03_rowpart_knobs_10M.log)
     a.early_refresh = (dual || persist || np >= 4) ? 1 : 0;
+    // staggered refreshes pay on shards beyond the dual-FILTER range (scan_body: roff)
+    a.stagger = n_tiles > 160 * 1024 ? 1 : 0;
     const bool groups = mode == 0;
     a.use_groups = groups ? 1 : 0;
     a.tile_list = tl_ptr;

@@ -282,6 +282,7 @@ struct ScanArgs {
     // reads np windows of consecutive tiles.  0: parts keep contiguous per-wave ranges (tile lists)
     int teams;
     int dyn_pct;             // dynamic-tail percentage the host used (teams recompute their split)
+    int stagger;             // FILTER: refreshes staggered over a workgroup's waves (see roff in scan_body)
 };
 
 
@@ -713,6 +714,11 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
     // (LEAN: never -- the 32 keys held across the k-loop cost the registers the persistent loop needs)
     const bool early_refresh = !LEAN && a.early_refresh != 0;
     int64_t u = u0, u_end = u1, pend = -1, done = 0;
+    // a.stagger: refreshes staggered over the workgroup's waves (wave v refreshes after tiles with (done + v) % RT
+    // == 0) -- each tile some waves publish and read fresh keys instead of all of them every RT-th tile.  Large
+    // shards only: 10M rows 2.988-2.993 -> 2.958-2.961 ms/step, k = 100 -0.3 %; 1.25M +0.7 %, 1M x 768 +1.2 %
+    // (profiles/r04_refresh_stagger_ab.jsonl, same box)
+    const int roff = a.stagger ? __builtin_amdgcn_readfirstlane((tid >> 6) % a.refresh_every) : 0;
     uint32_t graw = 0;
     bool issued = false;  // this run's grab is in flight (exactly one grab per run)
     if (dyn && u0 >= u1) {  // no static units (tiny launches): start in the pool
@@ -747,7 +753,8 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
             part_end = (part + 1) * a.part_tiles;
         }
         // a refresh applied in this tile's epilogue: its loads go out now (see refresh_load)
-        const bool rdue = MODE == SCAN_FILTER && a.use_groups && early_refresh && ((done + 1) % a.refresh_every) == 0;
+        const bool rdue = MODE == SCAN_FILTER && a.use_groups && early_refresh &&
+                          ((done + 1 + roff) % a.refresh_every) == 0;
         if (rdue) {
             refresh_load(rkey);
             asm volatile("" ::: "memory");  // keeps the loads here (the compiler would sink them to their use)
@@ -852,7 +859,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
                 }
         }
         ++done;
-        if (MODE == SCAN_FILTER && (done % a.refresh_every) == 0) {
+        if (MODE == SCAN_FILTER && ((done + roff) % a.refresh_every) == 0) {
             if (rdue) refresh_apply(rkey, true, false);
             else refresh(true);
         }

@@ -712,22 +712,27 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     const bool piped = st_tail != st && mode == 0;
     if (!piped) st_tail = st;
     const int64_t n_tiles = (h->n + 31) / 32;
-    // SAMPLE size for n units: n/128 tiles, at least 2048 (A/B: 128 beats 64 by 0.7 % at 10M).  (Capping it at a
-    // fraction of a small shard -- at 100k rows the fixed 2048 read 65 % of the shard again -- gained nothing:
-    // 0.11-0.13 ms/step either way, the per-step host submission bounds such small collections.)
+    // SAMPLE size for n units: n/128 tiles (A/B: 128 beats 64 by 0.7 % at 10M), at least 2048 -- or 1024 on shards
+    // up to 80k tiles (2.56M rows): with the kj-th largest starting floor (k_floor_kth) 1024 sampled tiles start
+    // the FILTER as well there and the early-SAMPLE chain is shorter -- 1M x 768 0.289 -> 0.284 ms/step, 2.5M
+    // 0.804 -> 0.800, 1.25M unchanged, 3072 slower; at 5M rows 1024 cost 0.5 % (profiles/
+    // r04_small_shard_sample_cadence_ab.jsonl, r04_sample_floor_1024_ab.jsonl).
+    // (Capping it at a fraction of a small shard -- at 100k rows a fixed 2048 read 65 % of the shard again --
+    // gained nothing: 0.11-0.13 ms/step either way, the per-step host submission bounds such small collections.)
     auto sample_target = [&](int64_t n) {
         // a shard sharing its GPU with other shards of a group samples 512 tiles: the co-located shards'
         // SAMPLEs add up (8 x 1.25M rows on one GPU: 3.387 / 3.308 / 3.297 ms per batch at 2048 / 1024 /
         // 512, profiles/r03_group_scan_streams.log)
-        const int64_t smin = h->shared_dev ? 512 : 2048;
+        const int64_t smin = h->shared_dev ? 512 : (n <= 80 * 1024 ? 1024 : 2048);
         return std::max<int64_t>(smin, n / 128);
     };
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that
     // FILTER still runs; this batch's FILTER then waits for them by event.  Only when the shard is
-    // large enough (>= 8 sample sizes, 524k rows) for the narrow SAMPLE to finish inside the previous
-    // FILTER (A/B at 16: 1M x 768 0.355 vs 0.325 ms/step; at 4, 300k-row shards lose 10 %).
-    constexpr int early_min = 8;
+    // large enough (>= 16384 tiles, 524k rows: 8 of round 3's 2048-tile samples) for the narrow SAMPLE to finish
+    // inside the previous FILTER (A/B at 16 samples: 1M x 768 0.355 vs 0.325 ms/step; at 4, 300k-row shards lose
+    // 10 %); kept in tiles when the sample floor went to 1024
+    constexpr int64_t early_min_tiles = 16384;
     // Not for a group shard sharing its GPU with other shards (dev_ids repeated): their early SAMPLEs on
     // high-priority streams then cut into each other's FILTERs -- 8 shards of 1.25M rows on one GPU
     // 4.87 ms/batch with, 3.76 without (profiles/r03_group_shared_gpu.log)
@@ -739,7 +744,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     const bool wide_likely = mode == 0 && wide_plan(h, pl, (kc + 31) / 32, h->tl_n >= 0);
     const int spare = wide_likely ? 0 : tail_cus(h);
     const bool early = piped && q_ready && h->tl_n < 0 && spare > 0 && !h->shared_dev &&
-                       n_tiles >= early_min * sample_target(n_tiles);
+                       n_tiles >= std::max<int64_t>(early_min_tiles, 8 * sample_target(n_tiles));
     // the persistent FILTER (hr_persist.hip) takes this batch: its FILTER runs in the instance streaming the
     // batches one after another; prep, SAMPLE, select and rescore are this function's as for any pipelined batch
     const bool persist = mode == 0 && !wide_likely && persist_wanted(h, pl, (kc + 31) / 32, early, mask_dev, n_tiles);
@@ -940,11 +945,15 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
             a.n_units = (n_vis + a.sample_stride - 1) / a.sample_stride;
             if (timed) HIP_TRY(hipEventRecord(ev.e[0], sp));
             if (int rc = launch_scan(h, sc, early ? spare : cus, pl, a, SCAN_SAMPLE, sp)) return rc;
-            // one row part and a strided sample: start the thresholds at the kj-th largest sampled group maximum
-            // (k_floor_kth; a sample of every tile -- small shards -- leaves the floor)
-            if (kj > 0 && np == 1 && a.sample_stride > 1) {
-                hipLaunchKernelGGL(k_floor_kth, dim3((Bp + 3) / 4), dim3(256), 0, sp, sc.mkeys.as<uint32_t>(),
-                                   sc.floor_q.as<float>(), Bp, kj);
+            // a strided sample: start the thresholds at the kj-th largest sampled group maximum (k_floor_kth; a
+            // sample of every tile -- small shards -- leaves the floor)
+            if (kj > 0 && a.sample_stride > 1) {
+                if (np == 1)
+                    hipLaunchKernelGGL(k_floor_kth, dim3((Bp + 3) / 4), dim3(256), 0, sp, sc.mkeys.as<uint32_t>(),
+                                       sc.floor_q.as<float>(), Bp, kj);
+                else
+                    hipLaunchKernelGGL(k_floor_kth_parts, dim3(Bp), dim3(64), 0, sp, sc.mkeys.as<uint32_t>(),
+                                       sc.floor_q.as<float>(), Bp, np, kj);
                 HIP_TRY(hipGetLastError());
             }
             ev.sampled = true;
@@ -2237,16 +2246,18 @@ extern "C" int hr_kc_for_k_dim(int k, int dim) {
     return std::min(HR_MAX_KC, (k + kc_margin(k, dim) + 31) / 32 * 32);
 }
 
-// The order statistic of a query's 32 group maxima that starts the FILTER's threshold and sets k_select's
-// (ScanArgs::kj): with one row part (kc <= 32) at least kc rows must lie at or above the threshold, and kc is
-// k + margin rounded UP to 32 -- the smallest group maximum, the 32nd largest.  The (k + margin)-th largest
+// The order statistic of a query's 32 np group maxima (np = ceil(kc / 32) row parts) that starts the FILTER's
+// threshold (k_floor_kth after the SAMPLE): at least kc rows must lie at or above the threshold, and kc is k +
+// margin rounded UP to 32 -- the smallest group maximum, the (32 np)-th largest.  The (k + margin)-th largest
 // leaves the guard the margin it was sized for and starts higher: the rows above the smallest of 32 group maxima
 // number ~32 H(32) = 130 of the rows seen, above the 26th largest (k = 10) ~32 ln(32 / 6) = 54 -- fewer candidates
 // appended while the SAMPLE's keys are the threshold (the first tiles of every wave).  Exactness is unchanged:
 // every key is the score of a row of its group, so j groups hold a row at or above the j-th largest key, and that
-// key only grows (exactness guard).  0: the smallest (row parts, or k + margin >= 32).
+// key only grows (exactness guard).  0: the smallest (k + margin fills every group, or a caller
+// asked for a kc of its own -- hr_index_search_shard's kc argument -- and gets kc candidates per shard as before).
 int hr_rank_for(int k, int kc, int dim) {
-    if (kc > 32) return 0;
+    if (kc != hr_kc_for_k_dim(k, dim)) return 0;
+    const int m = (kc + 31) / 32 * 32;
     const int j = std::min(kc, k + kc_margin(k, dim));
-    return j < 32 ? j : 0;
+    return j < m ? j : 0;
 }

@@ -1020,6 +1020,28 @@ static __global__ __attribute__((unused)) __launch_bounds__(256) void k_floor_kt
     if ((threadIdx.x & 63) == 0) floor_q[q] = fmaxf(floor_q[q], t);
 }
 
+// The same with row parts (np > 1: 32 np groups, keys [np][Bp][32]): one 64-thread block per query ranks its
+// 32 np <= 256 keys by counting and raises the floor to the kj-th largest.
+static __global__ __attribute__((unused)) __launch_bounds__(64) void k_floor_kth_parts(const uint32_t* __restrict__ mkeys,
+                                                                                        float* __restrict__ floor_q,
+                                                                                        int Bp, int np, int kj) {
+    __shared__ float v[256];
+    const int q = blockIdx.x, m = np * 32;
+    for (int i = threadIdx.x; i < m; i += 64) {
+        const uint32_t k = mkeys[((int64_t)(i >> 5) * Bp + q) * 32 + (i & 31)];
+        v[i] = key2f(k > HR_KEY_NEG_INF ? k : HR_KEY_NEG_INF);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += 64) {
+        int gt = 0, ge = 0;
+        for (int j = 0; j < m; ++j) {
+            gt += v[j] > v[i];
+            ge += v[j] >= v[i];
+        }
+        if (gt < kj && ge >= kj) floor_q[q] = fmaxf(floor_q[q], v[i]);  // (every such thread holds the same value)
+    }
+}
+
 constexpr int kRankMax = 1024;  // candidate sets up to this size are ranked by counting, larger ones sorted
 
 static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(const uint32_t* __restrict__ cnt, const float2* __restrict__ buf,

@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--persist", type=int, default=1, choices=(0, 1, 2),
                    help="persistent FILTER for the pipelined shard batches: 0 off (one FILTER launch per batch), "
                         "1 shards of 4.2M-5.1M rows (default: where it measured faster), 2 every shard size")
+    p.add_argument("--depth", type=int, default=2,
+                   help="batches in flight per rank (ShardedSearch depth): the host waits for batch i's guard flags "
+                        "when it submits batch i + depth")
     p.add_argument("--single-process", action="store_true",
                    help="one process, one index handle striped over --gpus devices (instead of one rank per GPU)")
     return p.parse_args()
@@ -315,6 +318,7 @@ def main_single_process(args):
     FastAPI process, one store per collection).  Batches are pipelined through hr_index_search_submit /
     _finalize (one host thread per shard, two batches in flight); same JSON line as the multi-process
     path, plus the host time per batch of the caller and of the busiest shard thread."""
+    _protect_stdout()
     import torch
 
     from hiprag import _native, synth
@@ -380,7 +384,7 @@ def main_single_process(args):
         result.update(recall_checks(args, N, D, K, q_dev[args.warmup, :nq].cpu().numpy(),
                                     r_dev[args.warmup, :nq].cpu().numpy(), s_dev[args.warmup, :nq].cpu().numpy(),
                                     q_iso[:nq], r_iso[:nq].cpu().numpy(), s_iso[:nq].cpu().numpy()))
-    print(json.dumps(result), flush=True)
+    emit(result)
 
 
 def _free_port() -> int:
@@ -435,6 +439,24 @@ def launch_probe(args) -> None:
         dist.destroy_process_group()
 
 
+_RESULT_OUT = None  # the process's original stdout (fd 1 goes to stderr while the GPU libraries run)
+
+
+def _protect_stdout():
+    """Keep stdout to the ONE JSON line: RCCL prints its version banner to fd 1 when a communicator comes up
+    ("RCCL version : ...", seen in the --collective runs), and so may other libraries.  Fd 1 is pointed at
+    stderr for the rest of the process and the result line goes to a duplicate of the original stdout."""
+    global _RESULT_OUT
+    if _RESULT_OUT is None:
+        sys.stdout.flush()
+        _RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(result: dict) -> None:
+    print(json.dumps(result), file=_RESULT_OUT or sys.stdout, flush=True)
+
+
 def main():
     args = parse()
     if args.single_process:
@@ -443,6 +465,7 @@ def main():
         sys.exit(launch_ranks(args, sys.argv[1:]))
     if args.launch_probe:
         return launch_probe(args)
+    _protect_stdout()
     import torch
     import torch.distributed as dist
 
@@ -496,7 +519,8 @@ def main():
     q_ready.record()
     s_dev = torch.empty((n_batches, B, K), dtype=torch.float32, device=dev)
     r_dev = torch.empty((n_batches, B, K), dtype=torch.int64, device=dev)
-    searcher = ShardedSearch(index, start, max_batch=B, device=dev, max_k=K, force_collective=args.collective)
+    searcher = ShardedSearch(index, start, max_batch=B, device=dev, max_k=K, force_collective=args.collective,
+                             depth=args.depth)
 
     # One step = one batch through the whole path.  Steps are pipelined two deep: submit()
     # enqueues batch i (scan, gather, merge, async copy of the guard flags) and finalizes the
@@ -514,6 +538,7 @@ def main():
     wide0 = index.wide_launches()
     persist0 = index.persist_stats()["batches"]
     fb0 = searcher.fallback_queries
+    wait0 = searcher.wait_s
     if G > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -532,6 +557,7 @@ def main():
         raise RuntimeError(f"persistent FILTER error {pst['error']}")
     persist = pst["batches"] - persist0 == args.steps  # every timed batch went through the persistent FILTER
     fallback_queries = searcher.fallback_queries - fb0  # guard failures in the timed region (collect fallback)
+    host_wait_s = searcher.wait_s - wait0  # blocked on guard flags; the rest of the loop's wall time is host work
     persist_timeline = None
     if persist:  # where the period goes (device stamps, us): medians over the timed batches
         tr = index.persist_trace(args.steps)
@@ -600,6 +626,8 @@ def main():
                      "read_ceiling_source": "profiles/r02_stream_ceiling.jsonl", "traffic": None,
                      "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg / passes, 4),
                      "sample_pass_ms": round(sample_avg, 4), "guard_fallback_queries": fallback_queries},
+        # host work per step (submit minus its waits for guard flags): at or above ms_per_step the step is host-bound
+        "host_ms_per_step": round(1000.0 * (elapsed - host_wait_s) / args.steps, 4),
         **({"persist_timeline": persist_timeline} if persist_timeline else {}),
         # the Q·Xᵀ contraction of the same launch on the MFMA pipe (bf16 dense peak, MI355X_MICROARCH.md)
         "mfma": {"achieved": round(mfma_tflops, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -690,7 +718,7 @@ def main():
             result["cpu_oracle"] = {"value": None, "error": repr(e)}
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if G > 1:
         dist.barrier()
     if dist.is_initialized():

@@ -26,6 +26,8 @@ this module is the C1 collective of the SURVEY kernel inventory.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from . import _native
@@ -109,6 +111,7 @@ class ShardedSearch:
             raise ValueError("force_collective needs an initialised process group")
         self.collective = self.G > 1 or bool(force_collective)  # the exchange goes through the process group
         self.fallback_queries = 0  # queries whose guard failed (collect fallback), cumulative
+        self.wait_s = 0.0  # host time blocked on guard flags in finalize (the rest of a submit is host work)
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
         # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
         self.kc = int(kc) if kc is not None else _native.kc_for_k(max_k, int(getattr(index, "dim", 0)))
@@ -234,7 +237,9 @@ class ShardedSearch:
         q, k, s_out, r_out, mask_ptr, B = slot.ticket
         slot.ticket = None
         if slot.event is not None:
+            t0 = time.perf_counter()
             slot.event.synchronize()
+            self.wait_s += time.perf_counter() - t0
         failed = self._failed_queries(slot, B)
         if len(failed):
             self.fallback_queries += len(failed)

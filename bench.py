@@ -614,7 +614,7 @@ def main():
         "config": {"workload": f"{N / 1e6:g}M x {D} {args.dtype} cosine exact top-{K}, batch {B}, row-sharded",
                    "rows": N, "dim": D, "batch": B, "k": K,
                    "parallelism": f"rowshard{G}" + ("+rccl" if searcher.collective else ""),
-                   "exchange": (f"RCCL all_gather_into_tensor ({dist.get_backend()})" if searcher.collective
+                   "exchange": (f"all-gather of the candidate records: {searcher.transport}" if searcher.collective
                                 else "none (one shard: local copy)")},
         "roofline": {"bound": "hbm",
                      "kernel": ("k_filter_wide8 (128-query FILTER)" if wide else
@@ -719,6 +719,7 @@ def main():
 
     if rank == 0:
         emit(result)
+    searcher.close()  # (every rank: the direct RCCL communicator goes before the process group)
     if G > 1:
         dist.barrier()
     if dist.is_initialized():

@@ -7,8 +7,9 @@ At world size 1 the exchange is normally a local copy; ``force_collective=True``
 per-shard records through ``all_gather_into_tensor`` and src_rank batches through ``broadcast`` on the
 tail / scan streams -- the branch an 8-GPU node runs (dist.py ``_all_gather`` / ``_broadcast``).  A
 subclass forces every query of one batch through the collect fallback, so ``_fallback``'s second
-all-gather runs too.  Every collective call is counted and the backend is reported, so the parent can
-assert the RCCL branch executed.  Runs in its own process so a hung communicator is bounded by the
+all-gather runs too.  Every exchange is counted (ShardedSearch.collective_calls) and the backend and transport
+(RCCL called directly on the tail / scan streams, dist.RcclComm) are reported, so the parent can assert the RCCL
+branch executed.  Runs in its own process so a hung communicator is bounded by the
 parent's timeout.
 """
 import os
@@ -34,19 +35,6 @@ def main(port: int, q_path: str, out_path: str, rows: int, dim: int) -> None:
 
     from hiprag import _native
     from hiprag.dist import ShardedSearch
-
-    counts = {"all_gather_into_tensor": 0, "broadcast": 0}
-    real_ag, real_bc = dist.all_gather_into_tensor, dist.broadcast
-
-    def ag(*a, **kw):
-        counts["all_gather_into_tensor"] += 1
-        return real_ag(*a, **kw)
-
-    def bc(*a, **kw):
-        counts["broadcast"] += 1
-        return real_bc(*a, **kw)
-
-    dist.all_gather_into_tensor, dist.broadcast = ag, bc
 
     q = np.load(q_path)["q"]  # (2, B, dim): planted batch, isotropic batch
     nb, B, _ = q.shape
@@ -77,9 +65,12 @@ def main(port: int, q_path: str, out_path: str, rows: int, dim: int) -> None:
     ff = ForcedFallback(idx, 0, max_batch=B, device=dev, max_k=k, force_collective=True)
     ff.search(qd[1], k, s_out=s[5], r_out=r[5])
     torch.cuda.synchronize()
+    calls = {c: ss.collective_calls[c] + ff.collective_calls[c] for c in ("all_gather", "broadcast")}
     np.savez(out_path, s=s.cpu().numpy(), r=r.cpu().numpy(), backend=np.array(backend),
-             ag=np.array(counts["all_gather_into_tensor"]), bc=np.array(counts["broadcast"]),
+             ag=np.array(calls["all_gather"]), bc=np.array(calls["broadcast"]), transport=np.array(ss.transport),
              persist=np.array(idx.persist_stats()["batches"]))
+    ss.close()
+    ff.close()
     dist.destroy_process_group()
 
 

@@ -49,7 +49,7 @@ def test_rccl_world1_exchange_c3_vs_oracle(tmp_path, N):
     print(proc.stdout[-2000:], proc.stderr[-4000:])
     assert proc.returncode == 0, proc.stderr[-4000:]
     got = np.load(out)
-    assert str(got["backend"]) == "nccl"
+    assert str(got["backend"]) == "nccl" and str(got["transport"]).startswith("rccl"), str(got["transport"])
     # 4 pipelined batches + 1 broadcast batch: one all-gather each; the forced fallback batch: two (the
     # merge's gather, then the collect records'); one broadcast
     assert int(got["ag"]) == 7 and int(got["bc"]) == 1, (int(got["ag"]), int(got["bc"]))

@@ -1,0 +1,19 @@
+# r04 u: the exchange through RCCL called directly on the tail stream (dist.RcclComm) -- the world-size-1 RCCL
+# parity test (10M and 5M rows), then the 1.25M / 10M benches with and without the collective
+set -u
+O=gpurun_out/r04u; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_rccl.py tests/test_gpu_dist.py > $O/tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; grep -E "passed|failed|error" $O/tests.log | tail -3; [ $rc -ne 0 ] && exit $rc
+run() {  # tag, command...
+  tag=$1; shift
+  timeout -k 10 240 "$@" --no-cpu --no-embed > $O/$tag.json 2> $O/$tag.err; rc=$?
+  echo "$tag rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/$tag.err; exit $rc; }
+  python3 -c "import json,sys;d=json.load(open('$O/$tag.json'));r=d['roofline'];print(d['value'],d['ms_per_step'],d.get('host_ms_per_step'),r['avg_launch_ms'],d['config']['exchange'])"
+}
+for rep in 1 2; do
+  run s125_rccl_$rep python3 bench.py --rows 1250000 --steps 200 --warmup 10 --collective
+  run s125_local_$rep python3 bench.py --rows 1250000 --steps 200 --warmup 10
+done
+run m10_rccl python3 bench.py --steps 100 --warmup 10 --collective
+run r5_rccl python3 bench.py --rows 5000000 --steps 60 --warmup 5 --collective
+echo done

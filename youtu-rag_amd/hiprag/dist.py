@@ -49,6 +49,65 @@ def _record_views(rec, B: int, kc: int):
     return rec[..., :n].view(*rec.shape[:-1], B, kc, 2), rec[..., n:n + B]
 
 
+class RcclComm:
+    """An RCCL communicator of the process group's ranks, called directly (ctypes, the librccl.so torch loaded) on
+    the streams the exchange is ordered on -- the tail stream for the all-gather, the scan stream for a broadcast.
+
+    Through torch.distributed an RCCL collective runs on the process group's own internal stream, joined to the
+    caller's stream by an event each way; with GPU_MAX_HW_QUEUES = 4 that extra stream shares a hardware queue
+    with the scan or tail streams, and the tail's all-gather then queues behind the next batch's FILTER launch:
+    a 1.25M-row shard (the G = 8 per-rank step) ran 0.448-0.469 ms/step through it against 0.418 with the
+    local copy, at world size 1, where the host work per step is only 0.09 ms (profiles/
+    r04_rccl_world1_host_time.jsonl).  A direct ncclAllGather on the tail stream adds no stream.  The unique
+    id goes to every rank with one broadcast over the process group; ncclCommInitRank is collective (every rank
+    constructs this at the same point)."""
+
+    def __init__(self, torch, dist, group, device):
+        import ctypes
+        import os
+
+        self.ct = ctypes
+        self.lib = lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+        lib.ncclGetErrorString.restype = ctypes.c_char_p
+        for f in ("ncclAllGather", "ncclBroadcast", "ncclCommInitRank", "ncclGetUniqueId", "ncclCommDestroy"):
+            getattr(lib, f).restype = ctypes.c_int
+
+        class _Uid(ctypes.Structure):
+            _fields_ = [("internal", ctypes.c_char * 128)]
+
+        self.rank = dist.get_rank(group)
+        self.G = dist.get_world_size(group)
+        uid = _Uid()
+        if self.rank == 0:
+            self._check(lib.ncclGetUniqueId(ctypes.byref(uid)))
+        buf = torch.frombuffer(bytearray(bytes(uid)), dtype=torch.uint8).to(device)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(buf, src, group=group)
+        uid = _Uid.from_buffer_copy(bytes(buf.cpu().numpy().tobytes()))
+        self.comm = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.G, uid, self.rank))
+
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise RuntimeError(f"RCCL error {rc}: {self.lib.ncclGetErrorString(rc).decode()}")
+
+    def all_gather(self, out_ptr: int, in_ptr: int, nbytes: int, stream: int) -> None:
+        c = self.ct
+        self._check(self.lib.ncclAllGather(c.c_void_p(in_ptr), c.c_void_p(out_ptr), c.c_size_t(nbytes), 1,  # uint8
+                                           self.comm, c.c_void_p(stream)))
+
+    def broadcast(self, ptr: int, nbytes: int, root: int, stream: int) -> None:
+        c = self.ct
+        self._check(self.lib.ncclBroadcast(c.c_void_p(ptr), c.c_void_p(ptr), c.c_size_t(nbytes), 1, root,
+                                           self.comm, c.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self.comm:
+            self._check(self.lib.ncclCommDestroy(self.comm))
+            self.comm = self.ct.c_void_p()
+
+
 class _Slot:
     def __init__(self, torch, device, G, B, kc, pinned, gather: bool):
         f64 = dict(dtype=torch.float64, device=device)
@@ -111,6 +170,7 @@ class ShardedSearch:
             raise ValueError("force_collective needs an initialised process group")
         self.collective = self.G > 1 or bool(force_collective)  # the exchange goes through the process group
         self.fallback_queries = 0  # queries whose guard failed (collect fallback), cumulative
+        self.collective_calls = {"all_gather": 0, "broadcast": 0}  # exchanges through the process group's ranks
         self.wait_s = 0.0  # host time blocked on guard flags in finalize (the rest of a submit is host work)
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
         # (16 -> kc 32, one row part); a larger k up to kc is served, with a thinner margin
@@ -124,6 +184,13 @@ class ShardedSearch:
         self._next = 0
         # tail stream: select/rescore, all-gather, merge and the flag copy of each batch
         self.tail = torch.cuda.Stream(self.device) if (overlap and pinned) else None
+        # RCCL itself on the tail / scan streams (RcclComm) when the group is nccl; gloo (CPU tests) goes
+        # through torch.distributed with host staging
+        self.backend = dist.get_backend(group) if self.collective else None
+        self.rccl = RcclComm(torch, dist, group, self.device) if (self.collective and self.backend == "nccl"
+                                                                   and pinned) else None
+        self.transport = ("rccl (direct, on the tail stream)" if self.rccl is not None else
+                          f"torch.distributed ({self.backend})" if self.collective else "local copy")
 
     # hooks (overridden in CPU tests of the orchestration logic)
     def _stream(self) -> int:
@@ -156,9 +223,14 @@ class ShardedSearch:
         if not self.collective:
             out[0].copy_(inp)
         else:
+            self.collective_calls["all_gather"] += 1
+            if self.rccl is not None:  # out (G, L) contiguous, rank r's record at row r
+                self._on_tail(lambda st: self.rccl.all_gather(out.data_ptr(), inp.data_ptr(),
+                                                              inp.numel() * inp.element_size(), st))
+                return
             # output as the rank-concatenation along dim 0 (accepted by RCCL and gloo alike)
             flat = out.view(self.G * inp.shape[0], *inp.shape[1:])
-            if out.is_cuda and self.dist.get_backend(self.group) != "nccl":
+            if out.is_cuda and self.backend != "nccl":
                 # gloo (tests: several ranks sharing one GPU) gathers host tensors
                 tmp = flat.cpu()
                 self.dist.all_gather_into_tensor(tmp, inp.cpu().contiguous(), group=self.group)
@@ -166,9 +238,28 @@ class ShardedSearch:
             else:
                 self.dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
 
+    def _on_tail(self, issue):
+        """Issue a direct RCCL call on the tail stream: every collective of the communicator then runs in ONE
+        stream's order on every rank (two streams could interleave two collectives differently on different ranks
+        and deadlock).  From another stream (the fallback's gather, a broadcast before the scan) the tail waits for
+        it first and it waits for the tail after -- rare paths; the per-batch gather is issued on the tail."""
+        torch = self.torch
+        cur = torch.cuda.current_stream(self.device)
+        if self.tail is None or cur == self.tail:
+            issue(self._stream())
+            return
+        self.tail.wait_stream(cur)
+        issue(self.tail.cuda_stream)
+        cur.wait_stream(self.tail)
+
     # the search
     def _broadcast(self, t, src: int):
-        if t.is_cuda and self.dist.get_backend(self.group) != "nccl":  # gloo (tests): host staging
+        self.collective_calls["broadcast"] += 1
+        if self.rccl is not None:  # src: a global rank; the communicator's ranks are the group's
+            root = self.dist.get_group_rank(self.group, src) if self.group is not None else src
+            self._on_tail(lambda st: self.rccl.broadcast(t.data_ptr(), t.numel() * t.element_size(), root, st))
+            return
+        if t.is_cuda and self.backend != "nccl":  # gloo (tests): host staging
             h = t.cpu()
             self.dist.broadcast(h, src, group=self.group)
             t.copy_(h)
@@ -249,6 +340,15 @@ class ShardedSearch:
     def _failed_queries(self, slot, B: int):
         """Indices of the batch's queries whose guard failed (hook: tests force the fallback)."""
         return np.nonzero(slot.fail_h[:B].numpy())[0]
+
+    def close(self):
+        """Finalize what is in flight and release the direct RCCL communicator (every rank, before the process
+        group is destroyed)."""
+        self.finalize_all()
+        if self.rccl is not None:
+            self.torch.cuda.synchronize(self.device)
+            self.rccl.close()
+            self.rccl = None
 
     def finalize_all(self):
         for i in range(len(self.slots)):

@@ -712,7 +712,8 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     const bool piped = st_tail != st && mode == 0;
     if (!piped) st_tail = st;
     const int64_t n_tiles = (h->n + 31) / 32;
-    // SAMPLE size for n units: n/128 tiles (A/B: 128 beats 64 by 0.7 % at 10M), at least 2048 -- or 1024 on shards
+    // SAMPLE size for n units: n/128 tiles (round 2: 128 beat 64 by 0.7 % at 10M; with the kj-th largest floor, n/256
+    // on shards beyond 160k tiles), at least 2048 -- or 1024 on shards
     // up to 80k tiles (2.56M rows): with the kj-th largest starting floor (k_floor_kth) 1024 sampled tiles start
     // the FILTER as well there and the early-SAMPLE chain is shorter -- 1M x 768 0.289 -> 0.284 ms/step, 2.5M
     // 0.804 -> 0.800, 1.25M unchanged, 3072 slower; at 5M rows 1024 cost 0.5 % (profiles/
@@ -724,7 +725,9 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
         // SAMPLEs add up (8 x 1.25M rows on one GPU: 3.387 / 3.308 / 3.297 ms per batch at 2048 / 1024 /
         // 512, profiles/r03_group_scan_streams.log)
         const int64_t smin = h->shared_dev ? 512 : (n <= 80 * 1024 ? 1024 : 2048);
-        return std::max<int64_t>(smin, n / 128);
+        // beyond the dual-FILTER range n/256: the SAMPLE beside the FILTER reads half as much (10M rows 2.958-2.968
+        // -> 2.944-2.956 ms/step, k = 100 -0.35 %; profiles/r04_sample_size_10M_ab.jsonl)
+        return std::max<int64_t>(smin, n > 160 * 1024 ? n / 256 : n / 128);
     };
     // Early SAMPLE (pipelined, queries ready by event): query prep and the SAMPLE pass run on the
     // index's own "pre" stream over the CUs the previous batch's FILTER leaves free, while that

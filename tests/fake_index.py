@@ -74,7 +74,8 @@ class AsyncOracleIndex(OracleIndex):
     """OracleIndex with the asynchronous host-query entry point of NativeIndex (search_submit_host /
     search_collect): results are computed at submit, and the completion count is written to the caller's
     eventfd from a timer thread after `delay` seconds -- the GPU's host function, simulated.  At most two
-    batches in flight, like the library."""
+    batches in flight, like the library, and like the library (hr_index_search_collect) a collect returns only
+    once that batch's notification has been written: the caller may close the fd right after."""
 
     def __init__(self, *a, delay=0.002, **kw):
         super().__init__(*a, **kw)
@@ -82,6 +83,7 @@ class AsyncOracleIndex(OracleIndex):
         self.needs_fallback: set = set()  # tickets whose collect would run the exact fallback (poll -> 2)
         self.collected: list = []
         self.devices = [0]
+        self.notified: dict = {}  # ticket -> threading.Event set once its eventfd write is done
 
     def search_submit_host(self, q, k, notify_fd=-1):
         import os
@@ -97,7 +99,15 @@ class AsyncOracleIndex(OracleIndex):
         self.next_ticket += 1
         self.tickets[t] = self.search(q, k)
         if notify_fd >= 0:
-            threading.Timer(self.delay, lambda: os.eventfd_write(notify_fd, 1)).start()
+            done = self.notified[t] = threading.Event()
+
+            def fire():
+                try:
+                    os.eventfd_write(notify_fd, 1)
+                finally:
+                    done.set()
+
+            threading.Timer(self.delay, fire).start()
         return t
 
     def search_poll(self, ticket):
@@ -110,6 +120,9 @@ class AsyncOracleIndex(OracleIndex):
         return 2 if ticket in self.needs_fallback else 1
 
     def search_collect(self, ticket, B, k):
+        ev = self.notified.pop(ticket, None)
+        if ev is not None and not ev.wait(10):  # the library waits for its notify host function the same way
+            raise RuntimeError("notification never written")
         self.needs_fallback.discard(ticket)
         self.collected.append(ticket)
         return self.tickets.pop(ticket)

@@ -125,3 +125,148 @@ def test_merge_guard_semantics():
     assert r.tolist() == [[3, 100]] and kth[0] == 0.8 and fail[0] == 0
     s, r, kth, fail = _numpy_merge(cand, torch.tensor([[0.85], [-np.inf]]), 2, 1, 3, 2)
     assert fail[0] == 1
+
+
+class StubRccl:
+    """A ctypes-shaped stand-in for librccl.so (the entry points RcclComm binds, same argument conventions) that
+    moves the bytes between the ranks with gloo on the host -- so RcclComm's G > 1 control flow (unique-id
+    broadcast, ncclCommInitRank(G, uid, rank), rank-ordered all-gather, broadcast, destroy) runs on CPU.  Pointers
+    are host addresses here (CPU tensors)."""
+
+    def __init__(self, uid_bytes: bytes):
+        import ctypes
+
+        self.ct, self.uid_bytes, self.calls = ctypes, uid_bytes, []
+
+        def get_error_string(rc):
+            return b"stub error"
+
+        def get_unique_id(uid_ref):
+            ctypes.memmove(ctypes.addressof(uid_ref._obj), self.uid_bytes, 128)
+            self.calls.append(("ncclGetUniqueId",))
+            return 0
+
+        def comm_init_rank(comm_ref, nranks, uid, rank):
+            self.calls.append(("ncclCommInitRank", int(nranks), bytes(uid.internal), int(rank)))
+            comm_ref._obj.value = 0x5EED
+            return 0
+
+        def all_gather(send, recv, count, dtype, comm, stream):
+            n = int(count.value)
+            assert dtype == 1 and comm.value == 0x5EED  # uint8, the communicator InitRank returned
+            mine = torch.frombuffer(bytearray(ctypes.string_at(send.value, n)), dtype=torch.uint8)
+            every = [torch.empty(n, dtype=torch.uint8) for _ in range(dist.get_world_size())]
+            dist.all_gather(every, mine)
+            for r, t in enumerate(every):  # rank r's bytes at offset r * count (ncclAllGather's layout)
+                ctypes.memmove(recv.value + r * n, t.numpy().tobytes(), n)
+            self.calls.append(("ncclAllGather", n))
+            return 0
+
+        def broadcast(send, recv, count, dtype, root, comm, stream):
+            n = int(count.value)
+            t = torch.frombuffer(bytearray(ctypes.string_at(send.value, n)), dtype=torch.uint8)
+            dist.broadcast(t, int(root))
+            ctypes.memmove(recv.value, t.numpy().tobytes(), n)
+            self.calls.append(("ncclBroadcast", n, int(root)))
+            return 0
+
+        def comm_destroy(comm):
+            self.calls.append(("ncclCommDestroy",))
+            return 0
+
+        self.ncclGetErrorString = get_error_string
+        self.ncclGetUniqueId = get_unique_id
+        self.ncclCommInitRank = comm_init_rank
+        self.ncclAllGather = all_gather
+        self.ncclBroadcast = broadcast
+        self.ncclCommDestroy = comm_destroy
+
+
+def _rccl_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+    from hiprag.dist import ShardedSearch, _record_len
+    from oracle import ref_numpy as R
+
+    lo, hi = N * rank // world, N * (rank + 1) // world
+    bounds = [(N * g // world, N * (g + 1) // world) for g in range(world)]
+    stored = oracle.c_build_synthetic(5, lo, hi - lo, DIM, "bf16", "cosine", 1)
+    q = np.random.default_rng(0).standard_normal((B, DIM)).astype(np.float32)
+    qn = R.process_queries(q, "cosine")
+    stub = StubRccl(uid_bytes=bytes([rank * 7 + 3]) * 128 if rank == 0 else bytes(128))
+    seen = {}
+
+    class CpuRccl(ShardedSearch):
+        def _stream(self):
+            return 0
+
+        def _shard_search(self, qt, k, cand, bound, mask_ptr, q_ready=None):
+            s, r = oracle.c_search(stored, "bf16", qn[: qt.shape[0]], KC, row_offset=lo, nthreads=1)
+            cand.view(torch.int64)[..., 1] = torch.from_numpy(r)
+            cand[..., 0] = torch.from_numpy(s)
+            bound[:] = torch.from_numpy(s[:, -1])
+
+        def _merge(self, cand_all, bound_all, G, Bq, kc, k, s_out, r_out, kth, fail):
+            # the packed records as the product's k_merge reads them: rank g's record at g * (record bytes)
+            assert cand_all.stride(0) * 8 == _record_len(Bq, kc) * 8 and bound_all.stride(0) == cand_all.stride(0)
+            rows = cand_all.contiguous().view(torch.int64)[..., 1].numpy()
+            for g, (a, b) in enumerate(bounds):  # rank order: row g of the gather holds rank g's shard rows
+                assert ((rows[g] >= a) & (rows[g] < b)).all(), (g, rows[g].min(), rows[g].max())
+            seen["merged"] = seen.get("merged", 0) + 1
+            s, r, kt, f = _numpy_merge(cand_all, bound_all, G, Bq, kc, k)
+            s_out.copy_(torch.from_numpy(s))
+            r_out.copy_(torch.from_numpy(r))
+            kth.copy_(torch.from_numpy(kt))
+            fail.copy_(torch.from_numpy(f))
+
+    ss = CpuRccl(index=None, row_offset=lo, max_batch=B, device=torch.device("cpu"), kc=KC, rccl_lib=stub)
+    assert ss.rccl is not None and ss.transport.startswith("rccl") and ss.rccl.G == world
+    s, r = ss.search(torch.from_numpy(q), K)
+    q_in = torch.from_numpy(q) if rank == 1 else torch.zeros((B, DIM))
+    s2, r2 = ss.search(q_in, K, src_rank=1)  # the batch known to rank 1 only: ncclBroadcast from root 1
+    assert torch.equal(s2, s) and torch.equal(r2, r)
+    ss.close()
+    names = [c[0] for c in stub.calls]
+    init = [c for c in stub.calls if c[0] == "ncclCommInitRank"][0]
+    out = {"rank": rank, "names": names, "init_G": init[1], "init_rank": init[3], "uid": init[2].hex(),
+           "merged": seen["merged"], "ag": [c[1] for c in stub.calls if c[0] == "ncclAllGather"],
+           "bc": [c[1:] for c in stub.calls if c[0] == "ncclBroadcast"]}
+    import json
+
+    with open(f"{result_path}.{rank}.json", "w") as f:
+        json.dump(out, f)
+    if rank == 0:
+        np.savez(result_path, s=s.numpy(), r=r.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_comm_two_ranks_with_stub_library(tmp_path):
+    """RcclComm's G > 1 control flow on CPU -- the unique id rank 0 draws reaches rank 1 through
+    the process-group broadcast, every rank calls ncclCommInitRank(G, that id, its rank), the all-gathered records
+    arrive in rank order and the merge reads them with the packed record stride, and the answer is the single-index
+    oracle's."""
+    import json
+
+    import oracle
+    from hiprag.dist import _record_len
+    from oracle import ref_numpy as R
+
+    path = str(tmp_path / "rccl")
+    mp.start_processes(_rccl_worker, args=(2, _free_port(), path), nprocs=2, join=True, start_method="spawn")
+    per = [json.load(open(f"{path}.{r}.json")) for r in range(2)]
+    uid0 = (bytes([3]) * 128).hex()
+    for r, o in enumerate(per):
+        assert o["init_G"] == 2 and o["init_rank"] == r and o["uid"] == uid0  # rank 1 never drew an id itself
+        assert o["names"][-1] == "ncclCommDestroy"
+        assert o["ag"] == [_record_len(B, KC) * 8] * 2  # one all-gather of the packed record per batch
+        assert o["bc"] == [[B * DIM * 4, 1]]            # the src_rank batch: one broadcast from root 1
+        assert o["merged"] == 2
+    assert "ncclGetUniqueId" in per[0]["names"] and "ncclGetUniqueId" not in per[1]["names"]
+    got = np.load(path + ".npz")
+    stored = oracle.c_build_synthetic(5, 0, N, DIM, "bf16", "cosine", 2)
+    q = np.random.default_rng(0).standard_normal((B, DIM)).astype(np.float32)
+    s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), K)
+    np.testing.assert_array_equal(got["r"], r_ref)
+    np.testing.assert_array_equal(got["s"], s_ref.astype(np.float32))

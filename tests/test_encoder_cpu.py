@@ -109,3 +109,27 @@ def test_pack_of_several_batches_is_their_concatenation():
         a, b = enc.forward_packed(enc.pack(i1, m1)), enc.forward_packed(enc.pack(i2, m2))
     assert both.lengths.tolist() == [*l1.tolist(), *l2.tolist()] and both.max_len == 30
     torch.testing.assert_close(h, torch.cat([a, b]), rtol=1e-5, atol=2e-5)
+
+
+def test_graphed_forward_only_captures_varlen_layers():
+    """a captured forward must not bake in host-sliced attention.  graph_safe() holds only when every
+    layer takes the varlen kernel (offsets read from the device tensor); GraphedForward runs everything else eagerly."""
+    from hiprag.rag.encoder import GraphedForward
+
+    torch.manual_seed(0)
+    model = build_random_bert("tiny", 3).eval()
+    enc = UnpaddedEncoder(model, use_varlen=False)
+    assert not enc.graph_safe()  # SDPA per sequence, sliced by host offsets
+    enc.varlen = lambda *a: None  # a varlen kernel: every layer's 1/sqrt(d) scale takes it
+    assert enc.graph_safe()
+    w, b, nH, d, scale, *rest = enc.layers[1]
+    enc.layers[1] = (w, b, nH, d, scale * 2.0, *rest)  # one layer with its own scale falls back to SDPA
+    assert not enc.graph_safe()
+    enc = UnpaddedEncoder(model, use_varlen=False)
+    g = GraphedForward(enc)
+    rng = np.random.default_rng(7)
+    ids, mask, lens = _batch(rng, 4, 16)
+    with torch.inference_mode():
+        pk = enc.pack(ids, mask, granule=16)
+        out = g(pk)
+    assert not g.graphs and g.replays == 0 and out.shape[0] == int(pk.cu_host[-1])

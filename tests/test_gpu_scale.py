@@ -57,16 +57,19 @@ def c3(native):
     idx.reserve(N3)
     idx.add_synthetic(SEED3, 0, N3)
     planted, iso = _queries(SEED3, N3, D3, 64, qseed=4242)
+    planted2, iso2 = _queries(SEED3, N3, D3, 64, qseed=4343)  # 128 more: the store's 256-query sample
     q = np.concatenate([planted, iso])
-    # one oracle pass over the 10M rows for all 128 queries at k = 100; top-10 is its prefix
-    s_ref, r_ref = oracle.c_search_synthetic(SEED3, 0, N3, D3, "bf16", "cosine", R.process_queries(q, "cosine"), 100)
-    yield idx, q, s_ref, r_ref
+    q2 = np.concatenate([planted2, iso2])
+    # one oracle pass over the 10M rows for all 256 queries at k = 100; top-10 is its prefix
+    s_all, r_all = oracle.c_search_synthetic(SEED3, 0, N3, D3, "bf16", "cosine",
+                                             R.process_queries(np.concatenate([q, q2]), "cosine"), 100)
+    yield idx, q, s_all[:128], r_all[:128], q2, s_all[128:], r_all[128:]
     idx.close()
 
 
 @pytest.mark.parametrize("k", [10, 100])
 def test_c3_10M_bf16_vs_oracle(c3, k):
-    idx, q, s_ref, r_ref = c3
+    idx, q, s_ref, r_ref, *_ = c3
     before, w0 = idx.stats(), idx.wide_launches()
     # 128 queries in ONE corpus pass: at k = 10 the 128-query FILTER (hr_wide.hip, one launch); at k = 100
     # (kc 160: 5 row parts, more than the 16-bit 128-query FILTER takes) two query groups in one k_scan launch
@@ -89,7 +92,7 @@ def test_c3_pipelined_path_vs_oracle(c3):
 
     from hiprag.dist import ShardedSearch
 
-    idx, q, s_ref, r_ref = c3
+    idx, q, s_ref, r_ref, *_ = c3
     k = 10
     qd = torch.from_numpy(q).cuda().view(2, 64, D3)
     ready = torch.cuda.Event()
@@ -107,6 +110,95 @@ def test_c3_pipelined_path_vs_oracle(c3):
                r_ref[64 * h:64 * (h + 1), :k])
 
 
+# ---------------------------------------------------------------- the reference's own call shapes at C3
+# VectorRetriever.retrieve issues ONE query per store search (base_retriever.py:57-63 -> chroma_store.py:118-120);
+# a serving process sees many of them at once, which HipVectorStore's micro-batcher coalesces (storage.py).
+def _call_shapes(idx, q, s_ref, r_ref):
+    """Synchronous searches of B = 1 and B = 16 (the shapes SURVEY §8(d) lists for C3; the second use of a shape
+    replays its captured HIP graph), planted and isotropic queries, k = 10 and 100, each identical to the oracle's
+    exact answer over all 10M rows."""
+    n = 0
+    for k in (10, 100):
+        for B in (1, 16):
+            for h in (0, 64):  # planted, isotropic
+                for b0 in range(h, h + 4 * B, B):  # 4 searches of each shape and kind
+                    s, r = idx.search(q[b0:b0 + B], k)
+                    _check(s, r, s_ref[b0:b0 + B, :k], r_ref[b0:b0 + B, :k])
+                    n += 1
+    print(f"\n{n} searches of B = 1 / 16: stats {idx.stats()}")
+
+
+class _LazyTable:
+    """Host records of the synthetic collection, computed for the rows a search returns (row r = chunk r % 1000 of
+    document r // 1000, the layout tools/bench_async.py loads): the store's _assemble indexes `.a` with the hit rows.
+    Building the real 10M-entry tables takes ~95 s of Python, longer than a test may run."""
+
+    def __init__(self, n: int, meta: bool):
+        self.n, self.meta, self.a = n, meta, self
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, rows):
+        rows = np.asarray(rows).reshape(-1)
+        out = np.empty(len(rows), object)
+        for j, r in enumerate(rows.tolist()):
+            d, i = divmod(r, 1000)
+            out[j] = {"document_id": f"doc{d}", "chunk_index": i} if self.meta else (f"doc{d}_chunk_{i}", f"doc{d}", "", i)
+        return out
+
+
+class _Count:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+def _store_async(idx, dtype, q, s_ref, r_ref, max_batch):
+    """256 concurrent single-query ``await store.search(query_embedding=..., top_k=10)`` tasks through HipVectorStore
+    over the 10M-row index: the micro-batcher's native launches (hr_index_search_submit_host, eventfd completion,
+    hr_index_search_collect, _assemble) -- every answer's chunk ids and score bits equal the oracle's."""
+    import asyncio
+
+    from hiprag.rag import HipVectorStore, VectorStoreConfig
+
+    cfg = VectorStoreConfig(backend="hip", collection_name="c3", persist_directory="/tmp/hiprag_c3_store",
+                            index_params={"dtype": dtype, "persist": False, "max_batch": max_batch})
+    st = HipVectorStore(cfg, index_factory=lambda d: idx)
+    st._ensure_index(D3)
+    st._records, st._metas, st._id_to_row = _LazyTable(N3, False), _LazyTable(N3, True), _Count(N3)
+
+    async def main():
+        return await asyncio.gather(*[st.search(query_embedding=x.tolist(), top_k=10) for x in q])
+
+    try:
+        out = asyncio.run(main())
+        launches, native = st._batcher.launches, st._batcher.native_launches
+    finally:
+        st._batcher.close()  # (not st.close(): the index belongs to the module fixture)
+    for i, res in enumerate(out):
+        want = [f"doc{r // 1000}_chunk_{r % 1000}" for r in r_ref[i, :10].tolist()]
+        assert [c.id for c, _ in res] == want, i
+        got = np.asarray([sc for _, sc in res], np.float32)
+        np.testing.assert_array_equal(got.view(np.uint32), s_ref[i, :10].astype(np.float32).view(np.uint32))
+    print(f"\nstore async, max_batch {max_batch}: {launches} launches, {native} through submit_host")
+    assert native >= 1 and launches <= -(-len(q) // max_batch) + 2
+
+
+def test_c3_call_shapes_bf16_vs_oracle(c3):
+    idx, q, s_ref, r_ref, *_ = c3
+    _call_shapes(idx, q, s_ref, r_ref)
+
+
+@pytest.mark.parametrize("max_batch", [64, 256])
+def test_c3_store_async_256_clients_bf16_vs_oracle(c3, max_batch):
+    idx, q, s_ref, r_ref, q2, s2, r2 = c3
+    _store_async(idx, "bf16", np.concatenate([q, q2]), np.concatenate([s_ref, s2]), np.concatenate([r_ref, r2]),
+                 max_batch)
+
+
 def test_c3_group_8_shards_pipelined_vs_oracle(c3, native):
     """The single-process multi-GPU handle at C3: one handle striped over 8 shards (on a one-GPU box the
     8 shards share the GPU: dev_ids = [0]*8 -- 8 x 1.25M rows, the per-GPU rows of the 8-GPU node), rows
@@ -115,7 +207,7 @@ def test_c3_group_8_shards_pipelined_vs_oracle(c3, native):
     k = 10 and 100, identical to the oracle over all 10M rows."""
     import torch
 
-    _, q, s_ref, r_ref = c3
+    _, q, s_ref, r_ref, *_ = c3
     n_vis = native.device_count()
     devs = [i % n_vis for i in range(8)]
     grp = native.NativeIndex(D3, "bf16", "cosine", devices=devs)
@@ -144,7 +236,7 @@ def test_c3_group_8_shards_pipelined_vs_oracle(c3, native):
 def test_c3_tombstones_and_filter_vs_oracle(c3):
     """Deleted rows (tombstones) and a where-clause bitmap at 10M: a dense random filter (full scan
     with the mask fused into the scan) and a few documents' contiguous row ranges (tile list)."""
-    idx, q, _, _ = c3
+    idx, q, _, _, *_ = c3
     rng = np.random.default_rng(77)
     dead = np.unique(rng.integers(0, N3, 20_000))
     idx.remove(dead)
@@ -175,9 +267,12 @@ def c3_f32(native):
     idx.reserve(N3)
     idx.add_synthetic(SEED3, 0, N3)
     planted, iso = _queries(SEED3, N3, D3, 64, qseed=5151)
+    planted2, iso2 = _queries(SEED3, N3, D3, 64, qseed=5252)
     q = np.concatenate([planted, iso])
-    s_ref, r_ref = oracle.c_search_synthetic(SEED3, 0, N3, D3, "f32", "cosine", R.process_queries(q, "cosine"), 100)
-    yield idx, q, s_ref, r_ref
+    q2 = np.concatenate([planted2, iso2])
+    s_all, r_all = oracle.c_search_synthetic(SEED3, 0, N3, D3, "f32", "cosine",
+                                             R.process_queries(np.concatenate([q, q2]), "cosine"), 100)
+    yield idx, q, s_all[:128], r_all[:128], q2, s_all[128:], r_all[128:]
     idx.close()
 
 
@@ -188,7 +283,7 @@ def test_c3_10M_f32_vs_oracle(c3_f32, k):
     whose window is widest here (isotropic queries over 10M rows).  B = 64 runs k_scan; B = 128 the fp32
     128-query FILTER (asserted through hr_index_wide_launches, row parts at k = 100).  Identical to the oracle's
     exact fp32 answer; the guard counters are printed."""
-    idx, q, s_ref, r_ref = c3_f32
+    idx, q, s_ref, r_ref, *_ = c3_f32
     for B in (64, 128):
         before, w0 = idx.stats(), idx.wide_launches()
         if B == 64:
@@ -202,6 +297,18 @@ def test_c3_10M_f32_vs_oracle(c3_f32, k):
         assert (w1 - w0 > 0) == (B == 128)
         _check(s[:64], r[:64], s_ref[:64, :k], r_ref[:64, :k])    # planted
         _check(s[64:], r[64:], s_ref[64:, :k], r_ref[64:, :k])    # isotropic
+
+
+def test_c3_call_shapes_f32_vs_oracle(c3_f32):
+    idx, q, s_ref, r_ref, *_ = c3_f32
+    _call_shapes(idx, q, s_ref, r_ref)
+
+
+@pytest.mark.parametrize("max_batch", [64, 256])
+def test_c3_store_async_256_clients_f32_vs_oracle(c3_f32, max_batch):
+    idx, q, s_ref, r_ref, q2, s2, r2 = c3_f32
+    _store_async(idx, "f32", np.concatenate([q, q2]), np.concatenate([s_ref, s2]), np.concatenate([r_ref, r2]),
+                 max_batch)
 
 
 # ---------------------------------------------------------------- C2: 1M x 768, f32 and bf16

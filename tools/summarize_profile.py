@@ -89,7 +89,10 @@ def main(src, tag, alg_bytes=None):
         elif e > end:
             busy += e - end
             end = e
-    out = {"tag": tag, "classification": "by kernel name" if {_base(r["Kernel_Name"]) for r in filt_rows} -
+    import datetime
+
+    out = {"tag": tag, "created_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+           "classification": "by kernel name" if {_base(r["Kernel_Name"]) for r in filt_rows} -
            {"k_scan"} else "legacy k_scan: largest grid and > 1/4 of the longest launch",
            "kernels_ms_avg": {k: statistics.mean(v) for k, v in dur.items()},
            "filter_kernels": sorted({_base(r["Kernel_Name"]) for r in filt_rows}),

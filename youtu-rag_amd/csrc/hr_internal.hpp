@@ -13,6 +13,7 @@
 #include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hiprag.h"
@@ -84,7 +85,7 @@ struct PersistLaunch;
 int launch_persist(int mt, int dtype, int P, int cus, const PersistLaunch& pa, int lds, hipStream_t st);
 int launch_persist_post(PersistCtl* c, uint32_t e, hipStream_t st);
 int launch_persist_close(PersistCtl* c, hipStream_t st);
-int launch_persist_wait(PersistCtl* c, int s, uint32_t target, uint32_t* host_err, hipStream_t st);
+int launch_persist_wait(PersistCtl* c, uint32_t e, uint32_t nwg, uint32_t* host_err, hipStream_t st);
 }  // namespace hr
 
 static constexpr int kCap = 8192;       // candidate buffer per query (shared-buffer / collect mode)
@@ -197,6 +198,10 @@ struct hr_index {
         size_t off_s = 0, off_r = 0, off_f = 0, off_k = 0;
         DevBuf q, cand, bound, kth, fail, s, r;
         hipEvent_t q_ready = nullptr, done = nullptr;
+        // the batch's notify host function (hipLaunchHostFunc behind `done`) has not returned yet: collect and
+        // destroy wait for it, so the caller never closes or reuses the fd number while that write is pending
+        std::atomic<int> notify_pending{0};
+        int notify_fd = -1;
     } aslot[2];
     int64_t aticket = 1;
     hipStream_t acopy = nullptr, atail = nullptr;

@@ -296,8 +296,15 @@ struct PersistCtl {                 // device memory; initialised once per index
     uint32_t stop;                  // a quiesce asked the instances to stop admitting
     uint32_t error;                 // a bounded wait gave up (1: instance, 2: tail)
     uint32_t runs;                  // instances that ran (did not find their batch processed already)
-    uint32_t pad[2];
-    uint32_t done[4];               // per slot: workgroup arrivals, monotonic (target = workgroups x epochs of the slot)
+    uint32_t opened;                // the epoch the running instance's leader opened the gate for (release-published)
+    uint32_t pad;
+    // per slot: the tail's wait for the slot's current batch gave up (k_persist_wait) -- k_select then flags every
+    // query of that batch as overflowed, so its guard fails and the exact collect pass answers it (never a partial scan)
+    uint32_t slot_fail[4];
+    // per epoch (index e % ring): (e << 32) | workgroup arrivals, reset to (e << 32) by the epoch's post.  Tagged
+    // rather than a monotonic per-slot count: an epoch that never completed (a failed submit, a timed-out wait) cannot
+    // shift the targets of later batches, and the tail's wait cannot match a stale epoch's count
+    unsigned long long arr[kPersistRing];
     // per-epoch s_memrealtime stamps (index e % ring; the post resets them): the last arrival (the tail's timing),
     // and for hr_index_persist_trace the post, the first and last workgroup start and the first arrival
     unsigned long long t_end[kPersistRing];
@@ -1050,7 +1057,8 @@ static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(
                                                  const uint32_t* __restrict__ mkeys, int np,
                                                  const float* __restrict__ floor_q, int use_groups, int B, int kc,
                                                  uint32_t* __restrict__ sel_rows, int* __restrict__ sel_cnt,
-                                                 float* __restrict__ bound_approx, int* __restrict__ overflow) {
+                                                 float* __restrict__ bound_approx, int* __restrict__ overflow,
+                                                 const uint32_t* __restrict__ force_ovf = nullptr) {
     // all LDS in the dynamic region (G17): 16 B of scalars, then the sort keys
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     int& m_sh = *(int*)smem;
@@ -1072,7 +1080,9 @@ static __global__ __attribute__((unused)) __launch_bounds__(1024) void k_select(
         if (tid == 0) {
             thr_sh = fmaxf(f, floor_q[q]);
             m_sh = 0;
-            ovf_sh = 0;
+            // force_ovf: the persistent FILTER's batch did not complete (k_persist_wait gave up): its candidate
+            // regions are partial, so the batch goes to the exact collect pass through the guard
+            ovf_sh = (force_ovf && __hip_atomic_load(force_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 1 : 0;
         }
     }
     __syncthreads();

@@ -81,6 +81,19 @@ __device__ uint32_t wait_admission(PersistCtl* c, uint32_t e, bool leader, uint3
     }
 }
 
+// one lane, once per workgroup: wait until this instance's leader has opened the gate (opened >= e0; epochs only grow)
+__device__ uint32_t wait_opened(PersistCtl* c, uint32_t e0, uint32_t* host_err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&c->opened, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < e0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHardTicks) {
+            report_error(c, host_err, 1u);
+            return 0u;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return 1u;
+}
+
 // The instance.  pa.e0: the epoch it was launched for (its post has completed: the launch waited for its event).
 template <int MT, int DT, int P>
 __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch pa) {
@@ -88,6 +101,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
     PersistCtl* const c = pa.ctl;
     const int tid = threadIdx.x;
     const bool leader = blockIdx.x == 0 && tid == 0;
+    bool first_wait = true;  // (tid 0) the next admission poll is this workgroup's first
     uint32_t e = pa.e0;
     if (tid == 0) cmd = ld_agent(&c->next_epoch) > e ? 0u : 1u;  // processed by an earlier instance: nothing to do
     __syncthreads();
@@ -95,14 +109,30 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
     if (leader) {
         __hip_atomic_fetch_add(&c->runs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // open the gate for this instance: every batch posted so far is ready (its post followed its SAMPLE); with a
-        // close requested (quiesce), keep it closed -- this instance then serves its own batch only
-        const uint32_t p = ld_agent(&c->posted);
-        st_agent(&c->gate, ld_agent(&c->stop) ? ((e - 1) | kGateClosed) : (p > e ? p : e));
+        // close requested (quiesce), keep it closed -- this instance then serves its own batch only.  A CAS loop, not
+        // a store: a k_persist_post admitting a batch between the read of `posted` and the write would otherwise be
+        // overwritten (that epoch then waited for the idle exit)
+        uint32_t g = ld_agent(&c->gate);
+        for (;;) {
+            const uint32_t p = ld_agent(&c->posted);
+            const uint32_t want = ld_agent(&c->stop) ? ((e - 1) | kGateClosed) : (p > e ? p : e);
+            if (__hip_atomic_compare_exchange_strong(&c->gate, &g, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                break;
+        }
+        // the other workgroups wait for this before their first admission poll (they could otherwise read the previous
+        // instance's closed gate and exit after e0)
+        __hip_atomic_store(&c->opened, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     for (bool first = true;; first = false) {
         const int s = (int)((e - 1) % kPersistSlots);
         if (!first) {
-            if (tid == 0) cmd = wait_admission(c, e, leader, pa.idle_ticks, pa.host_err);
+            if (tid == 0) {
+                cmd = 1u;
+                if (first_wait && !leader) cmd = wait_opened(c, pa.e0, pa.host_err);
+                first_wait = false;
+                if (cmd) cmd = wait_admission(c, e, leader, pa.idle_ticks, pa.host_err);
+            }
             __syncthreads();
             if (!cmd) break;
         }
@@ -128,7 +158,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan_persist(PersistLaunch 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __hip_atomic_fetch_add(&c->done[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&c->arr[e % kPersistRing], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long t = __builtin_amdgcn_s_memrealtime();
             __hip_atomic_fetch_max(&c->t_end[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_min(&c->t_end0[e % kPersistRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -146,6 +176,7 @@ __global__ void k_persist_post(PersistCtl* c, uint32_t e) {
         c->t_start1[r] = 0ull;
         c->t_start0[r] = ~0ull;
         c->t_end0[r] = ~0ull;
+        c->arr[r] = (unsigned long long)e << 32;  // no arrival yet (published by the release below)
         c->t_post[r] = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_max(&c->posted, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -164,17 +195,26 @@ __global__ void k_persist_close(PersistCtl* c) {
     }
 }
 
-// tail stream: wait until every workgroup is through the slot's batch (done[s] >= target)
-__global__ void k_persist_wait(PersistCtl* c, int s, uint32_t target, uint32_t* host_err) {
+// tail stream: wait until all nwg workgroups are through epoch e (its arrival word carries e's tag and nwg arrivals);
+// a wait that gives up marks the slot's batch failed (slot_fail[s], read by the k_select behind it: the batch goes to
+// the exact collect pass)
+__global__ void k_persist_wait(PersistCtl* c, uint32_t e, uint32_t nwg, uint32_t* host_err) {
     if (threadIdx.x != 0) return;
+    const int s = (int)((e - 1) % kPersistSlots);
+    const unsigned long long want = ((unsigned long long)e << 32) | nwg;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(ld_agent(&c->done[s]) - target) < 0) {
+    for (;;) {
+        const unsigned long long v =
+            __hip_atomic_load(&c->arr[e % kPersistRing], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 32) == e && v >= want) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kHardTicks) {
             report_error(c, host_err, 2u);
+            st_agent(&c->slot_fail[s], 1u);
             return;
         }
         __builtin_amdgcn_s_sleep(2);
     }
+    st_agent(&c->slot_fail[s], 0u);
 }
 
 template <int MT, int DT, int P>
@@ -214,8 +254,8 @@ int launch_persist_close(PersistCtl* c, hipStream_t st) {
     return HR_OK;
 }
 
-int launch_persist_wait(PersistCtl* c, int s, uint32_t target, uint32_t* host_err, hipStream_t st) {
-    hipLaunchKernelGGL(k_persist_wait, dim3(1), dim3(64), 0, st, c, s, target, host_err);
+int launch_persist_wait(PersistCtl* c, uint32_t e, uint32_t nwg, uint32_t* host_err, hipStream_t st) {
+    hipLaunchKernelGGL(k_persist_wait, dim3(1), dim3(64), 0, st, c, e, nwg, host_err);
     HIP_TRY(hipGetLastError());
     return HR_OK;
 }

@@ -62,12 +62,17 @@ class RcclComm:
     id goes to every rank with one broadcast over the process group; ncclCommInitRank is collective (every rank
     constructs this at the same point)."""
 
-    def __init__(self, torch, dist, group, device):
+    def __init__(self, torch, dist, group, device, lib=None):
+        """lib: the RCCL library (default: the librccl.so torch loaded); the CPU tests pass a ctypes-shaped stand-in
+        that moves the bytes over gloo, so this G > 1 control flow runs without GPUs."""
         import ctypes
+        import contextlib
         import os
 
         self.ct = ctypes
-        self.lib = lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+        if lib is None:
+            lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+        self.lib = lib
         lib.ncclGetErrorString.restype = ctypes.c_char_p
         for f in ("ncclAllGather", "ncclBroadcast", "ncclCommInitRank", "ncclGetUniqueId", "ncclCommDestroy"):
             getattr(lib, f).restype = ctypes.c_int
@@ -85,7 +90,8 @@ class RcclComm:
         dist.broadcast(buf, src, group=group)
         uid = _Uid.from_buffer_copy(bytes(buf.cpu().numpy().tobytes()))
         self.comm = ctypes.c_void_p()
-        with torch.cuda.device(device):
+        dev = torch.device(device)
+        with torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext():
             self._check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.G, uid, self.rank))
 
     def _check(self, rc: int) -> None:
@@ -154,10 +160,13 @@ class ShardedSearch:
     """Distributed exact top-k over a row-sharded index (torch.distributed group)."""
 
     def __init__(self, index, row_offset: int, max_batch: int, kc: int | None = None, group=None,
-                 device=None, depth: int = 2, max_k: int = 16, overlap: bool = True, force_collective: bool = False):
+                 device=None, depth: int = 2, max_k: int = 16, overlap: bool = True, force_collective: bool = False,
+                 rccl_lib=None):
         """force_collective: run the exchange (all-gather of the packed records, broadcast of src_rank
         batches) through the process group even at world size 1, where it is otherwise a local copy --
-        so a one-GPU box executes the RCCL branch an 8-GPU node runs (bench.py --collective)."""
+        so a one-GPU box executes the RCCL branch an 8-GPU node runs (bench.py --collective).
+        rccl_lib: take the direct-RCCL branch (RcclComm) with this library object whatever the backend (CPU tests of
+        the G > 1 control flow with a stand-in library)."""
         import torch
         import torch.distributed as dist
 
@@ -187,8 +196,11 @@ class ShardedSearch:
         # RCCL itself on the tail / scan streams (RcclComm) when the group is nccl; gloo (CPU tests) goes
         # through torch.distributed with host staging
         self.backend = dist.get_backend(group) if self.collective else None
-        self.rccl = RcclComm(torch, dist, group, self.device) if (self.collective and self.backend == "nccl"
-                                                                   and pinned) else None
+        if self.collective and rccl_lib is not None:
+            self.rccl = RcclComm(torch, dist, group, self.device, lib=rccl_lib)
+        else:
+            self.rccl = RcclComm(torch, dist, group, self.device) if (self.collective and self.backend == "nccl"
+                                                                       and pinned) else None
         self.transport = ("rccl (direct, on the tail stream)" if self.rccl is not None else
                           f"torch.distributed ({self.backend})" if self.collective else "local copy")
 
@@ -244,8 +256,11 @@ class ShardedSearch:
         and deadlock).  From another stream (the fallback's gather, a broadcast before the scan) the tail waits for
         it first and it waits for the tail after -- rare paths; the per-batch gather is issued on the tail."""
         torch = self.torch
+        if self.tail is None:  # (no tail stream: one stream's order already)
+            issue(self._stream())
+            return
         cur = torch.cuda.current_stream(self.device)
-        if self.tail is None or cur == self.tail:
+        if cur == self.tail:
             issue(self._stream())
             return
         self.tail.wait_stream(cur)
@@ -346,7 +361,8 @@ class ShardedSearch:
         group is destroyed)."""
         self.finalize_all()
         if self.rccl is not None:
-            self.torch.cuda.synchronize(self.device)
+            if self.device.type == "cuda":
+                self.torch.cuda.synchronize(self.device)
             self.rccl.close()
             self.rccl = None
 

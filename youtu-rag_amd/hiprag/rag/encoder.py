@@ -155,12 +155,24 @@ class UnpaddedEncoder:
         x = self.emb(input_ids=pk.ids[None], token_type_ids=pk.types[None], position_ids=pk.pos[None])[0]
         return self._layers(x, pk.cu, pk.cu_host, pk.max_len, n)
 
+    def _varlen_layer(self, scale: float, d: int) -> bool:
+        """This layer's attention goes to the flash varlen kernel (its own 1/sqrt(d) scale), which reads the
+        sequence offsets from the device tensor; else SDPA per sequence, sliced by the HOST offsets."""
+        return self.varlen is not None and abs(scale * d ** 0.5 - 1.0) < 1e-6
+
+    def graph_safe(self) -> bool:
+        """Every layer takes the varlen branch, so a captured forward depends on the batch's offsets only through
+        device tensors (GraphedForward copies them in before a replay).  The per-sequence SDPA fallback slices by
+        host offsets, which a capture would bake in (a later batch of the same shape but other lengths
+        then replayed the captured segmentation)."""
+        return all(self._varlen_layer(scale, d) for _, _, _, d, scale, *_ in self.layers)
+
     def _layers(self, h, cu_t, cu_host, max_len, n):
         torch = self.torch
         for w, b, nH, d, scale, attn_out, inter, out in self.layers:
             qkv = torch.nn.functional.linear(h, w, b).view(n, 3, nH, d)
             q, k, v = qkv.unbind(1)  # strided views: the flash kernel takes them as they are (no copies)
-            if self.varlen is not None and abs(scale * d ** 0.5 - 1.0) < 1e-6:  # (the kernel's own 1/sqrt(d))
+            if self._varlen_layer(scale, d):
                 a = self.varlen(q, k, v, cu_t, cu_t, max_len, max_len)
             else:
                 a = _sdpa_per_sequence(q, k, v, cu_host, max_len, scale)
@@ -231,7 +243,8 @@ class GraphedForward:
         key = (len(pk.cu_host) - 1, n, ml)
         ent = self.graphs.get(key)
         if ent is None:
-            if n > self.max_tokens or not pk.ids.is_cuda or len(self.graphs) >= self.max_graphs:
+            if (n > self.max_tokens or not pk.ids.is_cuda or len(self.graphs) >= self.max_graphs
+                    or not self.enc.graph_safe()):  # (host-sliced attention: never captured, see graph_safe)
                 return self.enc.forward_packed(pk)
             ent = self.graphs[key] = self._capture(pk, ml)
         for f in self.enc.observers:  # (a replay runs no Python forward: report the shape here)

@@ -175,7 +175,9 @@ def test_hash_tokenizer_native_text_kernel_matches_python():
         re_mod._NATIVE_TOK = old
 
 
-def test_ingest_pauses_the_cyclic_gc_and_restores_it(tmp_path):
+def test_ingest_keeps_the_cyclic_gc_enabled(tmp_path):
+    """The ingest no longer switches the collector off for its duration (a global side effect
+    on every other coroutine of the serving process)."""
     import gc
 
     seen = []
@@ -189,11 +191,7 @@ def test_ingest_pauses_the_cyclic_gc_and_restores_it(tmp_path):
                             index_params={"dtype": "f32", "persist": False})
     store = HipVectorStore(cfg, index_factory=lambda d: OracleIndex(d, "f32"))
     docs = [Document(id=f"d{i}", content="alpha beta gamma " * 20, metadata={}) for i in range(3)]
-    assert gc.isenabled()
     run(GpuIngestor(store, GcProbe(), chunking=ChunkingConfig(chunk_size=100, chunk_overlap=0)).ingest(docs))
-    assert seen and not any(seen) and gc.isenabled()
-    seen.clear()
-    run(GpuIngestor(store, GcProbe(), pause_gc=False).ingest(docs[:1]))
     assert seen and all(seen) and gc.isenabled()
 
 

@@ -339,6 +339,12 @@ struct XFrag;
 #ifndef HR_CORPUS_NT
 #define HR_CORPUS_NT 1
 #endif
+// HR_DIAG (timing builds only -- results are WRONG with any bit set; tools/gpu diagnostic A/Bs of where a
+// FILTER launch's time goes): 1 no candidate appends, 2 no threshold refreshes after the first, 4 no epilogue at
+// all (group maxima, compares), 8 no query staging into LDS, 16 no MFMA (a cheap XOR keeps the operands live)
+#ifndef HR_DIAG
+#define HR_DIAG 0
+#endif
 // HR_ROTATE_ROUNDS=0 builds the unrotated round-robin dealing (A/B and the regression check of
 // test_periodic_clusters_spread_over_waves only)
 #ifndef HR_ROTATE_ROUNDS
@@ -573,7 +579,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
 
     // stage the query fragments (QB*S KiB) into LDS once per launch; 8 loads in flight per
     // thread (a load->store loop pays one L2 round trip per 8 KiB)
-    stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
+    if (!(HR_DIAG & 8)) stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
     __syncthreads();
 
     if (u0 >= u1 && FILTER) {
@@ -760,7 +766,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
             part_end = (part + 1) * a.part_tiles;
         }
         // a refresh applied in this tile's epilogue: its loads go out now (see refresh_load)
-        const bool rdue = MODE == SCAN_FILTER && a.use_groups && early_refresh &&
+        const bool rdue = MODE == SCAN_FILTER && a.use_groups && early_refresh && !(HR_DIAG & 2) &&
                           ((done + 1 + roff) % a.refresh_every) == 0;
         if (rdue) {
             refresh_load(rkey);
@@ -789,11 +795,35 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const u32x4 qf = qs[((sb + i) * QB + qb) * 64 + lane];
-                    acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
+                    if (HR_DIAG & 16)
+                        acc[qb][i & 15] += __builtin_bit_cast(float, (qf.x ^ xf.x) & 0x3f000000u);
+                    else
+                        acc[qb] = mfma32<MT>(qf, xf, acc[qb]);
                 }
             }
         }
 
+        if constexpr ((HR_DIAG & 4) != 0) {  // timing build: no epilogue, the accumulators only kept live
+            float s = 0.0f;
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s += acc[qb][i];
+            if (s == 1234.5f) a.pcnt[wg] = (uint32_t)t;
+            ++done;
+            if (u + 1 < u_end) {
+                ++u;
+            } else if (pend >= 0 && done < n_units) {
+                in_static = false;
+                u = pend;
+                u_end = std::min<int64_t>(u + a.dyn_chunk, n_units);
+                pend = -1;
+                issued = false;
+            } else {
+                break;
+            }
+            continue;
+        }
         // epilogue: (euclidean) approximate score, predicate, group max, threshold filter
         if (a.xnorm) {
             // euclidean: this tile's row norms, read here and only here -- a vector load issued before
@@ -821,7 +851,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
                 gmax[qb][i] = fmaxf(gmax[qb][i], v);
                 if (FILTER) regs |= (__ballot(ok && v >= th[qb][i]) != 0 ? 1u : 0u) << (qb * 16 + i);
             }
-        if (FILTER && regs) {
+        if (FILTER && regs && !(HR_DIAG & 1)) {
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
@@ -866,7 +896,7 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
                 }
         }
         ++done;
-        if (MODE == SCAN_FILTER && ((done + roff) % a.refresh_every) == 0) {
+        if (MODE == SCAN_FILTER && !(HR_DIAG & 2) && ((done + roff) % a.refresh_every) == 0) {
             if (rdue) refresh_apply(rkey, true, false);
             else refresh(true);
         }

@@ -32,7 +32,10 @@ class Document:
         return f"Document(id={self.id}, content='{_preview(self.content)}', metadata={self.metadata})"
 
 
-@dataclass
+# Chunk and RetrievalResult carry __slots__ (the reference's are plain dataclasses, same fields and order): a search
+# returns one of each per hit, and without a per-instance __dict__ each hit is one tracked object fewer for Python's
+# cycle collector to promote and walk under load (tools/bench_store_host.py)
+@dataclass(slots=True)
 class Chunk:
     id: str
     document_id: str
@@ -46,7 +49,7 @@ class Chunk:
                 f"content='{_preview(self.content)}')")
 
 
-@dataclass
+@dataclass(slots=True)
 class RetrievalResult:
     chunk: Chunk
     score: float

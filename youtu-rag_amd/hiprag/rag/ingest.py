@@ -21,7 +21,6 @@ HierarchicalMarkdownSplitter with the configured chunk size and overlap (process
 """
 from __future__ import annotations
 
-import gc
 import logging
 from typing import Any
 
@@ -58,8 +57,7 @@ class GpuIngestor:
     """split -> embed -> add for a HipVectorStore, batching embedder work across documents."""
 
     def __init__(self, vector_store, embedder: BaseEmbedder, chunker=None, chunking: ChunkingConfig | None = None,
-                 embed_batch: int | None = None, summary_index: bool = True, pack_batches: int = 16,
-                 pause_gc: bool = True):
+                 embed_batch: int | None = None, summary_index: bool = True, pack_batches: int = 16):
         self.vector_store = vector_store
         self.summary_index = bool(summary_index)
         self.embedder = embedder
@@ -75,11 +73,6 @@ class GpuIngestor:
         # runs -- (chunks, vectors, ready event) of the batch embedded but not yet added
         self._inflight = None
         self._add_stream = None
-        # A bulk ingest allocates only objects that survive it (chunks, metadata dicts, row records) and
-        # no reference cycles, so each full collection Python runs in between walks them all for nothing
-        # (~0.3 s apiece at 100k chunks, the GPU idling meanwhile): the cyclic collector is paused for
-        # the call and restored after (pause_gc=False leaves it alone)
-        self.pause_gc = bool(pause_gc)
 
     def split(self, document: Document, metadata: dict[str, Any] | None = None) -> list[Chunk]:
         chunker = self.chunker
@@ -126,9 +119,6 @@ class GpuIngestor:
     async def ingest(self, documents: list[Document], metadata: dict[str, Any] | None = None) -> int:
         """Many documents; embedder batches span document boundaries.  Returns chunks created."""
         created, pending, pending_docs = 0, [], set()
-        paused = self.pause_gc and gc.isenabled()
-        if paused:
-            gc.disable()
         try:
             with self.vector_store.deferred_save():
                 for doc in documents:
@@ -151,9 +141,6 @@ class GpuIngestor:
             # would otherwise store it silently, after newer data)
             self._inflight = None
             raise
-        finally:
-            if paused:
-                gc.enable()
         return created
 
     async def _one(self, doc: Document, metadata, pending: list[Chunk]) -> int:

@@ -280,12 +280,6 @@ class HipVectorStore(BaseVectorStore):
         self._batcher = _SearchBatcher(self, int(params.get("max_batch", 64)), int(params.get("search_depth", 2)))
         # unfiltered batches launched from the event loop through the asynchronous native entry point
         self.native_async = bool(params.get("native_async", True))
-        # after a bulk load (>= gc_freeze_rows rows since the last freeze) the process's tracked objects move to
-        # the collector's permanent generation (gc.freeze); see _after_bulk_load.  index_params gc_freeze: false
-        # leaves the collector alone
-        self.gc_freeze = bool(params.get("gc_freeze", True))
-        self.gc_freeze_rows = int(params.get("gc_freeze_rows", 100_000))
-        self._rows_since_freeze = 0
         self._lock = threading.RLock()
         self._paths = P.Paths(config.persist_directory, config.collection_name)
         self._gen = 0
@@ -399,8 +393,6 @@ class HipVectorStore(BaseVectorStore):
             self._defer -= 1
             if self._defer == 0 and self._dirty:
                 self.flush()
-            if self._defer == 0:
-                self._after_bulk_load()
 
     def flush(self):
         """Write a new snapshot generation now (folds the journal in)."""
@@ -492,9 +484,6 @@ class HipVectorStore(BaseVectorStore):
             live[: len(self._live)] = self._live
             self._live = live
         self._live[first:n] = [rec is not None for rec in records]
-        self._rows_since_freeze += len(records)
-        if self._defer == 0:
-            self._after_bulk_load()
         if self.keep_embeddings:
             if self._raw is None or len(self._raw) < n:
                 raw = np.zeros((max(n, 2 * (0 if self._raw is None else len(self._raw)), 1024), self.dim), np.float32)
@@ -503,24 +492,6 @@ class HipVectorStore(BaseVectorStore):
                 self._raw = raw
             if vectors is not None:
                 self._raw[first:n] = vectors
-
-    def _after_bulk_load(self):
-        """gc.freeze() once a bulk load is in (>= gc_freeze_rows rows appended since the last freeze).
-
-        Every search hit is a new Chunk and a (Chunk, score) tuple -- tracked objects, by the API's types -- that
-        live until the caller drops them, so they reach the collector's oldest generation, and each full collection
-        then walks the whole process heap: 84 ms over a serving process's ~190k long-lived objects (torch alone is
-        ~170k), several times a second at 20k queries/s (profiles/r03_async_store_10M_gc.jsonl: 12.5k QPS at 256
-        clients, 20.2k with the application calling gc.freeze()).  Freezing moves the objects alive now (imports,
-        the loaded collection) into the permanent generation, so full collections walk only what was allocated
-        since: the standard serving recipe, done here once per bulk load so an unmodified application gets it.
-        Garbage cycles alive at the freeze are kept (not collected); index_params gc_freeze: false opts out."""
-        if not self.gc_freeze or self._rows_since_freeze < self.gc_freeze_rows:
-            return
-        import gc
-
-        gc.freeze()
-        self._rows_since_freeze = 0
 
     def _register(self, fresh: list[Chunk], first: int, vectors: np.ndarray | None):
         records = [self._record(c) for c in fresh]
@@ -774,8 +745,8 @@ class HipVectorStore(BaseVectorStore):
     def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
         """(Chunk, score) lists of a finished batch.  Runs on the event loop while the next launch is in
         flight, so it is the host's per-hit cost under load: the hits' host records are gathered for the
-        whole batch at once (object-array fancy indexing instead of a Python lookup per row and field) and
-        each Chunk is built straight into its __dict__ (a fresh metadata dict per hit, as Chroma returns)."""
+        whole batch at once (object-array fancy indexing instead of a Python lookup per row and field); each hit is
+        a slotted Chunk (two tracked objects per hit with its tuple) with a fresh metadata dict, as Chroma returns."""
         raw, (recs, metas, epoch) = ran
         n = len(prep[0])
         if raw is None or epoch != self._epoch:  # cleared since the search ran: its rows are gone
@@ -800,7 +771,7 @@ class HipVectorStore(BaseVectorStore):
             embs = [None] * len(rec_l)
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
-        new, C = object.__new__, Chunk
+        C = Chunk
         out, i = [], 0
         for cnt in per_q:  # one pass: each query's hits straight into its list
             res = []
@@ -809,11 +780,8 @@ class HipVectorStore(BaseVectorStore):
                 if r is None:
                     continue
                 m = meta_l[j]
-                c = new(C)
-                c.__dict__ = {"id": r[0], "document_id": m.get("document_id", ""), "content": r[2],
-                              "chunk_index": m.get("chunk_index", 0), "metadata": dict(m),
-                              "embedding": None if embs is None else embs[j]}
-                res.append((c, score_l[j]))
+                res.append((C(r[0], m.get("document_id", ""), r[2], m.get("chunk_index", 0), dict(m),
+                              None if embs is None else embs[j]), score_l[j]))
             out.append(res)
             i += cnt
         return out

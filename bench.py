@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--recall-queries", type=int, default=64, help="planted and isotropic queries of the recall checks")
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline, recall and the GPU embed leg (quick runs)")
     p.add_argument("--no-embed", action="store_true", help="skip the GPU embed+search leg")
+    p.add_argument("--embed-cus", default="48,64,96,128",
+                   help="CU shares of the query embedder in the embed+search leg's CU-split runs ('' = none)")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
     p.add_argument("--collective", action="store_true",
                    help="run the exchange through an RCCL process group even at --gpus 1 (world size 1): the timed "
@@ -69,6 +71,8 @@ def parse():
     p.add_argument("--persist", type=int, default=1, choices=(0, 1, 2),
                    help="persistent FILTER for the pipelined shard batches: 0 off (one FILTER launch per batch), "
                         "1 shards of 4.2M-5.1M rows (default: where it measured faster), 2 every shard size")
+    p.add_argument("--q256", type=int, default=1, choices=(0, 1),
+                   help="129-256-query batches: the 256-query FILTER (1, default) or two 128-query FILTER launches (0)")
     p.add_argument("--depth", type=int, default=2,
                    help="batches in flight per rank (ShardedSearch depth): the host waits for batch i's guard flags "
                         "when it submits batch i + depth")
@@ -276,14 +280,88 @@ def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> 
     torch.cuda.synchronize()
     t_pipe = (time.perf_counter() - t0) / n_batches
     tflops = flops["executed"] / n_batches / t_embed / 1e12
+    # the same pipeline with the GPU split by CU (VERDICT r04 missing #4): the compute-bound forward on its own CUs
+    # (a CU-masked stream), the HBM-bound scan -- prep, SAMPLE, FILTER, select, rescore, merge -- on the others
+    # (hr_index_set_cu_mask for the index's streams, masked scan / tail streams for ShardedSearch), so the two
+    # overlap instead of contending for every CU
+    split = {}
+    q_last = keep[-1][0].float().cpu().numpy()  # the last batch's embedded queries (shared-CU run)
+    if args.embed_cus:
+        split = embed_search_cu_split(args, searcher, emb, texts[2:], dev, K, B, s_out, r_out)
+    best = min([(t_pipe, None)] + [(v["ms_per_batch"] / 1e3, n) for n, v in split.items()])
+    # the embedded queries' answers against the oracle over all rows (the last batch, as the pipelined runs left it)
+    import oracle
+    from oracle import ref_numpy as R
+
+    s_ref, r_ref = oracle.c_search_synthetic(args.seed, 0, args.rows, D, args.dtype, "cosine",
+                                             R.process_queries(q_last, "cosine"), K)
+    oracle_ok = bool(np.array_equal(r_out[-1].cpu().numpy(), r_ref)
+                     and np.array_equal(s_out[-1].cpu().numpy(), s_ref.astype(np.float32)))
     return {"model": f"{args.cpu_embed_preset} shape (random init), bf16, unpadded forward + K7", "batch": B,
             "batches": n_batches, "tokens_per_batch": round(flops["tokens_real"] / n_batches, 1),
             "embed_ms_per_batch": round(1000 * t_embed, 3), "embed_tflops": round(tflops, 1),
             "embed_graphs": len(emb.graphed.graphs) if emb.graphed is not None else 0,
             "embed_frac_of_bf16_peak": round(tflops / MFMA_PEAK_TFLOPS, 4),
             "sequential": {"ms_per_batch": round(1000 * t_seq, 3), "qps": round(B / t_seq, 1)},
-            "pipelined": {"ms_per_batch": round(1000 * t_pipe, 3), "qps": round(B / t_pipe, 1)},
+            "pipelined": {"ms_per_batch": round(1000 * best[0], 3), "qps": round(B / best[0], 1),
+                          "embed_cus": best[1], "shared_cus_ms_per_batch": round(1000 * t_pipe, 3)},
+            "pipelined_cu_split": split,
+            "last_batch_ids_identical_to_oracle": oracle_ok,
             "path": "embed_query -> search (base_retriever.py:57-62), embedding + exact scan on the GPU"}
+
+
+def embed_search_cu_split(args, searcher, emb, texts, dev, K, B, s_out, r_out) -> dict:
+    """gpu_embed_plus_search's pipelined leg with the CUs partitioned: for each embed share n in --embed-cus, the
+    embedder runs on a stream masked to n CUs spread evenly over the chip (CU i with i * n // n_cu stepping), and the
+    index's internal streams plus ShardedSearch's scan and tail streams on the rest.  Every batch's answers are
+    checked against the shared-CU run's (same embeddings, so identical ids and scores).  Returns
+    {n: {ms_per_batch, qps}}."""
+    import torch
+
+    from hiprag import _native
+
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    ref_s, ref_r = s_out.clone(), r_out.clone()
+    out = {}
+    for n in (int(x) for x in args.embed_cus.split(",")):
+        if not 16 <= n <= n_cu - 48:
+            continue
+        e_cus = sorted({(i * n_cu) // n for i in range(n)})
+        s_cus = [c for c in range(n_cu) if c not in set(e_cus)]
+        raw = [_native.create_cu_stream(dev.index or 0, e_cus), _native.create_cu_stream(dev.index or 0, s_cus),
+               _native.create_cu_stream(dev.index or 0, s_cus)]
+        es, scan, tail = (torch.cuda.ExternalStream(r, device=dev) for r in raw)
+        tail0 = searcher.tail
+        try:
+            searcher.index.set_cu_mask(s_cus)
+            searcher.tail = tail
+            keep = []
+            for rep in range(2):  # (the first pass warms the masked streams)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i, t in enumerate(texts):
+                    with torch.cuda.stream(es):
+                        q = emb.embed_queries_device(t)
+                        ev = torch.cuda.Event()
+                        ev.record(es)
+                    keep.append((q, ev))
+                    scan.wait_event(ev)
+                    with torch.cuda.stream(scan):
+                        searcher.submit(q, K, s_out=s_out[i], r_out=r_out[i], q_ready=ev)
+                searcher.finalize_all()
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / len(texts)
+            ok = bool(torch.equal(s_out, ref_s) and torch.equal(r_out, ref_r))
+            out[str(n)] = {"ms_per_batch": round(1000 * dt, 3), "qps": round(B / dt, 1), "search_cus": len(s_cus),
+                           "results_identical_to_shared": ok}
+        finally:
+            searcher.finalize_all()
+            torch.cuda.synchronize()
+            searcher.tail = tail0
+            searcher.index.set_cu_mask(None)
+            for r in raw:
+                _native.destroy_stream(r)
+    return out
 
 
 def isotropic_queries(B: int, D: int, seed: int = 7) -> np.ndarray:
@@ -522,6 +600,7 @@ def main():
     t0 = time.time()
     index = _native.NativeIndex(D, args.dtype, "cosine", device=local)
     index.set_persist(args.persist)
+    index.set_q256(bool(args.q256))
     index.reserve(n_local)
     index.add_synthetic(args.seed, start, n_local)
     torch.cuda.synchronize()
@@ -554,7 +633,7 @@ def main():
     # three records: before SAMPLE, between the two, after FILTER): each event record leaves a
     # ~6 us bubble on the scan stream, so timing every launch would slow the steps being measured
     index.set_scan_timing(TIME_EVERY)
-    wide0 = index.wide_launches()
+    wide0, q2560 = index.wide_launches(), index.q256_launches()
     persist0 = index.persist_stats()["batches"]
     fb0 = searcher.fallback_queries
     wait0 = searcher.wait_s
@@ -571,6 +650,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     sample_ms, scan_ms = index.take_scan_times()
     wide_per_step = (index.wide_launches() - wide0) / args.steps  # 128-query FILTER launches per batch
+    q256_per_step = (index.q256_launches() - q2560) / args.steps  # 256-query FILTER launches per batch
     pst = index.persist_stats()
     if pst["error"]:
         raise RuntimeError(f"persistent FILTER error {pst['error']}")
@@ -617,6 +697,7 @@ def main():
     # FILTER launches per batch (the timed events bracket them all): 65-128 queries are one launch of the 128-query
     # FILTER (hr_wide.hip), 129-256 two -- counted by the index (hr_index_wide_launches); otherwise one launch
     wide = wide_per_step > 0
+    q256 = q256_per_step > 0
     passes = max(1, round(wide_per_step)) if wide else 1
     achieved = passes * alg_bytes / (scan_avg * 1e-3) / 1e9 if scan_avg > 0 else 0.0
     mfma_flops = 2 * 32 * -(-B // 32) * n_max_local * D  # padded query slots x rows x dims per FILTER launch
@@ -644,7 +725,8 @@ def main():
         "ranks_agree": ranks_agree, "result_sha256": digest,
         "rccl_ranks": searcher.rccl.G if searcher.rccl is not None else None,
         "roofline": {"bound": "hbm",
-                     "kernel": ("k_filter_wide8 (128-query FILTER)" if wide else
+                     "kernel": ("k_filter_q256 (256-query FILTER: one pass for four 64-query groups)" if q256 else
+                                "k_filter_wide8 (128-query FILTER)" if wide else
                                 "k_scan_persist (persistent FILTER; per-batch time = period between the device stamps "
                                 "of consecutive batches' last workgroup arrivals)" if persist else "k_scan_filter (FILTER pass)"),
                      "filter_launches_per_batch": passes, "achieved": round(achieved, 1),

@@ -237,6 +237,15 @@ int hr_index_set_persist(hr_index* h, int mode);
 int hr_index_persist_close(hr_index* h);
 int hr_index_persist_stats(hr_index* h, int64_t out[3]);
 int hr_index_persist_trace(hr_index* h, int n, double* out, int* n_out);
+/* CU partitioning (no reference counterpart: the reference's embedder and store are separate services, here the
+ * query embedder's forward and the scan share one GPU -- base_retriever.py:57-63 embed_query -> search).
+ * set_cu_mask: this index's internal streams run on the CUs of `mask` only (bit i of word j = CU 32 j + i;
+ * n_words = 0: all CUs) and its launch grids are sized for that many CUs; blocks while asynchronous batches are
+ * in flight (HR_E_BUSY).  stream_create_cu_mask: a stream restricted the same way (the caller's scan / tail /
+ * embedder streams), released with hr_stream_destroy. */
+int hr_index_set_cu_mask(hr_index* h, const uint32_t* mask, int n_words);
+int hr_stream_create_cu_mask(int device, const uint32_t* mask, int n_words, void** stream_out);
+int hr_stream_destroy(void* stream);
 /* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
  * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
 int hr_index_set_scan_timing(hr_index* h, int every);
@@ -263,6 +272,12 @@ int hr_index_graph_replays(hr_index* h, int64_t* out);
 /* Diagnostics: 128-query FILTER launches issued so far (65..256-query chunks at D = 256..1024; graph replays
  * not counted) -- tests use it to check which FILTER served a batch. */
 int hr_index_wide_launches(hr_index* h, int64_t* out);
+/* The 256-query FILTER (hr_q256.hip: 129-256-query batches, bf16 / f16 rows, D = 256..1024, k <= 16, no tile
+ * list -- one corpus pass for four 64-query groups, VectorRetriever.batch_retrieve / the store's micro-batches of up
+ * to 256 single-query calls, base_retriever.py:96-98, chroma_store.py:118-120).  set_q256(h, 0) sends those batches
+ * to two 128-query FILTER launches instead (A/B); q256_launches counts its launches (graph replays not counted). */
+int hr_index_set_q256(hr_index* h, int on);
+int hr_index_q256_launches(hr_index* h, int64_t* out);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

@@ -977,13 +977,16 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
         stored = oracle.c_build_synthetic(9, 0, n, dim, dtype, metric)
         qn = R.process_queries(q, metric)
         allowed = rng.random(n) < 0.7
+        # 129-256 queries with one row part on 16-bit rows: the 256-query FILTER (hr_q256.hip) instead
+        q256_expected = dtype != "f32" and n_parts == 1 and B > 128
         for m in (None, allowed):
             mk = None if m is None else oracle.mask_from_bool(m)
-            w0 = idx.wide_launches()
+            w0, x0 = idx.wide_launches(), idx.q256_launches()
             s, r = idx.search(q, k, mk)
             _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk, metric=metric))
             if m is None:
-                assert (idx.wide_launches() > w0) == wide_expected
+                assert (idx.q256_launches() > x0) == q256_expected
+                assert (idx.wide_launches() > w0) == (wide_expected and not q256_expected)
         parts = [idx.search(q[i:i + 64], k) for i in range(0, B, 64)]
         s, r = idx.search(q, k)
         np.testing.assert_array_equal(r, np.concatenate([p[1] for p in parts]))
@@ -996,6 +999,72 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
             _check(s, r, *oracle.c_search(stored, dtype, qn, k, oracle.mask_from_bool(live), metric=metric))
         if n > 500_000:
             break  # (one metric at a million rows)
+
+
+# ---------------------------------------------------------------- the 256-query FILTER (hr_q256.hip)
+@pytest.mark.parametrize("dim,dtype,n,B,k", [(1024, "bf16", 200_003, 256, 10), (768, "bf16", 150_001, 256, 16),
+                                             (512, "f16", 100_000, 200, 10), (256, "bf16", 70_001, 129, 5),
+                                             (1024, "bf16", 5_000, 256, 10), (1024, "f16", 64, 256, 3),
+                                             (768, "bf16", 1_000_003, 256, 10)])
+def test_q256_filter_vs_oracle(native, dim, dtype, n, B, k):
+    """129-256 queries, one row part, 16-bit rows: ONE launch of the 256-query FILTER scores every tile for four
+    64-query groups (two tiles per wave, query windows through LDS-DMA).  Fewer tiles than one round (5k and 64
+    rows: waves on zero-record V#s), padded groups (B = 129, 200), cosine / ip / euclidean, a dense mask, deleted
+    rows -- identical to the oracle and to the same batch through two 128-query FILTER launches (set_q256(False))."""
+    rng = np.random.default_rng(dim + B + n + 1)
+    metrics = ("cosine", "ip", "euclidean") if dtype == "bf16" and n < 500_000 else ("cosine",)
+    for metric in metrics:
+        idx = native.NativeIndex(dim, dtype, metric)
+        idx.add_synthetic(31, 0, n)
+        raw = R.gen_rows(31, 0, n, dim)
+        nq = min(B // 2, n)
+        q = np.concatenate([_planted_queries(raw, nq, rng), rng.standard_normal((B - nq, dim)).astype(np.float32)])
+        stored = oracle.c_build_synthetic(31, 0, n, dim, dtype, metric)
+        qn = R.process_queries(q, metric)
+        allowed = rng.random(n) < 0.8
+        for m in (None, allowed):
+            mk = None if m is None else oracle.mask_from_bool(m)
+            x0 = idx.q256_launches()
+            s, r = idx.search(q, k, mk)
+            _check(s, r, *oracle.c_search(stored, dtype, qn, k, mk, metric=metric))
+            assert idx.q256_launches() == x0 + 1
+        idx.set_q256(False)
+        w0, x0 = idx.wide_launches(), idx.q256_launches()
+        s2, r2 = idx.search(q, k)
+        assert idx.q256_launches() == x0 and idx.wide_launches() == w0 + 2
+        idx.set_q256(True)
+        s, r = idx.search(q, k)
+        np.testing.assert_array_equal(r, r2)
+        np.testing.assert_array_equal(s, s2)
+        if n > 1000:
+            gone = np.arange(n // 4, n // 4 + n // 9)
+            idx.remove(gone)
+            live = np.ones(n, bool)
+            live[gone] = False
+            s, r = idx.search(q, k)
+            _check(s, r, *oracle.c_search(stored, dtype, qn, k, oracle.mask_from_bool(live), metric=metric))
+        idx.close()
+
+
+def test_q256_filter_periodic_clusters(native):
+    """Clusters repeating every 4096 rows (a factor of the 256-query FILTER's wave count): the rotated two-tile
+    dealing spreads them, the private regions hold, and the answer is the oracle's."""
+    dim, n, B, C = 256, 2_000_000, 256, 4096
+    rng = np.random.default_rng(29)
+    centers = rng.standard_normal((C, dim)).astype(np.float32)
+    centers /= np.linalg.norm(centers, axis=1, keepdims=True)
+    noise = R.gen_rows(47, 0, n, dim)
+    noise /= np.linalg.norm(noise, axis=1, keepdims=True)
+    raw = centers[(np.arange(n, dtype=np.int64) * 2654435761) % C] + 0.7 * noise
+    idx = native.NativeIndex(dim, "bf16", "cosine")
+    idx.add(raw)
+    stored = R.process_rows(raw, "cosine", "bf16")
+    q = (raw[rng.choice(n, B, replace=False)] + 0.1 * rng.standard_normal((B, dim))).astype(np.float32)
+    before, x0 = idx.stats()["guard_failures"], idx.q256_launches()
+    s, r = idx.search(q, 10)
+    _check(s, r, *oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), 10))
+    assert idx.q256_launches() == x0 + 1
+    assert idx.stats()["guard_failures"] - before <= B // 8
 
 
 def test_wide_filter_periodic_clusters(native):

@@ -23,6 +23,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(LIB) or not shutil.which("/op
 # kernels that must not spill VGPRs at all, and the 128-query FILTER's known spills (not to grow)
 NO_SPILL = re.compile(r"k_scan_(filter|sample|collect|persist)")
 WIDE = re.compile(r"k_filter_wide8")
+Q256 = re.compile(r"k_filter_q256")
 
 
 @pytest.fixture(scope="module")
@@ -46,3 +47,14 @@ def test_wide_filter_spills_bounded(resources):
     assert len(wide) == 32, sorted(wide)
     worst = max(v.get("vgpr_spill_count", 0) for v in wide.values())
     assert worst <= 35, worst
+
+
+def test_q256_filter_does_not_spill(resources):
+    """The 256-query FILTER holds 256 accumulators in AGPRs and the corpus ring in VGPRs at one wave per SIMD: its
+    first builds spilled the ring to scratch (a rolled span loop) and then the accumulators (the register allocator
+    copying whole accumulators out of the AGPRs ahead of the epilogue) -- neither may come back."""
+    q = {k: v for k, v in resources.items() if Q256.search(k)}
+    assert len(q) == 8, sorted(q)
+    spilled = {k: v.get("vgpr_spill_count", 0) for k, v in q.items() if v.get("vgpr_spill_count", 0)}
+    assert not spilled, spilled
+    assert all(v.get("private_segment_fixed_size", 0) == 0 for v in q.values()), q

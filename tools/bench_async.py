@@ -79,9 +79,15 @@ def main():
     p.add_argument("--seconds", type=float, default=3.0)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--native-async", default="1", help="0/1 list: event-loop native launches (1) or worker threads (0)")
+    p.add_argument("--torch", type=int, default=1,
+                   help="import torch first: a serving process's heap (the in-process embedder), ~170k tracked objects "
+                        "that every full collection walks unless the application froze them")
     args = p.parse_args()
 
     import gc
+
+    if args.torch:
+        import torch  # noqa: F401
 
     import numpy as np
 

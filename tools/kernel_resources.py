@@ -47,7 +47,8 @@ def kernel_resources(lib: str) -> dict[str, dict]:
                 key, val = m.groups()
                 if key == "name" and not val.endswith(".kd"):
                     cur = out.setdefault(val, {})
-                elif cur is not None and key in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "agpr_count"):
+                elif cur is not None and key in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "agpr_count",
+                                                     "private_segment_fixed_size"):
                     cur[key] = int(val)
     return out
 

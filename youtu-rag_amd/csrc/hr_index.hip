@@ -49,6 +49,17 @@ struct Persist {
 static int persist_quiesce(hr_index* h);  // blocking: every instance has exited (mutations, destroy)
 static int persist_close(hr_index* h);    // non-blocking: the running instance exits once through its batches
 
+// ---------------------------------------------------------------- streams
+hipError_t index_stream_create(const hr_index* h, hipStream_t* s, bool high_priority) {
+    if (!h->cu_mask.empty())
+        return hipExtStreamCreateWithCUMask(s, (uint32_t)h->cu_mask.size(), h->cu_mask.data());
+    if (!high_priority) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
 // ---------------------------------------------------------------- create / grow
 extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out) {
     if (!out) return set_err(HR_E_INVALID, "out is null");
@@ -496,6 +507,27 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
     // two groups (hr_wide.hip) instead of one workgroup per group streaming the same tiles through L2
     if constexpr (MODE == SCAN_FILTER) {
         if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups) {
+            // 129-256 queries (four groups), one row part: ONE pass of the 256-query FILTER (hr_q256.hip) instead of
+            // two of the 128-query one
+            if (pl.NG == 4 && a.np == 1 && h->q256 && q256_filter_ok(h->dtype, h->S)) {
+                const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (a.n_units + 7) / 8));
+                const int64_t W = (int64_t)blocks * 4;  // waves: one candidate region per (group, wave)
+                HIP_TRY(sc.pbuf.ensure((size_t)4 * 64 * W * kCapW * sizeof(float2)));
+                HIP_TRY(sc.pcnt.ensure((size_t)4 * 64 * W * 4));
+                sc.last_W = W;
+                sc.last_Bp = 64;
+                sc.last_ng = 4;
+                sc.last_capw = kCapW;
+                sc.wtiles_valid = false;
+                h->last_scr = &sc;
+                ScanArgs b = a;
+                b.pbuf = sc.pbuf.as<float2>();
+                b.pcnt = sc.pcnt.as<uint32_t>();
+                b.capw = kCapW;
+                if (int rc = launch_filter_q256(MT, DT, h->S, blocks, b, st)) return set_err(rc, "256-query FILTER launch failed");
+                h->n_q256++;
+                return HR_OK;
+            }
             // waves: one candidate region per (group, wave); a wave takes one tile per round
             constexpr int wpb = 8;
             const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (a.n_units + wpb - 1) / wpb));
@@ -647,9 +679,7 @@ static int persist_configure(hr_index* h, const Plan& pl) {
     if (int rc = persist_quiesce(h)) return rc;
     if ((n_tiles + 7) / 8 < nwg) return set_err(HR_E_UNSUPPORTED, "shard too small for the persistent FILTER");
     if (!ps.pst) {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&ps.pst, hipStreamNonBlocking, hi));
+        HIP_TRY(index_stream_create(h, &ps.pst, true));
         for (auto& e : ps.posted) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ps.closed, hipEventDisableTiming));
         HIP_TRY(hipHostMalloc((void**)&ps.host_err, 64));
@@ -785,9 +815,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
             // highest priority: a stream of its own priority class gets its own hardware queue even
             // when the (GPU_MAX_HW_QUEUES = 4) normal-priority queues are shared by many streams --
             // sharing one with the scan stream would serialise the early SAMPLE behind the FILTER
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&h->pre, hipStreamNonBlocking, hi));
+            HIP_TRY(index_stream_create(h, &h->pre, true));
         }
         sp = h->pre;
     }
@@ -837,9 +865,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     hipStream_t sf = st;  // stream of the FILTER scan
     if (dual) {
         if (!sc.scan) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&sc.scan, hipStreamNonBlocking, hi));
+            HIP_TRY(index_stream_create(h, &sc.scan, true));
         }
         sf = sc.scan;
     }
@@ -1277,7 +1303,7 @@ static int sync_graph_search(hr_index* h, const float* q, int B, int k, float* s
         HIP_TRY(h->sync_out.ensure(up(sb) + rb));
         // captured on a stream of its own: a failed capture can leave its stream unusable
         hipStream_t cs = nullptr;
-        HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        HIP_TRY(index_stream_create(h, &cs, false));
         const uint64_t gen0 = g_buf_gen.load();
         uint8_t* pin = (uint8_t*)h->pin;
         float* s_dev = h->sync_out.as<float>();
@@ -1457,8 +1483,8 @@ extern "C" int hr_index_search_submit_host(hr_index* h, const float* q, int B, i
     auto& sl = *free_slot;
     if (int rc = set_device(h)) return rc;
     if (int rc = persist_close(h)) return rc;
-    if (!h->atail) HIP_TRY(hipStreamCreateWithFlags(&h->atail, hipStreamNonBlocking));
-    if (!h->acopy) HIP_TRY(hipStreamCreateWithFlags(&h->acopy, hipStreamNonBlocking));
+    if (!h->atail) HIP_TRY(index_stream_create(h, &h->atail, false));
+    if (!h->acopy) HIP_TRY(index_stream_create(h, &h->acopy, false));
     if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     if (!sl.q_ready) HIP_TRY(hipEventCreateWithFlags(&sl.q_ready, hipEventDisableTiming));
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -2107,6 +2133,59 @@ extern "C" int hr_index_set_persist(hr_index* h, int mode) {
     return HR_OK;
 }
 
+// Restrict this index's kernels to a set of CUs (include/hiprag.h): every internal stream is recreated on the mask
+// and the launch grids are sized for its CU count, so a compute-bound neighbour (the query embedder's forward) can
+// own the other CUs instead of contending for all of them.  n_words == 0 lifts the restriction.  The caller's own
+// streams (hr_index_search_device / _shard's stream arguments) are the caller's to mask (hr_stream_create_cu_mask).
+extern "C" int hr_index_set_cu_mask(hr_index* h, const uint32_t* mask, int n_words) {
+    if (!h || n_words < 0 || n_words > 64 || (n_words > 0 && !mask)) return set_err(HR_E_INVALID, "bad CU mask");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "CU masks: single-device indexes");
+    if (int rc = set_device(h)) return rc;
+    for (auto& sl : h->aslot)
+        if (sl.busy) return set_err(HR_E_BUSY, "asynchronous batches in flight: collect them first");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, h->device));
+    int n = 0;
+    for (int i = 0; i < n_words; ++i) n += __builtin_popcount(mask[i]);
+    if (n_words > 0 && (n < 16 || n > prop.multiProcessorCount)) return set_err(HR_E_INVALID, "a CU mask needs 16..n_cu CUs");
+    persist_free(h);  // (quiesces; re-created on the next persistent batch, on the new streams)
+    HIP_TRY(hipDeviceSynchronize());
+    for (hipStream_t* s : {&h->pre, &h->atail, &h->acopy})
+        if (*s) {
+            (void)hipStreamDestroy(*s);
+            *s = nullptr;
+        }
+    for (auto& sc : h->scr)
+        if (sc.scan) {
+            (void)hipStreamDestroy(sc.scan);
+            sc.scan = nullptr;
+        }
+    h->cu_mask.assign(mask, mask + n_words);
+    hipStream_t ns = nullptr;
+    HIP_TRY(index_stream_create(h, &ns, false));
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    h->stream = ns;
+    h->n_cu = n_words > 0 ? n : prop.multiProcessorCount;
+    return HR_OK;
+}
+
+// a stream of `device` whose kernels run on the CUs of `mask` only (bit i of word j: CU 32 j + i); release with
+// hr_stream_destroy
+extern "C" int hr_stream_create_cu_mask(int device, const uint32_t* mask, int n_words, void** stream_out) {
+    if (!mask || n_words <= 0 || n_words > 64 || !stream_out) return set_err(HR_E_INVALID, "bad CU mask");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
+    *stream_out = (void*)s;
+    return HR_OK;
+}
+
+extern "C" int hr_stream_destroy(void* stream) {
+    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return HR_OK;
+}
+
 // no further batch for now: a running persistent FILTER instance exits once through the batches it was given
 // (instead of after its idle timeout); returns at once
 extern "C" int hr_index_persist_close(hr_index* h) {
@@ -2230,6 +2309,24 @@ extern "C" int hr_index_wide_launches(hr_index* h, int64_t* out) {
     *out = h->n_wide;
     for (hr_index* s : h->shards)
         if (s != h) *out += s->n_wide;
+    return HR_OK;
+}
+
+// 256-query FILTER: on (default) / off (129-256-query batches then take two 128-query FILTER launches)
+extern "C" int hr_index_set_q256(hr_index* h, int on) {
+    if (!h) return set_err(HR_E_INVALID, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->q256 = on != 0;
+    for (hr_index* s : h->shards) s->q256 = on != 0;
+    return HR_OK;
+}
+
+extern "C" int hr_index_q256_launches(hr_index* h, int64_t* out) {
+    if (!h || !out) return set_err(HR_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int64_t n = h->n_q256;
+    for (hr_index* s : h->shards) n += s->n_q256;
+    *out = n;
     return HR_OK;
 }
 

@@ -79,6 +79,10 @@ int launch_filter_wide(int mt, int dtype, int S, int cus, const ScanArgs& a, hip
 // streamed window buffers (2 x 32 KiB, or 2 x 16 KiB for fp32 rows): at most 5 (bf16 / f16) or 7 (fp32) parts,
 // kc <= 160 / 224
 constexpr int wide_max_parts(int dtype) { return dtype == F32 ? 7 : 5; }
+// hr_q256.hip: the 256-query FILTER (four 64-query groups in one pass; bf16 / f16 rows, D = 256..1024, one row
+// part); candidate regions [4 groups][4 * cus waves][64][kCapW] as k_scan's
+bool q256_filter_ok(int dtype, int S);
+int launch_filter_q256(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st);
 // hr_persist.hip: the persistent FILTER (plans with 64-query tiles: P = 16 for 16-bit rows, 4 for fp32 rows)
 struct PersistCtl;
 struct PersistLaunch;
@@ -163,6 +167,8 @@ struct hr_index {
     int64_t n_exhaustive = 0;         // queries that needed the exhaustive exact pass (diagnostics)
     int64_t n_guard_fail = 0;         // queries that failed the exactness guard (collect fallback)
     int64_t n_wide = 0;               // 128-query FILTER launches issued (hr_wide.hip; not graph replays)
+    int64_t n_q256 = 0;               // 256-query FILTER launches issued (hr_q256.hip)
+    bool q256 = true;                 // hr_index_set_q256: 129-256-query batches take the 256-query FILTER
     std::vector<float> floor_host;
     // ---- hr_index_search (host queries, no mask) replayed as one HIP graph per batch shape: H2D of
     // the queries from pinned staging, prep, SAMPLE, FILTER, select, rescore, merge, D2H of results
@@ -221,7 +227,14 @@ struct hr_index {
     std::vector<char> g_peer;         // group: shard s's device has peer access with the primary
     struct GroupPipe* pipe = nullptr; // group: pipelined search (submit / finalize, hr_group.hip)
     struct Persist* ps = nullptr;     // persistent FILTER state (hr_index.hip; created on first use)
+    // hr_index_set_cu_mask: the CUs this index's own streams may use (empty: all).  Every internal stream is then
+    // created with hipExtStreamCreateWithCUMask and the launch grids are sized for popcount(mask) CUs
+    std::vector<uint32_t> cu_mask;
 };
+
+// an internal stream of h: on h's CU mask when one is set (priority is then not available), else high priority or
+// the default one (hr_index.hip)
+hipError_t index_stream_create(const hr_index* h, hipStream_t* s, bool high_priority);
 
 // group-handle entry points (hr_group.hip); each public hr_index_* call forwards here when h->G > 1
 int group_create(int dim, int dtype, int metric, int n_dev, const int* dev_ids, hr_index** out);

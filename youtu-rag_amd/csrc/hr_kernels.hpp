@@ -214,6 +214,10 @@ __global__ __launch_bounds__(256) void k_prep_q(const float* __restrict__ q, int
 }
 
 // ---------------------------------------------------------------- K3: the scan
+// s_waitcnt immediate that waits for vmcnt <= n only (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] |
+// vmcnt[5:4] in bits 15:14)
+constexpr int vmcnt_only(int n) { return 0x0F70 | (n & 15) | (((n >> 4) & 3) << 14); }
+
 // global -> LDS copy of n 16-byte vectors by the whole block, U loads in flight per thread
 __device__ inline void stage_lds(u32x4* dst, const u32x4* src, int n) {
     constexpr int U = 8;
@@ -371,6 +375,7 @@ __device__ inline u32x4 corpus_load(const uint8_t* p) {
 }
 template <int MT, bool NT>
 struct XFrag<MT, BF16, NT> {
+    static constexpr int kLoads = 1;  // 16-byte loads per lane per k-step
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
         v = corpus_load<NT>(rows + c * 1024 + lane * 16);
@@ -379,6 +384,7 @@ struct XFrag<MT, BF16, NT> {
 };
 template <int MT, bool NT>
 struct XFrag<MT, F16, NT> {
+    static constexpr int kLoads = 1;
     u32x4 v;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
         v = corpus_load<NT>(rows + c * 1024 + lane * 16);
@@ -387,6 +393,7 @@ struct XFrag<MT, F16, NT> {
 };
 template <int MT, bool NT>
 struct XFrag<MT, F32, NT> {
+    static constexpr int kLoads = 2;
     u32x4 a, b;
     __device__ inline void load(const uint8_t* rows, int64_t c, int lane) {
         a = corpus_load<NT>(rows + c * 2048 + lane * 16);
@@ -568,18 +575,41 @@ __device__ __forceinline__ void scan_body(ScanArgs a) {
         return a.tile_list ? (int64_t)scalar_word(a.tile_list, i) : i;
     };
 
-    // first loads of the corpus stream go out before the query staging, so their HBM latency
-    // overlaps it
+    // The query fragments (QB*S KiB) go to LDS once per launch by LDS-DMA (buffer_load ... lds: L2 -> LDS, no
+    // registers, no ds_write), issued BEFORE the corpus ring's first loads: vmcnt retires in issue order, so the
+    // wait for the fragments below then leaves the ring loads in flight.  (Staged with loads + ds_writes behind the
+    // ring, every workgroup waited out the ring's HBM latency, then the fragments', then the first refresh's before
+    // its first MFMA: 8 % of a 1.25M-row FILTER launch and 12 % at 1M x 768 went to that start,
+    // profiles/r05_small_shard_filter_diag_builds.jsonl.)  The persistent FILTER (LEAN) restages per batch with the
+    // ring already running and keeps the register copy.
+    const int n_q16 = a.S * QB * 64;  // 16-byte chunks of the query tile
+    if constexpr (!LEAN) {
+        if (!(HR_DIAG & 8)) {
+            const __amdgpu_buffer_rsrc_t qr =
+                __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, n_q16 * 16, 0x00020000);
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+            for (int c = wv * 64; c < n_q16; c += (int)blockDim.x)  // (wave-uniform: 64 chunks per instruction)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(lds + c * 16), 16,
+                                                         lane * 16, c * 16, 0, 0);
+        }
+    }
     XFrag<MT, DT, NT> ring[P];
-    if (u0 < u1) {
+    const bool ring0 = u0 < u1;
+    if (ring0) {
         const int64_t c0 = tile_at(u0) * S;
 #pragma unroll
         for (int i = 0; i < P; ++i) ring[i].load(a.rows, c0 + i, lane);
     }
-
-    // stage the query fragments (QB*S KiB) into LDS once per launch; 8 loads in flight per
-    // thread (a load->store loop pays one L2 round trip per 8 KiB)
-    if (!(HR_DIAG & 8)) stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, a.S * QB * 64);
+    if constexpr (LEAN) {
+        stage_lds((u32x4*)lds, (const u32x4*)a.qfrag, n_q16);
+    } else {
+        // this wave's DMAs have landed (only the ring's loads, issued after them, may be in flight); the barrier
+        // below makes every wave's visible
+        // (the builtin, not inline asm: the compiler's wait-count pass then knows the DMAs are complete and inserts
+        // no drain of its own in front of the k-loop's LDS reads)
+        if (ring0) __builtin_amdgcn_s_waitcnt(vmcnt_only(P * XFrag<MT, DT, NT>::kLoads));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+    }
     __syncthreads();
 
     if (u0 >= u1 && FILTER) {

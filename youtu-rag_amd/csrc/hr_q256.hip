@@ -1,0 +1,342 @@
+// hr_q256.hip -- the 256-query FILTER: one HBM read of every corpus tile for four 64-query groups.
+//
+// A batch of 129-256 queries was two launches of the 128-query FILTER (hr_wide.hip): two corpus passes, each at
+// about half the MFMA pipe (its eight 256-register waves are issue-bound).  Here the MFMA work of all 256 queries
+// rides on ONE pass -- 4x the MFMAs per byte of the 64-query k_scan, so a launch is about as much matrix work as
+// streaming time (10M x 1024: 2.6 ms of MFMA at the dense peak against 2.9 ms of HBM at the read ceiling):
+//  * one workgroup per CU, 4 waves, ONE wave per SIMD with the whole 512-register file: the 2 x 8 x 16 = 256
+//    accumulators of two tiles against 8 blocks of 32 queries sit in AGPRs, a 16-deep corpus ring per tile
+//    (32 KiB in flight per wave) and the query fragments in VGPRs -- a single wave keeps its SIMD's matrix pipe
+//    fed (v_mfma_f32_32x32x16 issues back to back at 32 cycles, MI355X_MICROARCH.md) with 16 independent MFMAs
+//    per k-step;
+//  * two tiles per wave per round: every query fragment read from LDS serves two MFMAs, and the workgroup's 8 tiles
+//    per round share one staging of the query windows;
+//  * the queries' fragments (4 x S KiB x 2: 512 KiB at D = 1024) stream through LDS in windows of 2 k-steps
+//    (16 KiB), staged by LDS-DMA (buffer_load ... lds: no registers) 8 windows ahead into a ring of 9 buffers
+//    (144 KiB).  LDS-DMA completions count in vmcnt, in order with the corpus ring's loads, so a window staged
+//    only one window ahead would make every wait on it drain the corpus ring too; staged as far ahead as the ring
+//    reaches, the wait that admits it retires only loads already consumed;
+//  * the A fragments are read with inline-asm ds_read_b128 and explicit lgkmcnt waits (one k-step ahead), so the
+//    compiler's conservative LDS-DMA tracking inserts no vmcnt drain in front of them;
+//  * thresholds per query in LDS (shared by the four waves); group maxima raised in the global table with one
+//    fire-and-forget atomicMax per passing score (rare: only scores at or above their threshold can raise the
+//    minimum over the groups); a refresh re-reads the global keys for one 64-query group per wave;
+//  * candidates go to k_scan's private per-(query group, wave) regions, so k_select reads them unchanged.
+// Exactness: the same invariant as the 128-query FILTER -- every row at or above a query's final threshold was
+// appended when scanned (thresholds only grow), and each group key is the score of an appended (or SAMPLE) row.
+// Scope: bf16 / f16 rows, D = 256 / 512 / 768 / 1024, one row part (k <= 16), no tile list; cosine / ip / l2.
+#include "hr_internal.hpp"
+#include "hr_kernels.hpp"
+
+namespace hr {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kQT = 256;              // threads per workgroup: 4 waves, one per SIMD
+constexpr int kWin = 2;               // k-steps per query window
+constexpr int kRing = 8;              // corpus ring depth in k-steps (per tile)
+constexpr int kLook = kRing / kWin;   // windows a window is staged ahead of its first use
+constexpr int kNB = kLook + 1;        // window buffers
+constexpr int kWQ = kWin * 8 * 64;    // u32x4 per window buffer: [k-step][block][lane]
+constexpr int kDma = kWQ / kQT;       // LDS-DMA instructions per thread per window
+// vmcnt at a window start that retires this wave's DMA of the NEXT window: younger than it are the ring loads of
+// kLook - 1 windows (2 tiles x kWin k-steps each) and the DMAs of kLook - 2 windows
+constexpr int kVmNext = (kLook - 1) * 2 * kWin + (kLook - 2) * kDma;
+static_assert(kVmNext <= 63, "vmcnt field");
+
+// f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N - 1>{}): loop indices usable as constants
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_read(uint32_t base) {  // ds_read_b128 base + OFF, not tracked by the compiler
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
+    return v;
+}
+
+template <int OFF>
+__device__ __forceinline__ void lds_write_f32(uint32_t addr, float v) {  // ds_write_b32, not tracked
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "n"(OFF) : "memory");
+}
+
+// one accumulator register read out of its AGPR at this point of the program (volatile: the register allocator
+// would otherwise copy whole 16-register accumulators to VGPRs early and spill them)
+template <int I>
+__device__ __forceinline__ float acc_read(const f32x16& v) {
+    float r;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(v[I]));
+    return r;
+}
+
+__device__ __forceinline__ float lds_read_f32(uint32_t addr) {  // ds_read_b32 and its wait, not tracked
+    float v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
+template <int MT, int S_>
+__global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
+    static_assert(S_ % kRing == 0 && S_ % kWin == 0, "tile depth");
+    __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
+    __shared__ __attribute__((aligned(16))) float th_lds[256];
+    __shared__ float sc[4 * 16 * 64];
+    constexpr int NQ = S_ / kRing;   // ring spans per tile
+
+    const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, g = lane & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t W = (int64_t)gridDim.x * 4;  // waves (candidate regions per query group)
+    const int64_t W2 = 2 * W;                  // tiles per round
+    const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;
+    const int64_t n_tiles = a.n_units;
+    const int64_t rounds = (n_tiles + W2 - 1) / W2;
+    const int64_t full_rounds = n_tiles / W2;
+    // round u: tiles [u W2, (u + 1) W2); wave wr takes u W2 + pos and u W2 + W + pos, pos rotated by a hash of u on
+    // full rounds (as k_scan / the 128-query FILTER: a period in the rows must not land in the same few waves)
+    auto tile_of = [&](int64_t u, int which) -> int64_t {
+        if (u >= rounds) return -1;
+        int64_t pos = wr;
+        if (HR_ROTATE_ROUNDS && u < full_rounds) {
+            pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
+            if (pos >= W) pos -= W;
+        }
+        const int64_t t = u * W2 + which * W + pos;
+        return wave_uniform(t < n_tiles ? t : -1);
+    };
+    auto rsrc = [&](int64_t t) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024)), (short)0,
+                                                 t < 0 ? 0 : S_ * 1024, 0x00020000);
+    };
+    const int voff = lane * 16;
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int ks) -> u32x4 {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, 2);  // nt
+    };
+    // query windows: window gw holds k-steps (gw kWin) mod S of every block; qfrag = [group 4][S][2 blocks][64][16 B]
+    const __amdgpu_buffer_rsrc_t qr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 4 * S_ * 2048, 0x00020000);
+    const uint32_t qw_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)qw;
+    auto stage = [&](int bi, int s0) {  // window starting at k-step s0 (of the tile) into buffer bi
+        u32x4* buf = qw + bi * kWQ;
+#pragma unroll
+        for (int j = 0; j < kDma; ++j) {
+            const int i = j >> 1, blk = (j & 1) * 4 + wv;  // chunk j * 256 + wv * 64 + lane of the window
+            const int soff = (((blk >> 1) * S_ + s0 + i) * 2 + (blk & 1)) * 1024;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 256 + wv * 64),
+                                                     16, voff, soff, 0, 0);
+        }
+    };
+    // the window buffer bi's base for this lane (byte address in LDS); block blk of k-step i sits at + (i 8 + blk) KiB
+    const uint32_t lane_addr = qw_base + (uint32_t)lane * 16u;
+    auto qbase = [&](int bi) -> uint32_t { return lane_addr + (uint32_t)(bi * kWQ * 16); };
+    // thresholds: th_lds[q] (this lane's half adds 4 queries); the scores of a passing block: sc[wave][register][lane]
+    const uint32_t th_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)th_lds;
+    const uint32_t th_lane = th_base + (uint32_t)half * 16u;
+    const uint32_t sc_lane = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sc + (uint32_t)(wv * 16 * 64 + lane) * 4u;
+
+    // ---- thresholds: this wave's 64-query group from the global keys (min over the 32 groups)
+    auto refresh = [&]() {
+        uint32_t key[32];
+        const uint32_t* kp = a.mkeys + (int64_t)(64 * wv + half) * 32 + g;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+            key[j] = __hip_atomic_load(kp + 64 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const float f = half_min32(key2f(key[j] > HR_KEY_NEG_INF ? key[j] : HR_KEY_NEG_INF));
+            const int q = 64 * wv + 2 * j + half;
+            const uint32_t ad = th_base + (uint32_t)q * 4u;  // (every lane of the half holds the minimum: no branch)
+            lds_write_f32<0>(ad, fmaxf(lds_read_f32(ad), f));
+        }
+    };
+    th_lds[tid] = a.floor_q[tid];  // (the floors once: thresholds only grow; kQT = 256 queries)
+    __syncthreads();
+    refresh();
+
+    // ---- prologue: the first kLook windows and the first ring of both tiles of round 0
+    u32x4 ra[kRing], rb[kRing];
+    for (int w = 0; w < kLook; ++w) stage(w, (w * kWin) % S_);  // (window w in buffer w)
+    {
+        const auto r0 = rsrc(tile_of(0, 0)), r1 = rsrc(tile_of(0, 1));
+#pragma unroll
+        for (int i = 0; i < kRing; ++i) {
+            ra[i] = ld(r0, i);
+            rb[i] = ld(r1, i);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    uint32_t mycnt[4] = {0u, 0u, 0u, 0u};  // lane q: candidates of query q of each 64-query group
+    // a passing block's registers one by one (scores parked in this wave's LDS slot): group maxima raised with one
+    // fire-and-forget atomicMax per passing score, the candidates appended to the group's private region
+    auto walk_block = [&](int b, bool ok, uint32_t row, uint32_t& cnt) {
+        const int gq = b >> 1;
+        float2* const reg = a.pbuf + ((gq * W + wr) * 64) * a.capw;
+#pragma unroll 1
+        for (int i = 0; i < 16; ++i) {
+            const float v = lds_read_f32(sc_lane + (uint32_t)i * 256u);
+            const int qm = (b & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query (within the group) of half 0
+            const int qh = qm + 4 * half;
+            const bool pass = ok && v >= lds_read_f32(th_base + (uint32_t)(gq * 64 + qh) * 4u);
+            const uint64_t msk = __ballot(pass);
+            if (!msk) continue;
+            if (pass) atomicMax(a.mkeys + (int64_t)(gq * 64 + qh) * 32 + g, f2key(v));
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const uint32_t mh = (uint32_t)(msk >> (32 * hh));
+                if (!mh) continue;
+                const int ql = qm + 4 * hh;
+                const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
+                if (pass && half == hh) {
+                    const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << g) - 1u));
+                    if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                }
+                cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
+            }
+        }
+    };
+    auto allow_word = [&](int64_t t) -> uint32_t {
+        if (t < 0) return 0u;
+        uint32_t w0 = scalar_word(a.live, t);
+        if (a.mask) w0 &= scalar_word(a.mask, t);
+        return w0;
+    };
+    const int RT = std::max(1, a.refresh_every);
+    // A fragments stream in (k-step, block) pairs -- pair p = 8 k + b of the running k-step count -- read kPf pairs
+    // ahead into a 4-slot rotation (16 VGPRs instead of a whole k-step's 64): the two MFMAs of a pair (64 cycles)
+    // cover the LDS latency of the reads behind it
+    constexpr int kPf = 2;
+    u32x4 pf[4];
+    pf[0] = lds_read<0>(qbase(0));
+    pf[1] = lds_read<1024>(qbase(0));
+    static_assert(kPf == 2, "prologue reads");
+    int wb = 0;  // buffer of the current window (window gw lives in buffer gw mod kNB)
+    uint32_t qcur = qbase(0), qnext = qbase(1);  // this lane's address in the current / next window's buffer
+
+    for (int64_t u = 0; u < rounds; ++u) {
+        const int64_t tA = tile_of(u, 0), tB = tile_of(u, 1);
+        const int64_t nA = tile_of(u + 1, 0), nB = tile_of(u + 1, 1);
+        const uint32_t allowA = allow_word(tA), allowB = allow_word(tB);
+        // (euclidean: the rows' |x|^2 loaded now, ahead of this round's ring refills -- a load issued in the epilogue
+        // would be the youngest in vmcnt and its wait would drain the whole ring)
+        const float xsA = (a.xnorm && tA >= 0) ? a.xnorm[tA * 32 + slot_row(tA, g)] : 0.0f;
+        const float xsB = (a.xnorm && tB >= 0) ? a.xnorm[tB * 32 + slot_row(tB, g)] : 0.0f;
+        // (every index into acc is a compile-time constant -- static_for, never a loop variable -- so the array is
+        // promoted to registers from the start: a runtime index, even one unrolling later resolves, keeps it a stack
+        // object that the epilogue reads back from scratch)
+        f32x16 acc[2][8];
+        static_for<2>([&](auto T_) {
+            static_for<8>([&](auto B_) { acc[decltype(T_)::value][decltype(B_)::value] = f32x16{}; });
+        });
+#pragma unroll
+        for (int qs = 0; qs < NQ; ++qs) {
+            const bool last = qs + 1 == NQ;
+            const auto sA = rsrc(last ? nA : tA), sB = rsrc(last ? nB : tB);
+            const int kb = last ? 0 : (qs + 1) * kRing;
+            static_for<kRing>([&](auto I_) {
+                constexpr int i = decltype(I_)::value;
+                if constexpr (i % kWin == 0) {
+                    // this wave's DMA of the next window has landed; the barrier makes every wave's visible and
+                    // retires every read of the buffer of the window before this one, which the DMA of the window
+                    // kLook ahead refills ((wb + kLook) mod kNB = wb - 1)
+                    if (i > 0 || qs > 0 || u > 0) wb = wb + 1 == kNB ? 0 : wb + 1;
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmNext) : "memory");
+                    __builtin_amdgcn_s_barrier();
+                    stage(wb == 0 ? kNB - 1 : wb - 1, (qs * kRing + i + kLook * kWin) % S_);
+                    qcur = qbase(wb);
+                    qnext = qbase(wb + 1 == kNB ? 0 : wb + 1);
+                }
+                const u32x4 xa = ra[i], xb = rb[i];
+                ra[i] = ld(sA, kb + i);
+                rb[i] = ld(sB, kb + i);
+                static_for<8>([&](auto B_) {
+                    constexpr int b = decltype(B_)::value;
+                    constexpr int p = i * 8 + b;  // pair within the span (slot p & 3: 128 pairs per span)
+                    constexpr int pn = p + kPf;   // the pair read now, kPf ahead (possibly in the next window / span)
+                    constexpr int kn = pn >> 3;   // its k-step within the span (kRing: the next span's first)
+                    const uint32_t base = (kn / kWin) != (i / kWin) ? qnext : qcur;
+                    pf[pn & 3] = lds_read<((kn % kWin) * 8 + (pn & 7)) * 1024>(base);
+                    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(pf[p & 3]) : "n"(kPf));
+                    acc[0][b] = mfma32<MT>(pf[p & 3], xa, acc[0][b]);
+                    acc[1][b] = mfma32<MT>(pf[p & 3], xb, acc[1][b]);
+                });
+            });
+        }
+
+        // ---- epilogue, block by block: the 16 scores of one 32-query block against their thresholds (read from LDS
+        // with inline asm: a compiler-visible LDS read would be fenced behind every LDS-DMA in flight -- vmcnt(0), the
+        // whole corpus ring), one ballot of "any register passes".  A passing block (rare after the first rounds) parks
+        // its scores in this wave's LDS slot and is walked register by register in a rolled loop, so the unrolled part
+        // stays small in registers and code.  Every accumulator read has constant indices (static_for).
+        static_for<2>([&](auto T_) {
+            constexpr int T = decltype(T_)::value;
+            const int64_t t = T ? tB : tA;
+            const uint32_t allow = T ? allowB : allowA;
+            const int rg = slot_row(t < 0 ? 0 : t, g);
+            const bool ok = (allow >> rg) & 1u;
+            const float xs = T ? xsB : xsA;
+            const float xm = a.xnorm ? 2.0f : 1.0f;  // euclidean: 2 q.x - |x|^2 (as k_scan)
+            const uint32_t row = (uint32_t)(t * 32 + rg);
+            static_for<8>([&](auto B_) {
+                constexpr int b = decltype(B_)::value;
+                u32x4 t4[4];
+                static_for<4>([&](auto R_) {
+                    constexpr int r = decltype(R_)::value;
+                    t4[r] = lds_read<(b * 32 + 8 * r) * 4>(th_lane);
+                });
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t4[0]), "+v"(t4[1]), "+v"(t4[2]), "+v"(t4[3]));
+                float v[16];
+                float d = -__builtin_inff();
+                static_for<16>([&](auto I_) {
+                    constexpr int i = decltype(I_)::value;
+                    v[i] = __builtin_fmaf(xm, acc_read<i>(acc[T][b]), -xs);
+                    d = fmaxf(d, v[i] - __builtin_bit_cast(float, t4[i >> 2][i & 3]));
+                });
+                if (!__ballot(ok && d >= 0.0f)) return;
+                static_for<16>([&](auto I_) {
+                    constexpr int i = decltype(I_)::value;
+                    lds_write_f32<i * 256>(sc_lane, v[i]);
+                });
+                walk_block(b, ok, row, mycnt[b >> 1]);
+            });
+        });
+        // thresholds of this wave's group: after rounds 1, 2, 4, 8 (the early keys rise fast), then every RT rounds
+        const int64_t v1 = u + 1;
+        if ((v1 & (v1 - 1)) == 0 ? v1 <= 8 : (v1 % RT) == 0) refresh();
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) a.pcnt[(x * W + wr) * 64 + lane] = mycnt[x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the look-ahead DMAs land before the workgroup's LDS goes)
+}
+
+template <int MT, int S_>
+int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_filter_q256<MT, S_>), dim3((unsigned)cus), dim3(kQT), 0, st, a);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
+}  // namespace
+
+bool q256_filter_ok(int dtype, int S) { return dtype != F32 && (S == 16 || S == 32 || S == 48 || S == 64); }
+
+int launch_filter_q256(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st) {
+    if (!q256_filter_ok(dtype, S)) return HR_E_UNSUPPORTED;
+#define HR_Q256_CASE(MTv, Sv) \
+    if (mt == MTv && S == Sv) return launch_t<MTv, Sv>(cus, a, st);
+    HR_Q256_CASE(BF16, 64)
+#ifndef HR_Q256_ONE  // (register-allocation studies compile one instantiation)
+    HR_Q256_CASE(BF16, 48) HR_Q256_CASE(BF16, 32) HR_Q256_CASE(BF16, 16)
+    HR_Q256_CASE(F16, 64) HR_Q256_CASE(F16, 48) HR_Q256_CASE(F16, 32) HR_Q256_CASE(F16, 16)
+#endif
+#undef HR_Q256_CASE
+    return HR_E_UNSUPPORTED;
+}
+
+}  // namespace hr

@@ -46,11 +46,35 @@ EXPORTS = [
     "hr_add_layernorm", "hr_index_info", "hr_index_graph_replays", "hr_index_wide_launches", "hr_kc_for_k_dim",
     "hr_index_search_submit", "hr_index_search_finalize", "hr_index_host_us", "hr_index_search_submit_host",
     "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
-    "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles",
+    "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles", "hr_index_set_cu_mask",
+    "hr_stream_create_cu_mask", "hr_stream_destroy", "hr_index_set_q256", "hr_index_q256_launches",
 ]
 
 _lib = None
 _lib_lock = threading.Lock()
+
+
+def cu_mask_words(cus) -> np.ndarray:
+    """uint32 mask words of a CU list (bit i of word j = CU 32 j + i)."""
+    cus = [int(c) for c in cus]
+    words = np.zeros(max(cus) // 32 + 1, np.uint32)
+    for c in cus:
+        words[c // 32] |= np.uint32(1 << (c % 32))
+    return words
+
+
+def create_cu_stream(device: int, cus) -> int:
+    """A raw HIP stream of `device` restricted to the CUs in `cus` (wrap it with torch.cuda.ExternalStream); release
+    it with destroy_stream."""
+    lib = load_library()
+    words = cu_mask_words(cus)
+    out = ctypes.c_void_p()
+    _check(lib.hr_stream_create_cu_mask(int(device), words.ctypes.data, len(words), ctypes.byref(out)))
+    return int(out.value)
+
+
+def destroy_stream(stream: int) -> None:
+    _check(load_library().hr_stream_destroy(ctypes.c_void_p(stream)))
 
 
 class NativeError(RuntimeError):
@@ -102,6 +126,11 @@ def load_library(path: str | None = None):
             "hr_index_persist_stats": [vp, vp],
             "hr_index_persist_trace": [vp, ctypes.c_int, vp, vp],
             "hr_index_wave_tiles": [vp, vp, i32, vp],
+            "hr_index_set_cu_mask": [vp, vp, i32],
+            "hr_stream_create_cu_mask": [i32, vp, i32, pp],
+            "hr_stream_destroy": [vp],
+            "hr_index_set_q256": [vp, i32],
+            "hr_index_q256_launches": [vp, vp],
             "hr_index_size": [vp, vp, vp],
             "hr_index_info": [vp, vp, vp, vp, vp],
             "hr_index_get_rows": [vp, vp, i64, vp],
@@ -132,6 +161,8 @@ def load_library(path: str | None = None):
             "hr_add_layernorm": [vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, i32, vp],
         }
         for name, args in sig.items():
+            if p != (path or LIB_PATH) and not hasattr(L, name):
+                continue  # an A/B timing build of an older source (HIPRAG_LIB_OVERRIDE) may lack newer entry points
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = i32
@@ -382,6 +413,16 @@ class NativeIndex:
         _check(self.lib.hr_index_stats(self._h, out))
         return {"main_passes": out[0], "guard_failures": out[1], "exhaustive": out[2]}
 
+    def set_q256(self, on: bool) -> None:
+        """The 256-query FILTER for 129-256-query batches (default on; off: two 128-query FILTER launches)."""
+        _check(self.lib.hr_index_set_q256(self._h, 1 if on else 0))
+
+    def q256_launches(self) -> int:
+        """256-query FILTER launches issued so far (hr_index_q256_launches)."""
+        out = ctypes.c_int64(0)
+        _check(self.lib.hr_index_q256_launches(self._h, ctypes.byref(out)))
+        return out.value
+
     def wide_launches(self) -> int:
         """128-query FILTER launches issued so far (hr_index_wide_launches)."""
         out = ctypes.c_int64(0)
@@ -398,6 +439,12 @@ class NativeIndex:
     def set_persist(self, mode: int) -> None:
         """Persistent FILTER of pipelined shard batches: 0 off, 1 shards of 4.2M-5.1M rows (default), 2 any size."""
         _check(self.lib.hr_index_set_persist(self._h, int(mode)))
+
+    def set_cu_mask(self, cus) -> None:
+        """Run this index's internal streams on the CUs listed in `cus` (None / empty: all CUs); see
+        hr_index_set_cu_mask and cu_mask_words."""
+        words = cu_mask_words(cus) if cus else np.zeros(0, np.uint32)
+        _check(self.lib.hr_index_set_cu_mask(self._h, words.ctypes.data if len(words) else None, len(words)))
 
     def persist_close(self) -> None:
         """No further batch for now: a running persistent FILTER exits once through its batches."""

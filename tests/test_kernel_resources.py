@@ -58,3 +58,19 @@ def test_q256_filter_does_not_spill(resources):
     spilled = {k: v.get("vgpr_spill_count", 0) for k, v in q.items() if v.get("vgpr_spill_count", 0)}
     assert not spilled, spilled
     assert all(v.get("private_segment_fixed_size", 0) == 0 for v in q.values()), q
+
+
+def test_no_bit_cast_of_a_vector_element():
+    """hipcc (ROCm 7.2 clang) lowers __builtin_bit_cast(float, v[c]) -- v an ext_vector_type -- to v[0] for every c
+    (it loads only that dword).  The first 256-query FILTER read its per-query thresholds that way and compared every
+    register against one query's threshold; bit_cast the whole vector, then index.  No source may use the form."""
+    import glob
+
+    pat = re.compile(r"__builtin_bit_cast\(\s*(float|u?int32_t|int|unsigned)\s*,\s*[A-Za-z_][A-Za-z_0-9]*\s*(\[[^\]]+\])+\s*\)")
+    csrc = os.path.join(REPO, "youtu-rag_amd", "csrc")
+    hits = []
+    for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")):
+        for i, line in enumerate(open(f), 1):
+            if pat.search(line):
+                hits.append(f"{os.path.basename(f)}:{i}: {line.strip()}")
+    assert not hits, hits

@@ -62,6 +62,21 @@ __device__ __forceinline__ u32x4 lds_read(uint32_t base) {  // ds_read_b128 base
     return v;
 }
 
+// four ds_read_b128 at base + OFF + 32 r and their wait in ONE asm statement: with the wait in a separate statement
+// the compiler may copy an output register between the two (it takes the asm's outputs as ready at once) and the
+// copy reads the register before the load has landed
+template <int OFF>
+__device__ __forceinline__ void lds_read4_wait(uint32_t base, u32x4 (&t)[4]) {
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:%5\n\t"
+        "ds_read_b128 %1, %4 offset:%6\n\t"
+        "ds_read_b128 %2, %4 offset:%7\n\t"
+        "ds_read_b128 %3, %4 offset:%8\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+        : "v"(base), "n"(OFF), "n"(OFF + 32), "n"(OFF + 64), "n"(OFF + 96));
+}
+
 template <int OFF>
 __device__ __forceinline__ void lds_write_f32(uint32_t addr, float v) {  // ds_write_b32, not tracked
     asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "n"(OFF) : "memory");
@@ -287,17 +302,15 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             static_for<8>([&](auto B_) {
                 constexpr int b = decltype(B_)::value;
                 u32x4 t4[4];
-                static_for<4>([&](auto R_) {
-                    constexpr int r = decltype(R_)::value;
-                    t4[r] = lds_read<(b * 32 + 8 * r) * 4>(th_lane);
-                });
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t4[0]), "+v"(t4[1]), "+v"(t4[2]), "+v"(t4[3]));
+                lds_read4_wait<b * 128>(th_lane, t4);
+                // (bit_cast the whole vector, then index: this clang lowers a bit_cast of ONE component, t4[r][c], to
+                // component 0 for every c, and then loads only that dword)
                 float v[16];
                 float d = -__builtin_inff();
                 static_for<16>([&](auto I_) {
                     constexpr int i = decltype(I_)::value;
                     v[i] = __builtin_fmaf(xm, acc_read<i>(acc[T][b]), -xs);
-                    d = fmaxf(d, v[i] - __builtin_bit_cast(float, t4[i >> 2][i & 3]));
+                    d = fmaxf(d, v[i] - __builtin_bit_cast(f32x4, t4[i >> 2])[i & 3]);
                 });
                 if (!__ballot(ok && d >= 0.0f)) return;
                 static_for<16>([&](auto I_) {

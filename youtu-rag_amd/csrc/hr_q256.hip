@@ -36,15 +36,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kQT = 256;              // threads per workgroup: 4 waves, one per SIMD
 constexpr int kWin = 2;               // k-steps per query window
-constexpr int kRing = 8;              // corpus ring depth in k-steps (per tile)
-constexpr int kLook = kRing / kWin;   // windows a window is staged ahead of its first use
-constexpr int kNB = kLook + 1;        // window buffers
 constexpr int kWQ = kWin * 8 * 64;    // u32x4 per window buffer: [k-step][block][lane]
 constexpr int kDma = kWQ / kQT;       // LDS-DMA instructions per thread per window
-// vmcnt at a window start that retires this wave's DMA of the NEXT window: younger than it are the ring loads of
-// kLook - 1 windows (2 tiles x kWin k-steps each) and the DMAs of kLook - 2 windows
-constexpr int kVmNext = (kLook - 1) * 2 * kWin + (kLook - 2) * kDma;
-static_assert(kVmNext <= 63, "vmcnt field");
+// corpus ring depth in k-steps per tile: 16 (32 KiB in flight per wave) where the registers hold it spill-free --
+// at D = 512 / 768 (two or three ring spans per tile) the allocator spills a 16-deep ring, so 8 there
+constexpr int ring_for(int S) { return (S == 32 || S == 48) ? 8 : 16; }
+template <int S_>
+struct Q256Geom {
+    static constexpr int kRing = ring_for(S_);
+    static constexpr int kLook = kRing / kWin;  // windows a window is staged ahead of its first use
+    static constexpr int kNB = kLook + 1;       // window buffers
+    // vmcnt at a window start that retires this wave's DMA of the NEXT window: younger than it are the ring loads
+    // of kLook - 1 windows (2 tiles x kWin k-steps each) and the DMAs of kLook - 2 windows
+    static constexpr int kVmNext = (kLook - 1) * 2 * kWin + (kLook - 2) * kDma;
+    static_assert(kVmNext <= 63, "vmcnt field");
+};
 
 // f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N - 1>{}): loop indices usable as constants
 template <int N, int I = 0, class F>
@@ -91,6 +97,13 @@ __device__ __forceinline__ float acc_read(const f32x16& v) {
     return r;
 }
 
+template <int OFF>
+__device__ __forceinline__ float lds_read_f32o(uint32_t addr) {  // ds_read_b32 at addr + OFF and its wait
+    float v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+    return v;
+}
+
 __device__ __forceinline__ float lds_read_f32(uint32_t addr) {  // ds_read_b32 and its wait, not tracked
     float v;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
@@ -99,10 +112,12 @@ __device__ __forceinline__ float lds_read_f32(uint32_t addr) {  // ds_read_b32 a
 
 template <int MT, int S_>
 __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
+    constexpr int kRing = Q256Geom<S_>::kRing, kLook = Q256Geom<S_>::kLook, kNB = Q256Geom<S_>::kNB;
+    constexpr int kVmNext = Q256Geom<S_>::kVmNext;
     static_assert(S_ % kRing == 0 && S_ % kWin == 0, "tile depth");
     __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
     __shared__ __attribute__((aligned(16))) float th_lds[256];
-    __shared__ float sc[4 * 16 * 64];
+    __shared__ float sc[4 * 8 * 64];  // per wave: 8 parked scores (half a block) x 64 lanes
     constexpr int NQ = S_ / kRing;   // ring spans per tile
 
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, g = lane & 31;
@@ -153,22 +168,26 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     // thresholds: th_lds[q] (this lane's half adds 4 queries); the scores of a passing block: sc[wave][register][lane]
     const uint32_t th_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)th_lds;
     const uint32_t th_lane = th_base + (uint32_t)half * 16u;
-    const uint32_t sc_lane = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sc + (uint32_t)(wv * 16 * 64 + lane) * 4u;
+    const uint32_t sc_lane = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sc + (uint32_t)(wv * 8 * 64 + lane) * 4u;
 
     // ---- thresholds: this wave's 64-query group from the global keys (min over the 32 groups)
+    // (register-light: the 32 key loads are buffer loads at SGPR offsets from one lane offset and the 32 threshold
+    // updates use immediate LDS offsets -- 64-bit addresses per key were hoisted out of the round loop and spilled)
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)a.mkeys, (short)0, kQT * 32 * 4, 0x00020000);
+    const uint32_t key_lane = (uint32_t)(((64 * wv + half) * 32 + g) * 4);  // key (query 64 wv + half, group g)
+    const uint32_t th_q = th_base + (uint32_t)(64 * wv + half) * 4u;        // threshold of query 64 wv + half
     auto refresh = [&]() {
         uint32_t key[32];
-        const uint32_t* kp = a.mkeys + (int64_t)(64 * wv + half) * 32 + g;
-#pragma unroll
-        for (int j = 0; j < 32; ++j)
-            key[j] = __hip_atomic_load(kp + 64 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
+        static_for<32>([&](auto J_) {  // query 64 wv + 2 j + half; sc1 = the agent-coherent load of an atomic
+            constexpr int j = decltype(J_)::value;
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(kr, key_lane, j * 256, 16);
+        });
+        static_for<32>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
             const float f = half_min32(key2f(key[j] > HR_KEY_NEG_INF ? key[j] : HR_KEY_NEG_INF));
-            const int q = 64 * wv + 2 * j + half;
-            const uint32_t ad = th_base + (uint32_t)q * 4u;  // (every lane of the half holds the minimum: no branch)
-            lds_write_f32<0>(ad, fmaxf(lds_read_f32(ad), f));
-        }
+            // (every lane of the half holds the minimum: no branch)
+            lds_write_f32<8 * j>(th_q, fmaxf(lds_read_f32o<8 * j>(th_q), f));
+        });
     };
     th_lds[tid] = a.floor_q[tid];  // (the floors once: thresholds only grow; kQT = 256 queries)
     __syncthreads();
@@ -191,12 +210,12 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     uint32_t mycnt[4] = {0u, 0u, 0u, 0u};  // lane q: candidates of query q of each 64-query group
     // a passing block's registers one by one (scores parked in this wave's LDS slot): group maxima raised with one
     // fire-and-forget atomicMax per passing score, the candidates appended to the group's private region
-    auto walk_block = [&](int b, bool ok, uint32_t row, uint32_t& cnt) {
+    auto walk_block = [&](int b, bool ok, uint32_t row, uint32_t& cnt, int i0) {  // registers i0 .. i0 + 7
         const int gq = b >> 1;
         float2* const reg = a.pbuf + ((gq * W + wr) * 64) * a.capw;
 #pragma unroll 1
-        for (int i = 0; i < 16; ++i) {
-            const float v = lds_read_f32(sc_lane + (uint32_t)i * 256u);
+        for (int i = i0; i < i0 + 8; ++i) {
+            const float v = lds_read_f32(sc_lane + (uint32_t)(i - i0) * 256u);
             const int qm = (b & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query (within the group) of half 0
             const int qh = qm + 4 * half;
             const bool pass = ok && v >= lds_read_f32(th_base + (uint32_t)(gq * 64 + qh) * 4u);
@@ -313,11 +332,14 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                     d = fmaxf(d, v[i] - __builtin_bit_cast(f32x4, t4[i >> 2])[i & 3]);
                 });
                 if (!__ballot(ok && d >= 0.0f)) return;
-                static_for<16>([&](auto I_) {
-                    constexpr int i = decltype(I_)::value;
-                    lds_write_f32<i * 256>(sc_lane, v[i]);
+                static_for<2>([&](auto H_) {  // (two halves of 8 registers: the LDS slot holds 8)
+                    constexpr int h8 = decltype(H_)::value * 8;
+                    static_for<8>([&](auto I_) {
+                        constexpr int i = decltype(I_)::value;
+                        lds_write_f32<i * 256>(sc_lane, v[h8 + i]);
+                    });
+                    walk_block(b, ok, row, mycnt[b >> 1], h8);
                 });
-                walk_block(b, ok, row, mycnt[b >> 1]);
             });
         });
         // thresholds of this wave's group: after rounds 1, 2, 4, 8 (the early keys rise fast), then every RT rounds

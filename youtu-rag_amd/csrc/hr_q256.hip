@@ -30,6 +30,27 @@
 
 namespace hr {
 
+// HR_Q256_DIAG (timing builds only -- results are WRONG with any bit set): 1 no query-window staging in the loop,
+// 2 no corpus ring loads, 4 no per-window barrier, 8 no MFMA (operands consumed by a cheap VALU op) and no
+// epilogue, 16 no epilogue, 32 no refresh after round 8
+#ifndef HR_Q256_DIAG
+#define HR_Q256_DIAG 0
+#endif
+// A/B knobs (results identical): LDS prefetch distance in (k-step, block) pairs, a wave's two tiles adjacent
+// (1) or W apart (0), the corpus loads' cache policy (2 = nt)
+#ifndef HR_Q256_PF
+#define HR_Q256_PF 2
+#endif
+#ifndef HR_Q256_ADJ
+#define HR_Q256_ADJ 0
+#endif
+#ifndef HR_Q256_STAMPS  // diagnostic build: per-wave cycle shares of the round's phases, printed
+#define HR_Q256_STAMPS 0
+#endif
+#ifndef HR_Q256_NT
+#define HR_Q256_NT 2
+#endif
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -110,6 +131,19 @@ __device__ __forceinline__ float lds_read_f32(uint32_t addr) {  // ds_read_b32 a
     return v;
 }
 
+#if HR_Q256_STAMPS
+__device__ __forceinline__ uint64_t q256_stamp() {  // (diagnostic builds only: cycle shares, never run times)
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define HR_STAMP(var) const uint64_t var = q256_stamp()
+#else
+#define HR_STAMP(var)
+#endif
+
 template <int MT, int S_>
 __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     constexpr int kRing = Q256Geom<S_>::kRing, kLook = Q256Geom<S_>::kLook, kNB = Q256Geom<S_>::kNB;
@@ -117,7 +151,6 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     static_assert(S_ % kRing == 0 && S_ % kWin == 0, "tile depth");
     __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
     __shared__ __attribute__((aligned(16))) float th_lds[256];
-    __shared__ float sc[4 * 8 * 64];  // per wave: 8 parked scores (half a block) x 64 lanes
     constexpr int NQ = S_ / kRing;   // ring spans per tile
 
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, g = lane & 31;
@@ -137,7 +170,7 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
             if (pos >= W) pos -= W;
         }
-        const int64_t t = u * W2 + which * W + pos;
+        const int64_t t = HR_Q256_ADJ ? u * W2 + 2 * pos + which : u * W2 + which * W + pos;
         return wave_uniform(t < n_tiles ? t : -1);
     };
     auto rsrc = [&](int64_t t) {
@@ -146,7 +179,7 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     };
     const int voff = lane * 16;
     auto ld = [&](__amdgpu_buffer_rsrc_t r, int ks) -> u32x4 {
-        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, 2);  // nt
+        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, HR_Q256_NT);  // nt
     };
     // query windows: window gw holds k-steps (gw kWin) mod S of every block; qfrag = [group 4][S][2 blocks][64][16 B]
     const __amdgpu_buffer_rsrc_t qr =
@@ -165,10 +198,9 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     // the window buffer bi's base for this lane (byte address in LDS); block blk of k-step i sits at + (i 8 + blk) KiB
     const uint32_t lane_addr = qw_base + (uint32_t)lane * 16u;
     auto qbase = [&](int bi) -> uint32_t { return lane_addr + (uint32_t)(bi * kWQ * 16); };
-    // thresholds: th_lds[q] (this lane's half adds 4 queries); the scores of a passing block: sc[wave][register][lane]
+    // thresholds: th_lds[q] (this lane's half adds 4 queries)
     const uint32_t th_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)th_lds;
     const uint32_t th_lane = th_base + (uint32_t)half * 16u;
-    const uint32_t sc_lane = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)sc + (uint32_t)(wv * 8 * 64 + lane) * 4u;
 
     // ---- thresholds: this wave's 64-query group from the global keys (min over the 32 groups)
     // (register-light: the 32 key loads are buffer loads at SGPR offsets from one lane offset and the 32 threshold
@@ -210,18 +242,20 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     uint32_t mycnt[4] = {0u, 0u, 0u, 0u};  // lane q: candidates of query q of each 64-query group
     // a passing block's registers one by one (scores parked in this wave's LDS slot): group maxima raised with one
     // fire-and-forget atomicMax per passing score, the candidates appended to the group's private region
-    auto walk_block = [&](int b, bool ok, uint32_t row, uint32_t& cnt, int i0) {  // registers i0 .. i0 + 7
+    // a passing block's registers (the set bits of regs, one per register holding a passing score), scores and
+    // thresholds in registers -- read at a wave-uniform dynamic index (M0-relative register moves, no memory): group
+    // maxima raised with one fire-and-forget atomicMax per passing score, candidates appended to the group's region
+    auto walk_block = [&](int b, bool ok, uint32_t row, uint32_t& cnt, const f32x16& V, const f32x16& TH, uint32_t regs) {
         const int gq = b >> 1;
         float2* const reg = a.pbuf + ((gq * W + wr) * 64) * a.capw;
-#pragma unroll 1
-        for (int i = i0; i < i0 + 8; ++i) {
-            const float v = lds_read_f32(sc_lane + (uint32_t)(i - i0) * 256u);
+        while (regs) {
+            const int i = __builtin_amdgcn_readfirstlane(__builtin_ctz(regs));
+            regs &= regs - 1u;
+            const float v = V[i];
             const int qm = (b & 1) * 32 + (i & 3) + 8 * (i >> 2);  // query (within the group) of half 0
-            const int qh = qm + 4 * half;
-            const bool pass = ok && v >= lds_read_f32(th_base + (uint32_t)(gq * 64 + qh) * 4u);
+            const bool pass = ok && v >= TH[i];
             const uint64_t msk = __ballot(pass);
-            if (!msk) continue;
-            if (pass) atomicMax(a.mkeys + (int64_t)(gq * 64 + qh) * 32 + g, f2key(v));
+            if (pass) atomicMax(a.mkeys + (int64_t)(gq * 64 + qm + 4 * half) * 32 + g, f2key(v));
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
                 const uint32_t mh = (uint32_t)(msk >> (32 * hh));
@@ -246,15 +280,19 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     // A fragments stream in (k-step, block) pairs -- pair p = 8 k + b of the running k-step count -- read kPf pairs
     // ahead into a 4-slot rotation (16 VGPRs instead of a whole k-step's 64): the two MFMAs of a pair (64 cycles)
     // cover the LDS latency of the reads behind it
-    constexpr int kPf = 2;
+    constexpr int kPf = HR_Q256_PF;
+    static_assert(kPf >= 1 && kPf <= 3, "4-slot rotation");
     u32x4 pf[4];
-    pf[0] = lds_read<0>(qbase(0));
-    pf[1] = lds_read<1024>(qbase(0));
-    static_assert(kPf == 2, "prologue reads");
+    static_for<kPf>([&](auto P_) { pf[decltype(P_)::value] = lds_read<decltype(P_)::value * 1024>(qbase(0)); });
     int wb = 0;  // buffer of the current window (window gw lives in buffer gw mod kNB)
     uint32_t qcur = qbase(0), qnext = qbase(1);  // this lane's address in the current / next window's buffer
 
+    uint32_t dsink = 0;  // (HR_Q256_DIAG & 8 timing builds only)
+#if HR_Q256_STAMPS
+    uint64_t c_loop = 0, c_wait = 0, c_epi = 0, c_ref = 0;
+#endif
     for (int64_t u = 0; u < rounds; ++u) {
+        HR_STAMP(s_r0);
         const int64_t tA = tile_of(u, 0), tB = tile_of(u, 1);
         const int64_t nA = tile_of(u + 1, 0), nB = tile_of(u + 1, 1);
         const uint32_t allowA = allow_word(tA), allowB = allow_word(tB);
@@ -281,15 +319,25 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                     // retires every read of the buffer of the window before this one, which the DMA of the window
                     // kLook ahead refills ((wb + kLook) mod kNB = wb - 1)
                     if (i > 0 || qs > 0 || u > 0) wb = wb + 1 == kNB ? 0 : wb + 1;
+                    HR_STAMP(s_w0);
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmNext) : "memory");
-                    __builtin_amdgcn_s_barrier();
-                    stage(wb == 0 ? kNB - 1 : wb - 1, (qs * kRing + i + kLook * kWin) % S_);
+                    if (!(HR_Q256_DIAG & 4)) __builtin_amdgcn_s_barrier();
+#if HR_Q256_STAMPS
+                    HR_STAMP(s_w1);
+                    c_wait += s_w1 - s_w0;
+#endif
+                    if (!(HR_Q256_DIAG & 1)) stage(wb == 0 ? kNB - 1 : wb - 1, (qs * kRing + i + kLook * kWin) % S_);
                     qcur = qbase(wb);
                     qnext = qbase(wb + 1 == kNB ? 0 : wb + 1);
                 }
                 const u32x4 xa = ra[i], xb = rb[i];
-                ra[i] = ld(sA, kb + i);
-                rb[i] = ld(sB, kb + i);
+                if (!(HR_Q256_DIAG & 2)) {
+                    ra[i] = ld(sA, kb + i);
+                    rb[i] = ld(sB, kb + i);
+                } else {  // (timing build: the ring registers stay live without loads)
+                    ra[i] ^= xb;
+                    rb[i] ^= xa;
+                }
                 static_for<8>([&](auto B_) {
                     constexpr int b = decltype(B_)::value;
                     constexpr int p = i * 8 + b;  // pair within the span (slot p & 3: 128 pairs per span)
@@ -298,54 +346,87 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                     const uint32_t base = (kn / kWin) != (i / kWin) ? qnext : qcur;
                     pf[pn & 3] = lds_read<((kn % kWin) * 8 + (pn & 7)) * 1024>(base);
                     asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(pf[p & 3]) : "n"(kPf));
-                    acc[0][b] = mfma32<MT>(pf[p & 3], xa, acc[0][b]);
-                    acc[1][b] = mfma32<MT>(pf[p & 3], xb, acc[1][b]);
+                    if constexpr ((HR_Q256_DIAG & 8) != 0) {  // (timing build: operands consumed, no MFMA)
+                        dsink ^= pf[p & 3].x ^ pf[p & 3].w ^ xa.x ^ xb.y;
+                    } else {
+                        acc[0][b] = mfma32<MT>(pf[p & 3], xa, acc[0][b]);
+                        acc[1][b] = mfma32<MT>(pf[p & 3], xb, acc[1][b]);
+                    }
                 });
             });
         }
 
-        // ---- epilogue, block by block: the 16 scores of one 32-query block against their thresholds (read from LDS
-        // with inline asm: a compiler-visible LDS read would be fenced behind every LDS-DMA in flight -- vmcnt(0), the
-        // whole corpus ring), one ballot of "any register passes".  A passing block (rare after the first rounds) parks
-        // its scores in this wave's LDS slot and is walked register by register in a rolled loop, so the unrolled part
-        // stays small in registers and code.  Every accumulator read has constant indices (static_for).
-        static_for<2>([&](auto T_) {
-            constexpr int T = decltype(T_)::value;
-            const int64_t t = T ? tB : tA;
-            const uint32_t allow = T ? allowB : allowA;
-            const int rg = slot_row(t < 0 ? 0 : t, g);
-            const bool ok = (allow >> rg) & 1u;
-            const float xs = T ? xsB : xsA;
-            const float xm = a.xnorm ? 2.0f : 1.0f;  // euclidean: 2 q.x - |x|^2 (as k_scan)
-            const uint32_t row = (uint32_t)(t * 32 + rg);
+        if constexpr ((HR_Q256_DIAG & 16) != 0) {  // (timing build: no epilogue, the accumulators kept live)
+            float z = 0.0f;
+            static_for<2>([&](auto T_) {
+                static_for<8>([&](auto B_) { z += acc_read<0>(acc[decltype(T_)::value][decltype(B_)::value]); });
+            });
+            mycnt[0] += __builtin_bit_cast(uint32_t, z) + allowA + allowB;
+        }
+        HR_STAMP(s_r1);
+        // ---- epilogue, block by block: one read of the block's 16 thresholds (inline asm: a compiler-visible LDS read
+        // would be fenced behind every LDS-DMA in flight -- vmcnt(0), the whole corpus ring) serves both tiles; per
+        // tile the 16 scores against them and one ballot of "any register passes".  A passing block (rare after the
+        // first rounds) gets a 16-bit mask of its passing registers and a rolled loop over the set bits reads score and
+        // threshold at a dynamic register index, so the unrolled part stays small in code.  Inner product / cosine compare the
+        // accumulators themselves; euclidean forms 2 q.x - |x|^2 first (as k_scan).  Every accumulator read has
+        // constant indices (static_for).
+        auto epilogue = [&](auto EUC_) {
+            constexpr bool EUC = decltype(EUC_)::value;
+            const int rgA = slot_row(tA < 0 ? 0 : tA, g), rgB = slot_row(tB < 0 ? 0 : tB, g);
+            const bool okA = (allowA >> rgA) & 1u, okB = (allowB >> rgB) & 1u;
+            const uint32_t rowA = (uint32_t)(tA * 32 + rgA), rowB = (uint32_t)(tB * 32 + rgB);
             static_for<8>([&](auto B_) {
                 constexpr int b = decltype(B_)::value;
                 u32x4 t4[4];
                 lds_read4_wait<b * 128>(th_lane, t4);
                 // (bit_cast the whole vector, then index: this clang lowers a bit_cast of ONE component, t4[r][c], to
                 // component 0 for every c, and then loads only that dword)
-                float v[16];
-                float d = -__builtin_inff();
-                static_for<16>([&](auto I_) {
-                    constexpr int i = decltype(I_)::value;
-                    v[i] = __builtin_fmaf(xm, acc_read<i>(acc[T][b]), -xs);
-                    d = fmaxf(d, v[i] - __builtin_bit_cast(f32x4, t4[i >> 2])[i & 3]);
-                });
-                if (!__ballot(ok && d >= 0.0f)) return;
-                static_for<2>([&](auto H_) {  // (two halves of 8 registers: the LDS slot holds 8)
-                    constexpr int h8 = decltype(H_)::value * 8;
-                    static_for<8>([&](auto I_) {
+                f32x4 tf[4];
+                static_for<4>([&](auto R_) { tf[decltype(R_)::value] = __builtin_bit_cast(f32x4, t4[decltype(R_)::value]); });
+                static_for<2>([&](auto T_) {
+                    constexpr int T = decltype(T_)::value;
+                    const bool ok = T ? okB : okA;
+                    f32x16 V, TH;
+                    float d = -__builtin_inff();
+                    static_for<16>([&](auto I_) {
                         constexpr int i = decltype(I_)::value;
-                        lds_write_f32<i * 256>(sc_lane, v[h8 + i]);
+                        const float r = acc_read<i>(acc[T][b]);
+                        V[i] = EUC ? __builtin_fmaf(2.0f, r, -(T ? xsB : xsA)) : r;
+                        TH[i] = tf[i >> 2][i & 3];
+                        d = fmaxf(d, V[i] - TH[i]);
                     });
-                    walk_block(b, ok, row, mycnt[b >> 1], h8);
+                    if (!__ballot(ok && d >= 0.0f)) return;
+                    uint32_t regs = 0;  // the registers holding a passing score (wave-uniform bits)
+                    static_for<16>([&](auto I_) {
+                        constexpr int i = decltype(I_)::value;
+                        regs |= (__ballot(ok && V[i] >= TH[i]) != 0 ? 1u : 0u) << i;
+                    });
+                    walk_block(b, ok, T ? rowB : rowA, mycnt[b >> 1], V, TH, regs);
                 });
             });
-        });
+        };
+        if constexpr ((HR_Q256_DIAG & 24) == 0) {
+            if (a.xnorm) epilogue(std::true_type{});
+            else epilogue(std::false_type{});
+        }
+        HR_STAMP(s_r2);
         // thresholds of this wave's group: after rounds 1, 2, 4, 8 (the early keys rise fast), then every RT rounds
         const int64_t v1 = u + 1;
-        if ((v1 & (v1 - 1)) == 0 ? v1 <= 8 : (v1 % RT) == 0) refresh();
+        if ((v1 & (v1 - 1)) == 0 ? v1 <= 8 : (!(HR_Q256_DIAG & 32) && (v1 % RT) == 0)) refresh();
+#if HR_Q256_STAMPS
+        HR_STAMP(s_r3);
+        c_loop += s_r1 - s_r0;
+        c_epi += s_r2 - s_r1;
+        c_ref += s_r3 - s_r2;
+#endif
     }
+    if constexpr ((HR_Q256_DIAG & 8) != 0) mycnt[0] += dsink;
+#if HR_Q256_STAMPS
+    if (lane == 0 && (blockIdx.x % 32) == 0)
+        printf("q256 stamps blk %d wave %d rounds %ld loop %lu (window waits %lu) epilogue %lu refresh %lu\n", (int)blockIdx.x,
+               wv, (long)rounds, (unsigned long)c_loop, (unsigned long)c_wait, (unsigned long)c_epi, (unsigned long)c_ref);
+#endif
 #pragma unroll
     for (int x = 0; x < 4; ++x) a.pcnt[(x * W + wr) * 64 + lane] = mycnt[x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the look-ahead DMAs land before the workgroup's LDS goes)

@@ -20,7 +20,8 @@
 //    compiler's conservative LDS-DMA tracking inserts no vmcnt drain in front of them;
 //  * thresholds per query in LDS (shared by the four waves); group maxima raised in the global table with one
 //    fire-and-forget atomicMax per passing score (rare: only scores at or above their threshold can raise the
-//    minimum over the groups); a refresh re-reads the global keys for one 64-query group per wave;
+//    minimum over the groups); a refresh re-reads the global keys of the wave's 64-query group (a part of them per
+//    round, loaded a round ahead);
 //  * candidates go to k_scan's private per-(query group, wave) regions, so k_select reads them unchanged.
 // Exactness: the same invariant as the 128-query FILTER -- every row at or above a query's final threshold was
 // appended when scanned (thresholds only grow), and each group key is the score of an appended (or SAMPLE) row.
@@ -32,7 +33,7 @@ namespace hr {
 
 // HR_Q256_DIAG (timing builds only -- results are WRONG with any bit set): 1 no query-window staging in the loop,
 // 2 no corpus ring loads, 4 no per-window barrier, 8 no MFMA (operands consumed by a cheap VALU op) and no
-// epilogue, 16 no epilogue, 32 no refresh after round 8
+// epilogue, 16 no epilogue, 32 no refresh after round 2
 #ifndef HR_Q256_DIAG
 #define HR_Q256_DIAG 0
 #endif
@@ -59,9 +60,9 @@ constexpr int kQT = 256;              // threads per workgroup: 4 waves, one per
 constexpr int kWin = 2;               // k-steps per query window
 constexpr int kWQ = kWin * 8 * 64;    // u32x4 per window buffer: [k-step][block][lane]
 constexpr int kDma = kWQ / kQT;       // LDS-DMA instructions per thread per window
-// corpus ring depth in k-steps per tile: 16 (32 KiB in flight per wave) where the registers hold it spill-free --
-// at D = 512 / 768 (two or three ring spans per tile) the allocator spills a 16-deep ring, so 8 there
-constexpr int ring_for(int S) { return (S == 32 || S == 48) ? 8 : 16; }
+// corpus ring depth in k-steps per tile: 8 (16 KiB in flight per wave; 16 measured within 1.5 % at D = 1024 and
+// its registers are worth more as the partial refresh's: a refresh that drains the ring costs 7 %), 16 at D = 256
+constexpr int ring_for(int S) { return S == 16 ? 16 : 8; }
 template <int S_>
 struct Q256Geom {
     static constexpr int kRing = ring_for(S_);
@@ -102,6 +103,34 @@ __device__ __forceinline__ void lds_read4_wait(uint32_t base, u32x4 (&t)[4]) {
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
         : "v"(base), "n"(OFF), "n"(OFF + 32), "n"(OFF + 64), "n"(OFF + 96));
+}
+
+// sixteen ds_read_b128 at base + OFF + 32 r (four blocks' thresholds) and ONE wait
+template <int OFF>
+__device__ __forceinline__ void lds_read16_wait(uint32_t base, u32x4 (&t)[16]) {
+    asm volatile(
+        "ds_read_b128 %0, %16 offset:%17\n\tds_read_b128 %1, %16 offset:%18\n\tds_read_b128 %2, %16 offset:%19\n\t"
+        "ds_read_b128 %3, %16 offset:%20\n\tds_read_b128 %4, %16 offset:%21\n\tds_read_b128 %5, %16 offset:%22\n\t"
+        "ds_read_b128 %6, %16 offset:%23\n\tds_read_b128 %7, %16 offset:%24\n\tds_read_b128 %8, %16 offset:%25\n\t"
+        "ds_read_b128 %9, %16 offset:%26\n\tds_read_b128 %10, %16 offset:%27\n\tds_read_b128 %11, %16 offset:%28\n\t"
+        "ds_read_b128 %12, %16 offset:%29\n\tds_read_b128 %13, %16 offset:%30\n\tds_read_b128 %14, %16 offset:%31\n\t"
+        "ds_read_b128 %15, %16 offset:%32\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]),
+          "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]), "=&v"(t[12]), "=&v"(t[13]), "=&v"(t[14]), "=&v"(t[15])
+        : "v"(base), "n"(OFF), "n"(OFF + 32), "n"(OFF + 64), "n"(OFF + 96), "n"(OFF + 128), "n"(OFF + 160),
+          "n"(OFF + 192), "n"(OFF + 224), "n"(OFF + 256), "n"(OFF + 288), "n"(OFF + 320), "n"(OFF + 352), "n"(OFF + 384),
+          "n"(OFF + 416), "n"(OFF + 448), "n"(OFF + 480));
+}
+
+// eight ds_read_b32 at base + 8 j and ONE wait (the thresholds of queries 2 j apart)
+__device__ __forceinline__ void lds_read8_stride8_wait(uint32_t base, float (&t)[8]) {
+    asm volatile(
+        "ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:8\n\tds_read_b32 %2, %8 offset:16\n\t"
+        "ds_read_b32 %3, %8 offset:24\n\tds_read_b32 %4, %8 offset:32\n\tds_read_b32 %5, %8 offset:40\n\t"
+        "ds_read_b32 %6, %8 offset:48\n\tds_read_b32 %7, %8 offset:56\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
+        : "v"(base)
+        : "memory");
 }
 
 template <int OFF>
@@ -221,6 +250,46 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             lds_write_f32<8 * j>(th_q, fmaxf(lds_read_f32o<8 * j>(th_q), f));
         });
     };
+    // partial refresh: the keys of 2 kKR of the wave's 64 queries (part p), loaded at the START of a round into kKR
+    // registers and applied after its epilogue -- their wait then retires only loads issued a round earlier, where a
+    // refresh that loads and applies at once waits behind the whole corpus ring (a drain per refresh: 7 % of the
+    // launch).  A quarter per round: each query every 4 rounds.
+    constexpr int kKR = 8;
+    constexpr int kParts = 32 / kKR;
+    uint32_t qkey[kKR];
+    auto part_load = [&](int p) {
+        static_for<kKR>([&](auto J_) {  // query 64 wv + 2 kKR p + 2 j + half, group g
+            constexpr int j = decltype(J_)::value;
+            qkey[j] = __builtin_amdgcn_raw_buffer_load_b32(kr, key_lane, p * (kKR * 256) + j * 256, 16);
+        });
+    };
+    static_assert(kKR == 8, "lds_read8_stride8_wait");
+    auto part_apply = [&](int p) {  // (eight reductions interleaved step by step, one LDS round trip, eight writes)
+        const uint32_t base = th_q + (uint32_t)p * (kKR * 8u);
+        uint32_t m[kKR];  // order-preserving keys: the minimum over the half's 32 groups in integer compares
+        static_for<kKR>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            m[j] = qkey[j] > HR_KEY_NEG_INF ? qkey[j] : HR_KEY_NEG_INF;
+        });
+        auto step = [&](auto CTRL_) {
+            static_for<kKR>([&](auto J_) {
+                constexpr int j = decltype(J_)::value;
+                m[j] = min(m[j], dpp_u32<decltype(CTRL_)::value>(m[j]));
+            });
+        };
+        step(std::integral_constant<int, 0xB1>{});   // quad_perm 1,0,3,2
+        step(std::integral_constant<int, 0x4E>{});   // quad_perm 2,3,0,1
+        step(std::integral_constant<int, 0x141>{});  // row_half_mirror
+        step(std::integral_constant<int, 0x140>{});  // row_mirror
+        float t[kKR];
+        lds_read8_stride8_wait(base, t);
+        static_for<kKR>([&](auto J_) {  // lane l with l ^ 16 (v_permlane16_swap; no LDS swizzle and its wait)
+            constexpr int j = decltype(J_)::value;
+            const auto r = __builtin_amdgcn_permlane16_swap(m[j], m[j], false, false);
+            const uint32_t x = r[0], y = r[1];  // (components copied out first: see the bit_cast note in the epilogue)
+            lds_write_f32<8 * j>(base, fmaxf(t[j], key2f(min(x, y))));
+        });
+    };
     th_lds[tid] = a.floor_q[tid];  // (the floors once: thresholds only grow; kQT = 256 queries)
     __syncthreads();
     refresh();
@@ -276,13 +345,13 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
         if (a.mask) w0 &= scalar_word(a.mask, t);
         return w0;
     };
-    const int RT = std::max(1, a.refresh_every);
     // A fragments stream in (k-step, block) pairs -- pair p = 8 k + b of the running k-step count -- read kPf pairs
     // ahead into a 4-slot rotation (16 VGPRs instead of a whole k-step's 64): the two MFMAs of a pair (64 cycles)
     // cover the LDS latency of the reads behind it
     constexpr int kPf = HR_Q256_PF;
-    static_assert(kPf >= 1 && kPf <= 3, "4-slot rotation");
-    u32x4 pf[4];
+    static_assert(kPf >= 1 && kPf <= 3, "prefetch distance");
+    constexpr int kSlots = 4;  // (a power of two dividing the 128 pairs of a span: the rotation runs on across spans)
+    u32x4 pf[kSlots];
     static_for<kPf>([&](auto P_) { pf[decltype(P_)::value] = lds_read<decltype(P_)::value * 1024>(qbase(0)); });
     int wb = 0;  // buffer of the current window (window gw lives in buffer gw mod kNB)
     uint32_t qcur = qbase(0), qnext = qbase(1);  // this lane's address in the current / next window's buffer
@@ -293,6 +362,7 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
 #endif
     for (int64_t u = 0; u < rounds; ++u) {
         HR_STAMP(s_r0);
+        if (u >= 2 && !(HR_Q256_DIAG & 32)) part_load((int)(u % kParts));
         const int64_t tA = tile_of(u, 0), tB = tile_of(u, 1);
         const int64_t nA = tile_of(u + 1, 0), nB = tile_of(u + 1, 1);
         const uint32_t allowA = allow_word(tA), allowB = allow_word(tB);
@@ -344,13 +414,13 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                     constexpr int pn = p + kPf;   // the pair read now, kPf ahead (possibly in the next window / span)
                     constexpr int kn = pn >> 3;   // its k-step within the span (kRing: the next span's first)
                     const uint32_t base = (kn / kWin) != (i / kWin) ? qnext : qcur;
-                    pf[pn & 3] = lds_read<((kn % kWin) * 8 + (pn & 7)) * 1024>(base);
-                    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(pf[p & 3]) : "n"(kPf));
+                    pf[pn % kSlots] = lds_read<((kn % kWin) * 8 + (pn & 7)) * 1024>(base);
+                    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(pf[p % kSlots]) : "n"(kPf));
                     if constexpr ((HR_Q256_DIAG & 8) != 0) {  // (timing build: operands consumed, no MFMA)
-                        dsink ^= pf[p & 3].x ^ pf[p & 3].w ^ xa.x ^ xb.y;
+                        dsink ^= pf[p % kSlots].x ^ pf[p % kSlots].w ^ xa.x ^ xb.y;
                     } else {
-                        acc[0][b] = mfma32<MT>(pf[p & 3], xa, acc[0][b]);
-                        acc[1][b] = mfma32<MT>(pf[p & 3], xb, acc[1][b]);
+                        acc[0][b] = mfma32<MT>(pf[p % kSlots], xa, acc[0][b]);
+                        acc[1][b] = mfma32<MT>(pf[p % kSlots], xb, acc[1][b]);
                     }
                 });
             });
@@ -376,14 +446,22 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             const int rgA = slot_row(tA < 0 ? 0 : tA, g), rgB = slot_row(tB < 0 ? 0 : tB, g);
             const bool okA = (allowA >> rgA) & 1u, okB = (allowB >> rgB) & 1u;
             const uint32_t rowA = (uint32_t)(tA * 32 + rgA), rowB = (uint32_t)(tB * 32 + rgB);
+            // thresholds four blocks at a time (one LDS round trip per four blocks; one per block at D = 256, whose
+            // 16-deep ring leaves no room for 64 more registers)
+            constexpr int kTB = S_ == 16 ? 1 : 4;
+            u32x4 t4b[4 * kTB];
             static_for<8>([&](auto B_) {
                 constexpr int b = decltype(B_)::value;
-                u32x4 t4[4];
-                lds_read4_wait<b * 128>(th_lane, t4);
+                if constexpr (b % kTB == 0) {
+                    if constexpr (kTB == 4) lds_read16_wait<b * 128>(th_lane, t4b);
+                    else lds_read4_wait<b * 128>(th_lane, *(u32x4(*)[4])t4b);
+                }
                 // (bit_cast the whole vector, then index: this clang lowers a bit_cast of ONE component, t4[r][c], to
                 // component 0 for every c, and then loads only that dword)
                 f32x4 tf[4];
-                static_for<4>([&](auto R_) { tf[decltype(R_)::value] = __builtin_bit_cast(f32x4, t4[decltype(R_)::value]); });
+                static_for<4>([&](auto R_) {
+                    tf[decltype(R_)::value] = __builtin_bit_cast(f32x4, t4b[(b % kTB) * 4 + decltype(R_)::value]);
+                });
                 static_for<2>([&](auto T_) {
                     constexpr int T = decltype(T_)::value;
                     const bool ok = T ? okB : okA;
@@ -411,9 +489,10 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             else epilogue(std::false_type{});
         }
         HR_STAMP(s_r2);
-        // thresholds of this wave's group: after rounds 1, 2, 4, 8 (the early keys rise fast), then every RT rounds
-        const int64_t v1 = u + 1;
-        if ((v1 & (v1 - 1)) == 0 ? v1 <= 8 : (!(HR_Q256_DIAG & 32) && (v1 % RT) == 0)) refresh();
+        // thresholds of this wave's group: all of them after rounds 1 and 2 (the early keys rise fast), then a part
+        // after every round
+        if (u < 2) refresh();
+        else if (!(HR_Q256_DIAG & 32)) part_apply((int)(u % kParts));
 #if HR_Q256_STAMPS
         HR_STAMP(s_r3);
         c_loop += s_r1 - s_r0;

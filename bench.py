@@ -62,8 +62,10 @@ def parse():
     p.add_argument("--recall-queries", type=int, default=64, help="planted and isotropic queries of the recall checks")
     p.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline, recall and the GPU embed leg (quick runs)")
     p.add_argument("--no-embed", action="store_true", help="skip the GPU embed+search leg")
-    p.add_argument("--embed-cus", default="48,64,96,128",
-                   help="CU shares of the query embedder in the embed+search leg's CU-split runs ('' = none)")
+    # (off by default: with the CUs split 48/64/96/128 : rest the pipeline measured 5.4k / 6.6k / 7.0k / 7.0k QPS
+    # against 9.1k sharing every CU and 9.8k sequential -- profiles/r05_embed_cu_split.json)
+    p.add_argument("--embed-cus", default="",
+                   help="CU shares of the query embedder in the embed+search leg's CU-split runs, e.g. 64,96 ('' = none)")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: launcher only
     p.add_argument("--collective", action="store_true",
                    help="run the exchange through an RCCL process group even at --gpus 1 (world size 1): the timed "
@@ -359,9 +361,14 @@ def embed_search_cu_split(args, searcher, emb, texts, dev, K, B, s_out, r_out) -
             torch.cuda.synchronize()
             searcher.tail = tail0
             searcher.index.set_cu_mask(None)
-            for r in raw:
-                _native.destroy_stream(r)
+            # the masked streams stay alive to process exit: torch's caching allocator keeps per-stream records of the
+            # embedder's blocks, and destroying a stream under them aborted the interpreter at exit
+            # (std::bad_variant_access)
+            _KEEP_STREAMS.extend(raw)
     return out
+
+
+_KEEP_STREAMS: list = []
 
 
 def isotropic_queries(B: int, D: int, seed: int = 7) -> np.ndarray:

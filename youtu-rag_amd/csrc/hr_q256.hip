@@ -359,6 +359,7 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     uint32_t dsink = 0;  // (HR_Q256_DIAG & 8 timing builds only)
 #if HR_Q256_STAMPS
     uint64_t c_loop = 0, c_wait = 0, c_epi = 0, c_ref = 0;
+    uint32_t c_blocks = 0, c_regs = 0;  // passing tile-blocks and walked registers
 #endif
     for (int64_t u = 0; u < rounds; ++u) {
         HR_STAMP(s_r0);
@@ -462,25 +463,42 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                 static_for<4>([&](auto R_) {
                     tf[decltype(R_)::value] = __builtin_bit_cast(f32x4, t4b[(b % kTB) * 4 + decltype(R_)::value]);
                 });
+                // both tiles' scores and the max of (score - threshold) over the 16 registers first -- independent
+                // work and a reduction tree, not a chain of dependent maxima -- then the two ballots
+                f32x16 V[2], TH;
+                float d[2];
+                static_for<16>([&](auto I_) {
+                    constexpr int i = decltype(I_)::value;
+                    TH[i] = tf[i >> 2][i & 3];
+                });
                 static_for<2>([&](auto T_) {
                     constexpr int T = decltype(T_)::value;
-                    const bool ok = T ? okB : okA;
-                    f32x16 V, TH;
-                    float d = -__builtin_inff();
+                    float e[16];
                     static_for<16>([&](auto I_) {
                         constexpr int i = decltype(I_)::value;
                         const float r = acc_read<i>(acc[T][b]);
-                        V[i] = EUC ? __builtin_fmaf(2.0f, r, -(T ? xsB : xsA)) : r;
-                        TH[i] = tf[i >> 2][i & 3];
-                        d = fmaxf(d, V[i] - TH[i]);
+                        V[T][i] = EUC ? __builtin_fmaf(2.0f, r, -(T ? xsB : xsA)) : r;
+                        e[i] = V[T][i] - TH[i];
                     });
-                    if (!__ballot(ok && d >= 0.0f)) return;
+                    static_for<8>([&](auto I_) { e[decltype(I_)::value] = fmaxf(e[decltype(I_)::value], e[decltype(I_)::value + 8]); });
+                    static_for<4>([&](auto I_) { e[decltype(I_)::value] = fmaxf(e[decltype(I_)::value], e[decltype(I_)::value + 4]); });
+                    static_for<2>([&](auto I_) { e[decltype(I_)::value] = fmaxf(e[decltype(I_)::value], e[decltype(I_)::value + 2]); });
+                    d[T] = fmaxf(e[0], e[1]);
+                });
+                static_for<2>([&](auto T_) {
+                    constexpr int T = decltype(T_)::value;
+                    const bool ok = T ? okB : okA;
+                    if (!__ballot(ok && d[T] >= 0.0f)) return;
                     uint32_t regs = 0;  // the registers holding a passing score (wave-uniform bits)
                     static_for<16>([&](auto I_) {
                         constexpr int i = decltype(I_)::value;
-                        regs |= (__ballot(ok && V[i] >= TH[i]) != 0 ? 1u : 0u) << i;
+                        regs |= (__ballot(ok && V[T][i] >= TH[i]) != 0 ? 1u : 0u) << i;
                     });
-                    walk_block(b, ok, T ? rowB : rowA, mycnt[b >> 1], V, TH, regs);
+                    walk_block(b, ok, T ? rowB : rowA, mycnt[b >> 1], V[T], TH, regs);
+#if HR_Q256_STAMPS
+                    c_blocks += 1;
+                    c_regs += __builtin_popcount(regs);
+#endif
                 });
             });
         };
@@ -503,8 +521,9 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     if constexpr ((HR_Q256_DIAG & 8) != 0) mycnt[0] += dsink;
 #if HR_Q256_STAMPS
     if (lane == 0 && (blockIdx.x % 32) == 0)
-        printf("q256 stamps blk %d wave %d rounds %ld loop %lu (window waits %lu) epilogue %lu refresh %lu\n", (int)blockIdx.x,
-               wv, (long)rounds, (unsigned long)c_loop, (unsigned long)c_wait, (unsigned long)c_epi, (unsigned long)c_ref);
+        printf("q256 stamps blk %d wave %d rounds %ld loop %lu (window waits %lu) epilogue %lu refresh %lu blocks %u regs %u\n",
+               (int)blockIdx.x, wv, (long)rounds, (unsigned long)c_loop, (unsigned long)c_wait, (unsigned long)c_epi,
+               (unsigned long)c_ref, c_blocks, c_regs);
 #endif
 #pragma unroll
     for (int x = 0; x < 4; ++x) a.pcnt[(x * W + wr) * 64 + lane] = mycnt[x];

@@ -37,13 +37,14 @@ namespace hr {
 #ifndef HR_Q256_DIAG
 #define HR_Q256_DIAG 0
 #endif
-// A/B knobs (results identical): LDS prefetch distance in (k-step, block) pairs, a wave's two tiles adjacent
+// A/B knobs (results identical): LDS prefetch distance in (k-step, block) pairs, a wave's two tiles adjacent (1:
+// +0.7 % at 10M x 1024, B = 256)
 // (1) or W apart (0), the corpus loads' cache policy (2 = nt)
 #ifndef HR_Q256_PF
 #define HR_Q256_PF 2
 #endif
 #ifndef HR_Q256_ADJ
-#define HR_Q256_ADJ 0
+#define HR_Q256_ADJ 1
 #endif
 #ifndef HR_Q256_STAMPS  // diagnostic build: per-wave cycle shares of the round's phases, printed
 #define HR_Q256_STAMPS 0
@@ -67,10 +68,15 @@ template <int S_>
 struct Q256Geom {
     static constexpr int kRing = ring_for(S_);
     static constexpr int kLook = kRing / kWin;  // windows a window is staged ahead of its first use
-    static constexpr int kNB = kLook + 1;       // window buffers
-    // vmcnt at a window start that retires this wave's DMA of the NEXT window: younger than it are the ring loads
-    // of kLook - 1 windows (2 tiles x kWin k-steps each) and the DMAs of kLook - 2 windows
-    static constexpr int kVmNext = (kLook - 1) * 2 * kWin + (kLook - 2) * kDma;
+    // a workgroup barrier every kBar windows: with kLook + kBar buffers the DMA at window w refills the buffer of
+    // window w - kBar, which every wave has left by the last barrier (kBar = 2: half the barriers; one per window at
+    // D = 256, whose 16-deep ring leaves no LDS for two spare buffers)
+    static constexpr int kBar = S_ == 16 ? 1 : 2;
+    static constexpr int kNB = kLook + kBar;  // window buffers
+    // vmcnt at a barrier window that retires this wave's DMAs of the next kBar windows (the windows read before the
+    // next barrier): younger than the last of them are the ring loads of kLook - kBar windows (2 tiles x kWin
+    // k-steps each) and the DMAs of kLook - kBar - 1 windows
+    static constexpr int kVmNext = (kLook - kBar) * 2 * kWin + (kLook - kBar - 1) * kDma;
     static_assert(kVmNext <= 63, "vmcnt field");
 };
 
@@ -176,7 +182,7 @@ __device__ __forceinline__ uint64_t q256_stamp() {  // (diagnostic builds only: 
 template <int MT, int S_>
 __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     constexpr int kRing = Q256Geom<S_>::kRing, kLook = Q256Geom<S_>::kLook, kNB = Q256Geom<S_>::kNB;
-    constexpr int kVmNext = Q256Geom<S_>::kVmNext;
+    constexpr int kVmNext = Q256Geom<S_>::kVmNext, kBar = Q256Geom<S_>::kBar;
     static_assert(S_ % kRing == 0 && S_ % kWin == 0, "tile depth");
     __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
     __shared__ __attribute__((aligned(16))) float th_lds[256];
@@ -386,18 +392,21 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             static_for<kRing>([&](auto I_) {
                 constexpr int i = decltype(I_)::value;
                 if constexpr (i % kWin == 0) {
-                    // this wave's DMA of the next window has landed; the barrier makes every wave's visible and
-                    // retires every read of the buffer of the window before this one, which the DMA of the window
-                    // kLook ahead refills ((wb + kLook) mod kNB = wb - 1)
                     if (i > 0 || qs > 0 || u > 0) wb = wb + 1 == kNB ? 0 : wb + 1;
-                    HR_STAMP(s_w0);
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmNext) : "memory");
-                    if (!(HR_Q256_DIAG & 4)) __builtin_amdgcn_s_barrier();
+                    // (windows per span and per round are even, so the span-local parity is the global one)
+                    if constexpr ((i / kWin) % kBar == 0) {
+                        // this wave's DMAs of the next kBar windows have landed; the barrier makes every wave's
+                        // visible and retires every read of the buffers the DMAs of the next kBar windows refill
+                        HR_STAMP(s_w0);
+                        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmNext) : "memory");
+                        if (!(HR_Q256_DIAG & 4)) __builtin_amdgcn_s_barrier();
 #if HR_Q256_STAMPS
-                    HR_STAMP(s_w1);
-                    c_wait += s_w1 - s_w0;
+                        HR_STAMP(s_w1);
+                        c_wait += s_w1 - s_w0;
 #endif
-                    if (!(HR_Q256_DIAG & 1)) stage(wb == 0 ? kNB - 1 : wb - 1, (qs * kRing + i + kLook * kWin) % S_);
+                    }
+                    // the window kLook ahead goes into the buffer of window gw - kBar ((wb + kLook) mod kNB)
+                    if (!(HR_Q256_DIAG & 1)) stage(wb >= kBar ? wb - kBar : wb - kBar + kNB, (qs * kRing + i + kLook * kWin) % S_);
                     qcur = qbase(wb);
                     qnext = qbase(wb + 1 == kNB ? 0 : wb + 1);
                 }

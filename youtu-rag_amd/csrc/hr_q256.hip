@@ -37,9 +37,8 @@ namespace hr {
 #ifndef HR_Q256_DIAG
 #define HR_Q256_DIAG 0
 #endif
-// A/B knobs (results identical): LDS prefetch distance in (k-step, block) pairs, a wave's two tiles adjacent (1:
-// +0.7 % at 10M x 1024, B = 256)
-// (1) or W apart (0), the corpus loads' cache policy (2 = nt)
+// A/B knobs (results identical): LDS prefetch distance in (k-step, block) pairs, a wave's two tiles adjacent (1;
+// +0.7 % against W apart (0) at 10M x 1024, B = 256), the corpus loads' cache policy (2 = nt)
 #ifndef HR_Q256_PF
 #define HR_Q256_PF 2
 #endif

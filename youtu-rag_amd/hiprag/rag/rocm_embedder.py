@@ -181,6 +181,28 @@ def build_random_bert(preset: str = "bge-large", seed: int = 0, **overrides):
     return model
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
+
+
+def enable_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
+    """Load TunableOp GEMM results (read-only: tuning stays off, and the process's own results file is a private temp
+    path, so nothing rewrites the shipped one).  Returns whether the results were accepted (their validators --
+    torch, HIP, hipBLASLt, rocBLAS versions and the GPU arch -- must match this process)."""
+    import tempfile
+
+    import torch
+
+    if not (os.path.exists(path) and torch.cuda.is_available()):
+        return False
+    import torch.cuda.tunable as tun
+
+    tun.tuning_enable(False)
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"hiprag_tunableop_{os.getpid()}.csv"))
+    ok = bool(tun.read_file(path))
+    tun.enable(ok)
+    return ok
+
+
 class TorchRocmEmbedder(BaseEmbedder):
     """BaseEmbedder running the embedding model in-process on an MI355X (provider "rocm")."""
 
@@ -188,7 +210,8 @@ class TorchRocmEmbedder(BaseEmbedder):
                  batch_size: int = 64, max_length: int = 1024, gpu_id: int = 0, device=None, dtype: str = "float32",
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
                  trust_remote_code: bool = False, fused_layernorm: bool | None = None, unpadded: bool | None = None,
-                 forward_tokens: int | None = None, cuda_graphs: bool | None = None, **_ignored):
+                 forward_tokens: int | None = None, cuda_graphs: bool | None = None,
+                 tuned_gemms: bool | None = None, **_ignored):
         import torch
 
         self.torch = torch
@@ -215,6 +238,12 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.tokenizer = tokenizer if tokenizer is not None else HashWordTokenizer(
             getattr(getattr(model, "config", None), "vocab_size", 30522))
         self.model = model.to(self.device, tdt).eval()
+        # encoder GEMMs from the TunableOp results shipped for gfx950 (tools/embed_tune.py: every hipBLASLt / rocBLAS
+        # solution of the bge shapes at each 64-token count benchmarked, the fastest kept), read-only; shapes not in
+        # the file, or a file whose library versions do not match, keep the heuristic choice
+        if tuned_gemms is None:
+            tuned_gemms = self.device.type == "cuda" and self.dtype_name != "float32"
+        self.tuned_gemms = enable_tuned_gemms() if tuned_gemms else False
         # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
         self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0
         # the encoder over the real tokens only (hiprag.rag.encoder): fp16 / bf16 models on the GPU, where the

@@ -16,7 +16,7 @@ import shutil
 import statistics
 import sys
 
-FILTER_NAMES = ("k_scan_filter", "k_filter_wide8", "k_scan_persist")
+FILTER_NAMES = ("k_scan_filter", "k_filter_wide8", "k_filter_q256", "k_scan_persist")
 SAMPLE_NAMES = ("k_scan_sample",)
 # the measured practical read ceiling (tools/stream_ceiling.hip, profiles/r02_stream_ceiling.jsonl): a summary
 # whose FILTER rate exceeds it has mis-classified launches

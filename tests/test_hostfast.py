@@ -1,0 +1,80 @@
+"""The store's result assembly in C (csrc/host/hostfast.c) against the Python loop it replaces
+(storage._assemble_py): same (Chunk, score) lists on the same gathered hits -- rows deleted since the search (None),
+metadata without document_id / chunk_index, embeddings, queries with no hits -- and the same errors on malformed
+input.  CPU only."""
+import gc
+
+import pytest
+
+from hiprag.rag import storage
+from hiprag.rag.base import Chunk
+
+hostfast = pytest.importorskip("hiprag.rag._hostfast", reason="_hostfast not built (run __graft_entry__.build())")
+
+
+def _hits(n, seed=0):
+    import random
+
+    r = random.Random(seed)
+    rec, meta, sc = [], [], []
+    for i in range(n):
+        rec.append(None if r.random() < 0.1 else (f"id{i}", f"d{i % 7}", f"content {i}"))
+        m = {"src": f"s{i}"}
+        if r.random() < 0.8:
+            m["document_id"] = f"d{i % 7}"
+        if r.random() < 0.8:
+            m["chunk_index"] = i
+        meta.append(m)
+        sc.append(r.random())
+    return rec, meta, sc
+
+
+def _flat(res):
+    return [[(c.id, c.document_id, c.content, c.chunk_index, c.metadata, c.embedding, s) for c, s in q] for q in res]
+
+
+@pytest.mark.parametrize("with_embs", [False, True])
+def test_assemble_matches_python(with_embs):
+    rec, meta, sc = _hits(600, seed=3)
+    per_q = [10, 0, 37, 3, 250, 0, 300]
+    embs = [[float(i), -1.0] for i in range(600)] if with_embs else None
+    a = hostfast.assemble(Chunk, rec, meta, sc, per_q, embs)
+    b = storage._assemble_py(Chunk, rec, meta, sc, per_q, embs)
+    assert _flat(a) == _flat(b)
+    assert all(type(c) is Chunk for q in a for c, _ in q)
+    # metadata is a fresh copy per hit, as the Python loop makes
+    c0 = a[0][0][0]
+    j0 = next(j for j, r in enumerate(rec) if r is not None)
+    assert c0.metadata == meta[j0] and c0.metadata is not meta[j0]
+
+
+def test_assemble_objects_are_sound():
+    """The results outlive their inputs (references held, not borrowed); which results the collector is spared."""
+    rec, meta, sc = _hits(200, seed=5)
+    a = hostfast.assemble(Chunk, rec, meta, sc, [200], None)
+    del rec, meta, sc
+    gc.collect()
+    assert all(isinstance(s, float) and isinstance(c.metadata, dict) for c, s in a[0])
+    # atomic-valued hits are left untracked (the cycle collector does not walk them); embedding lists keep them tracked
+    assert not any(gc.is_tracked(c) for c, _ in a[0])
+    rec, meta, sc = _hits(5, seed=6)
+    e = hostfast.assemble(Chunk, rec, meta, sc, [5], [[1.0]] * 5)
+    assert all(gc.is_tracked(c) for c, _ in e[0])
+    assert gc.isenabled()
+
+
+def test_assemble_rejects_bad_input():
+    rec, meta, sc = _hits(10)
+    with pytest.raises(ValueError):
+        hostfast.assemble(Chunk, rec, meta, sc, [11], None)
+    with pytest.raises(ValueError):
+        hostfast.assemble(Chunk, rec, meta, sc[:5], [5], None)
+    with pytest.raises(TypeError):
+        hostfast.assemble(Chunk, [("only-id",)], [{}], [1.0], [1], None)
+
+    class NoSlots:
+        pass
+
+    with pytest.raises((TypeError, AttributeError)):
+        hostfast.assemble(NoSlots, rec, meta, sc, [10], None)
+    assert gc.isenabled()  # the collector is re-enabled on every error path

@@ -98,7 +98,12 @@ def main():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--torch", type=int, default=1, help="import torch first (a serving process's heap)")
     p.add_argument("--freeze", default="0", help="0/1 list: the application calls gc.freeze() after loading")
+    p.add_argument("--assemble", default="c", help="c / py: the store's result assembly (_hostfast or the Python loop)")
     a = p.parse_args()
+    if a.assemble == "py":
+        from hiprag.rag import storage
+
+        storage._hostfast = None
     if a.torch:
         import torch  # noqa: F401
     st = build(a.rows, a.dim, a.max_batch, a.k)
@@ -114,7 +119,7 @@ def main():
         g1 = [s["collections"] for s in gc.get_stats()]
         print(json.dumps({"freeze": fz, "qps": round(qps, 1), "clients": a.clients, "max_batch": a.max_batch,
                           "tracked_objects": len(gc.get_objects()), "collections_per_gen": [y - x for x, y in zip(g0, g1)],
-                          "torch": a.torch}), flush=True)
+                          "torch": a.torch, "assemble": a.assemble}), flush=True)
 
 
 if __name__ == "__main__":

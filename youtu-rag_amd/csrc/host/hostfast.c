@@ -1,0 +1,138 @@
+// _hostfast: the store's per-hit result assembly in C (HipVectorStore._assemble, storage.py).  A finished batch of
+// B queries x k hits becomes B lists of (Chunk, score) tuples; in Python each hit costs a slotted-dataclass __init__
+// frame, two dict lookups and a dict copy (~2 us), which bounds the store's event loop at ~23k queries/s while the
+// GPU serves 52k.  Here each Chunk is allocated with its type's tp_alloc and its six slots are written at the member
+// offsets read from the class once (no __init__ frame: the dataclass __init__ only assigns the fields), with the same
+// values the Python loop produces: id = rec[0], document_id = meta.get("document_id", ""), content = rec[2],
+// chunk_index = meta.get("chunk_index", 0), metadata = a fresh copy of meta, embedding = embs[j] or None.
+// A batch's hits are ~2 tracked objects each: without the two measures below the cycle collector (one gen-0 pass per
+// 700 allocations, each promoting half-built results) costs more than the assembly (tools/bench_store_host.py).
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <structmember.h>
+
+static const char* kFields[6] = {"id", "document_id", "content", "chunk_index", "metadata", "embedding"};
+
+static int slot_offsets(PyTypeObject* cls, Py_ssize_t off[6]) {
+    for (int f = 0; f < 6; ++f) {
+        PyObject* d = PyObject_GetAttrString((PyObject*)cls, kFields[f]);  // the class attribute: a member descriptor
+        if (!d) return -1;
+        if (!PyObject_TypeCheck(d, &PyMemberDescr_Type) || ((PyMemberDescrObject*)d)->d_member->type != T_OBJECT_EX) {
+            Py_DECREF(d);
+            PyErr_Format(PyExc_TypeError, "%s.%s is not a __slots__ member", cls->tp_name, kFields[f]);
+            return -1;
+        }
+        off[f] = ((PyMemberDescrObject*)d)->d_member->offset;
+        Py_DECREF(d);
+    }
+    return 0;
+}
+
+// assemble(cls, rec_l, meta_l, score_l, per_q, embs) -> list of B lists of (cls instance, float)
+static PyObject* assemble(PyObject* self, PyObject* args) {
+    PyTypeObject* cls;
+    PyObject *recs, *metas, *scores, *per_q, *embs;
+    if (!PyArg_ParseTuple(args, "O!O!O!O!O!O", &PyType_Type, &cls, &PyList_Type, &recs, &PyList_Type, &metas,
+                          &PyList_Type, &scores, &PyList_Type, &per_q, &embs))
+        return NULL;
+    if (cls->tp_dictoffset != 0) return PyErr_Format(PyExc_TypeError, "%s has a __dict__", cls->tp_name);
+    Py_ssize_t off[6];
+    if (slot_offsets(cls, off)) return NULL;
+    const Py_ssize_t n_hits = PyList_GET_SIZE(recs);
+    if (PyList_GET_SIZE(metas) != n_hits || PyList_GET_SIZE(scores) != n_hits ||
+        (embs != Py_None && (!PyList_Check(embs) || PyList_GET_SIZE(embs) != n_hits)))
+        return PyErr_Format(PyExc_ValueError, "hit lists of different lengths");
+    PyObject* k_doc = PyUnicode_InternFromString("document_id");
+    PyObject* k_idx = PyUnicode_InternFromString("chunk_index");
+    PyObject* empty = PyUnicode_FromString("");
+    PyObject* zero = PyLong_FromLong(0);
+    const Py_ssize_t B = PyList_GET_SIZE(per_q);
+    PyObject* out = PyList_New(B);
+    int gc_was = 0;
+    if (!k_doc || !k_idx || !empty || !zero || !out) goto fail;
+    // the cycle collector is held off while the batch's 2 tracked objects per hit are made: one deferred collection
+    // after the batch instead of one every 700 allocations, each promoting half-built results to older generations
+    gc_was = PyGC_Disable();
+    Py_ssize_t j = 0;
+    for (Py_ssize_t q = 0; q < B; ++q) {
+        const Py_ssize_t cnt = PyLong_AsSsize_t(PyList_GET_ITEM(per_q, q));
+        if (cnt < 0 || j + cnt > n_hits) {
+            if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "per-query counts exceed the hits");
+            goto fail;
+        }
+        PyObject* res = PyList_New(0);
+        if (!res) goto fail;
+        PyList_SET_ITEM(out, q, res);
+        for (Py_ssize_t e = j + cnt; j < e; ++j) {
+            PyObject* r = PyList_GET_ITEM(recs, j);
+            if (r == Py_None) continue;  // a row deleted since the search ran
+            PyObject* m = PyList_GET_ITEM(metas, j);
+            if (!PyTuple_Check(r) || PyTuple_GET_SIZE(r) < 3 || !PyDict_Check(m)) {
+                PyErr_SetString(PyExc_TypeError, "a host record is not (id, _, content) with a metadata dict");
+                goto fail;
+            }
+            PyObject* doc = PyDict_GetItemWithError(m, k_doc);
+            if (!doc && PyErr_Occurred()) goto fail;
+            PyObject* idx = PyDict_GetItemWithError(m, k_idx);
+            if (!idx && PyErr_Occurred()) goto fail;
+            PyObject* md = PyDict_Copy(m);
+            if (!md) goto fail;
+            PyObject* c = cls->tp_alloc(cls, 0);
+            if (!c) {
+                Py_DECREF(md);
+                goto fail;
+            }
+            PyObject* vals[6] = {PyTuple_GET_ITEM(r, 0), doc ? doc : empty, PyTuple_GET_ITEM(r, 2), idx ? idx : zero, md,
+                                 embs == Py_None ? Py_None : PyList_GET_ITEM(embs, j)};
+            for (int f = 0; f < 6; ++f) {
+                if (f != 4) Py_INCREF(vals[f]);  // (md: the new reference moves in)
+                *(PyObject**)((char*)c + off[f]) = vals[f];
+            }
+            PyObject* pair = PyTuple_New(2);
+            if (!pair) {
+                Py_DECREF(c);
+                goto fail;
+            }
+            PyObject* s = PyList_GET_ITEM(scores, j);
+            Py_INCREF(s);
+            PyTuple_SET_ITEM(pair, 0, c);
+            PyTuple_SET_ITEM(pair, 1, s);
+            if (!PyObject_GC_IsTracked(md) && (vals[5] == Py_None || !PyObject_IS_GC(vals[5]))) {
+                // a Chunk of strings, numbers and an untracked (atomic-valued) metadata dict references no container
+                // that can lead back to it, so the cycle collector is given none of a batch's hits to walk: as
+                // CPython does for tuples and dicts of atomic values (the pair tuple is one; the dict stays
+                // untracked until a container is stored in it).  What this gives up: a cycle a caller later
+                // builds THROUGH a returned Chunk (its own metadata holding the Chunk) is not collected.
+                PyObject_GC_UnTrack(c);
+                PyObject_GC_UnTrack(pair);
+            }
+            if (PyList_Append(res, pair)) {
+                Py_DECREF(pair);
+                goto fail;
+            }
+            Py_DECREF(pair);
+        }
+    }
+    if (gc_was) PyGC_Enable();
+    Py_DECREF(k_doc);
+    Py_DECREF(k_idx);
+    Py_DECREF(empty);
+    Py_DECREF(zero);
+    return out;
+fail:
+    if (gc_was) PyGC_Enable();
+    Py_XDECREF(k_doc);
+    Py_XDECREF(k_idx);
+    Py_XDECREF(empty);
+    Py_XDECREF(zero);
+    Py_XDECREF(out);
+    return NULL;
+}
+
+static PyMethodDef kMethods[] = {
+    {"assemble", assemble, METH_VARARGS, "assemble(cls, rec_l, meta_l, score_l, per_q, embs) -> list[list[(cls, score)]]"},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_hostfast", NULL, -1, kMethods};
+
+PyMODINIT_FUNC PyInit__hostfast(void) { return PyModule_Create(&kModule); }

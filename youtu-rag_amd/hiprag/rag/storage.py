@@ -60,6 +60,28 @@ from . import persist as P
 from .base import BaseVectorStore, Chunk
 from .config import VectorStoreConfig
 
+try:  # the per-hit result assembly in C (csrc/host/hostfast.c, built by csrc/Makefile); host-side only, same output
+    from . import _hostfast
+except ImportError:  # pragma: no cover - a source tree without the build: the Python loop below
+    _hostfast = None
+
+
+def _assemble_py(C, rec_l, meta_l, score_l, per_q, embs):
+    """The per-query (Chunk, score) lists of a batch's gathered hits; _hostfast.assemble is the same in C."""
+    out, i = [], 0
+    for cnt in per_q:  # one pass: each query's hits straight into its list
+        res = []
+        for j in range(i, i + cnt):
+            r = rec_l[j]
+            if r is None:
+                continue
+            m = meta_l[j]
+            res.append((C(r[0], m.get("document_id", ""), r[2], m.get("chunk_index", 0), dict(m),
+                          None if embs is None else embs[j]), score_l[j]))
+        out.append(res)
+        i += cnt
+    return out
+
 logger = logging.getLogger(__name__)
 
 _METRIC = {"cosine": "cosine", "dot": "ip", "euclidean": "l2"}
@@ -237,7 +259,7 @@ class _SearchBatcher:
                         continue
                     for e, r in zip(batch, res):
                         if not e[4].done():
-                            e[4].set_result(r[: e[1]])
+                            e[4].set_result(r if len(r) <= e[1] else r[: e[1]])
                 batch = []
         except BaseException as exc:  # never leave a waiter hanging: fail what this drain holds
             err = exc if isinstance(exc, Exception) else RuntimeError(f"search batcher stopped: {exc!r}")
@@ -771,20 +793,7 @@ class HipVectorStore(BaseVectorStore):
             embs = [None] * len(rec_l)
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
-        C = Chunk
-        out, i = [], 0
-        for cnt in per_q:  # one pass: each query's hits straight into its list
-            res = []
-            for j in range(i, i + cnt):
-                r = rec_l[j]
-                if r is None:
-                    continue
-                m = meta_l[j]
-                res.append((C(r[0], m.get("document_id", ""), r[2], m.get("chunk_index", 0), dict(m),
-                              None if embs is None else embs[j]), score_l[j]))
-            out.append(res)
-            i += cnt
-        return out
+        return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, rec_l, meta_l, score_l, per_q, embs)
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:

@@ -5,8 +5,9 @@
 // offsets read from the class once (no __init__ frame: the dataclass __init__ only assigns the fields), with the same
 // values the Python loop produces: id = rec[0], document_id = meta.get("document_id", ""), content = rec[2],
 // chunk_index = meta.get("chunk_index", 0), metadata = a fresh copy of meta, embedding = embs[j] or None.
-// A batch's hits are ~2 tracked objects each: without the two measures below the cycle collector (one gen-0 pass per
-// 700 allocations, each promoting half-built results) costs more than the assembly (tools/bench_store_host.py).
+// A batch's hits would be 2 tracked objects each (the Chunk and its pair tuple): walked by every gen-0 pass of the
+// cycle collector and promoted with the results held, the collector cost more than the assembly did
+// (tools/bench_store_host.py); see the untracking below.  The collector itself is never switched off.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <structmember.h>
@@ -48,11 +49,7 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
     PyObject* zero = PyLong_FromLong(0);
     const Py_ssize_t B = PyList_GET_SIZE(per_q);
     PyObject* out = PyList_New(B);
-    int gc_was = 0;
     if (!k_doc || !k_idx || !empty || !zero || !out) goto fail;
-    // the cycle collector is held off while the batch's 2 tracked objects per hit are made: one deferred collection
-    // after the batch instead of one every 700 allocations, each promoting half-built results to older generations
-    gc_was = PyGC_Disable();
     Py_ssize_t j = 0;
     for (Py_ssize_t q = 0; q < B; ++q) {
         const Py_ssize_t cnt = PyLong_AsSsize_t(PyList_GET_ITEM(per_q, q));
@@ -113,14 +110,12 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
             Py_DECREF(pair);
         }
     }
-    if (gc_was) PyGC_Enable();
     Py_DECREF(k_doc);
     Py_DECREF(k_idx);
     Py_DECREF(empty);
     Py_DECREF(zero);
     return out;
 fail:
-    if (gc_was) PyGC_Enable();
     Py_XDECREF(k_doc);
     Py_XDECREF(k_idx);
     Py_XDECREF(empty);

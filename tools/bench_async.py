@@ -82,9 +82,21 @@ def main():
     p.add_argument("--torch", type=int, default=1,
                    help="import torch first: a serving process's heap (the in-process embedder), ~170k tracked objects "
                         "that every full collection walks unless the application froze them")
+    p.add_argument("--profile", default="", help="write a cProfile summary of each measured run to PATH.<clients>_<mb>")
     args = p.parse_args()
 
     import gc
+
+    gc_time = [0.0, 0.0, 0.0]  # seconds inside collections, per generation
+    gc_t0 = [0.0]
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gc_t0[0] = time.perf_counter()
+        else:
+            gc_time[info["generation"]] += time.perf_counter() - gc_t0[0]
+
+    gc.callbacks.append(on_gc)
 
     if args.torch:
         import torch  # noqa: F401
@@ -112,9 +124,20 @@ def main():
             st._batcher.max_batch, st._batcher.depth, st.native_async = mb, depth, bool(na)
             asyncio.run(run_clients(st, queries, 64, 0.5, args.k))  # warm
             for C in (int(x) for x in args.clients.split(",")):
-                gc0 = sum(s["collections"] for s in gc.get_stats())
+                gc0 = [s["collections"] for s in gc.get_stats()]
+                gct0 = list(gc_time)
                 nat0 = st._batcher.native_launches
+                if args.profile:
+                    import cProfile
+                    import pstats
+
+                    prof = cProfile.Profile()
+                    prof.enable()
                 lat, wall, launches = asyncio.run(run_clients(st, queries, C, args.seconds, args.k))
+                if args.profile:
+                    prof.disable()
+                    with open(f"{args.profile}.{C}_{mb}", "w") as f:
+                        pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(30)
                 a = np.asarray(lat) * 1e3
                 print(json.dumps({"rows": args.rows, "max_batch": mb, "depth": depth, "gc_freeze": fz,
                                   "native_async": na, "native_launches": st._batcher.native_launches - nat0,
@@ -123,7 +146,10 @@ def main():
                                   "latency_ms_p50": round(float(np.percentile(a, 50)), 3),
                                   "latency_ms_p99": round(float(np.percentile(a, 99)), 3),
                                   "launches": launches, "mean_launch_size": round(len(lat) / max(1, launches), 1),
-                                  "gc_collections": sum(s["collections"] for s in gc.get_stats()) - gc0}),
+                                  "gc_collections": sum(s["collections"] for s in gc.get_stats()) - sum(gc0),
+                                  "gc_collections_per_gen": [s["collections"] - c for s, c in zip(gc.get_stats(), gc0)],
+                                  "gc_ms_per_gen": [round(1e3 * (t - t0), 1) for t, t0 in zip(gc_time, gct0)],
+                                  "profiled": bool(args.profile)}),
                       flush=True)
 
 

@@ -145,7 +145,10 @@ class _SearchBatcher:
         self._native: deque = deque()  # completion futures of native launches, in submission order
         self._loop = None         # the loop the eventfd reader is registered with
 
-    async def search(self, q: np.ndarray, top_k: int, filters):
+    def submit(self, q: np.ndarray, top_k: int, filters) -> asyncio.Future:
+        """Queue one query; the future resolves to its (Chunk, score) list.  A plain call, not a coroutine: the
+        caller's own coroutine awaits the future, so a query in flight holds one coroutine frame fewer for the
+        cycle collector to walk and promote (the store's event loop is collector-bound under load)."""
         dim = self.store.dim
         if dim is not None and q.shape[0] != dim:  # checked before queueing: a bad query fails alone
             raise ValueError(f"query dim {q.shape[0]} != collection dim {dim}")
@@ -156,7 +159,7 @@ class _SearchBatcher:
             self.running = True
             # start draining on the next loop iteration: every task that is ready now enqueues first
             loop.call_soon(lambda: loop.create_task(self._drain()))
-        return await fut
+        return fut
 
     def _take(self):
         key = self.pending[0][3]
@@ -800,7 +803,7 @@ class HipVectorStore(BaseVectorStore):
         if int(top_k) <= 0:
             return []
         q = np.asarray(query_embedding, dtype=np.float32).reshape(-1)
-        return await self._batcher.search(q, top_k, filters)
+        return await self._batcher.submit(q, top_k, filters)
 
     def get_by_id_sync(self, chunk_id: str) -> Chunk | None:
         with self._lock:

@@ -458,3 +458,29 @@ def test_store_leaves_the_collector_alone(tmp_path, monkeypatch):
     with s.deferred_save():
         s.add_chunks_sync(chunks("b", 300, seed=1))
     assert not calls and gc.isenabled()
+
+
+def test_cancelled_search_leaves_its_batch_alone(tmp_path):
+    """One client cancelling its search (a request timeout) cancels only its own future: the other queries of
+    the same native batch get their answers, the batch is still collected, and the store keeps serving."""
+    s, holder = make_async_store(tmp_path, max_batch=16)
+    s.add_chunks_sync(chunks("a", 200))
+    q = np.random.default_rng(13).standard_normal((12, 16)).astype(np.float32)
+    want = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q, 4)]
+    holder["idx"].delay = 0.05
+
+    async def main():
+        tasks = [asyncio.ensure_future(s.search(query_embedding=x.tolist(), top_k=4)) for x in q]
+        await asyncio.sleep(0.01)  # the batch is in flight
+        tasks[3].cancel()
+        done = await asyncio.gather(*tasks, return_exceptions=True)
+        again = await s.search(query_embedding=q[0].tolist(), top_k=4)
+        return done, again
+
+    done, again = run(main())
+    assert isinstance(done[3], asyncio.CancelledError)
+    assert [[(c.id, sc) for c, sc in r] for i, r in enumerate(done) if i != 3] == \
+        [w for i, w in enumerate(want) if i != 3]
+    assert [(c.id, sc) for c, sc in again] == want[0]
+    assert s._batcher.native_launches >= 1 and not holder["idx"].tickets
+    s.close()

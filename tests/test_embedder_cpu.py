@@ -87,6 +87,43 @@ def test_embedder_matches_reference_encode_on_cpu(cpu_emb):
     assert cpu_emb.max_length == 64
 
 
+def test_concurrent_embed_query_calls_share_forwards(cpu_emb):
+    """The reference's retrieve() embeds one query per call; concurrent calls are coalesced into forwards of up to
+    batch_size queries (run in the embedder's worker thread), each caller getting its own query's vector; a
+    cancelled call leaves the rest of its forward alone."""
+    qs = [f"query number {i} about w{i * 7 % 13}" for i in range(8)]
+    want = cpu_emb.encode_queries(qs).numpy()
+    co = cpu_emb._coalescer
+    f0, n0 = co.forwards, co.queries
+
+    async def main():
+        tasks = [asyncio.ensure_future(cpu_emb.embed_query(q)) for q in qs]
+        await asyncio.sleep(0)  # every call has queued its query
+        tasks[5].cancel()
+        return await asyncio.gather(*tasks, return_exceptions=True)
+
+    got = run(main())
+    assert isinstance(got[5], asyncio.CancelledError)
+    for i, v in enumerate(got):
+        if i != 5:
+            assert isinstance(v, list) and len(v) == want.shape[1]
+            np.testing.assert_allclose(v, want[i], rtol=0, atol=1e-5)
+    # 8 calls, batch_size 3: at most ceil(7 / 3) + 1 forwards, never one per call
+    assert co.queries - n0 in (7, 8) and co.forwards - f0 <= 4
+    # a failing forward reaches every caller of its batch, and the coalescer keeps serving
+    inner = cpu_emb._query_lists
+    cpu_emb._query_lists = lambda q: (_ for _ in ()).throw(RuntimeError("forward failed"))
+    try:
+        async def two():
+            return await asyncio.gather(*[cpu_emb.embed_query(q) for q in qs[:2]], return_exceptions=True)
+
+        bad = run(two())
+    finally:
+        cpu_emb._query_lists = inner
+    assert all(isinstance(e, RuntimeError) for e in bad)
+    np.testing.assert_allclose(run(cpu_emb.embed_query(qs[0])), want[0], rtol=0, atol=1e-5)
+
+
 def test_embedder_rejects_missing_local_model():
     with pytest.raises(FileNotFoundError):
         TorchRocmEmbedder("/nonexistent/model", device="cpu")

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""The reference's query path under concurrent callers: C client coroutines each call
+``VectorRetriever.retrieve(query)`` in a loop (base_retriever.py:53-59: embed_query, then store.search with
+``query_embedding=``), against a HipVectorStore of N synthetic rows and the in-process bge-large-shaped embedder
+(random init, bf16).  One JSON line per (coalesce, clients): throughput, latency, forwards and launches.
+``--coalesce 0`` is the per-call forward (one query per forward, on the event loop).
+Usage: python tools/bench_retrieve.py [--rows 10000000 --clients 64,256 --coalesce 1,0 --seconds 4]"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "youtu-rag_amd"), REPO, os.path.join(REPO, "tools")]
+
+
+def queries(n: int, seed: int = 5) -> list[str]:
+    import random
+
+    r = random.Random(seed)
+    words = [f"term{i}" for i in range(5000)]
+    return [" ".join(r.choice(words) for _ in range(r.randint(6, 20))) + "?" for _ in range(n)]
+
+
+async def clients(ret, qs, C: int, seconds: float, k: int):
+    lat: list[float] = []
+    stop = time.perf_counter() + seconds
+
+    async def client(c):
+        j = c
+        while time.perf_counter() < stop:
+            t0 = time.perf_counter()
+            res = await ret.retrieve(qs[j % len(qs)], top_k=k)
+            lat.append(time.perf_counter() - t0)
+            assert len(res) == k
+            j += C
+
+    t0 = time.perf_counter()
+    await asyncio.gather(*(client(c) for c in range(C)))
+    return lat, time.perf_counter() - t0
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", type=int, default=10_000_000)
+    p.add_argument("--clients", default="64,256")
+    p.add_argument("--coalesce", default="1,0")
+    p.add_argument("--seconds", type=float, default=4.0)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--max-batch", type=int, default=64, help="store search batches and embed forwards")
+    a = p.parse_args()
+
+    import numpy as np
+    import torch  # noqa: F401
+
+    from bench_async import build_store
+    from hiprag.rag import RetrieverConfig, VectorRetriever
+    from hiprag.rag.rocm_embedder import TorchRocmEmbedder, _QueryCoalescer
+
+    t0 = time.perf_counter()
+    st, _ = build_store(a.rows, a.max_batch)
+    emb = TorchRocmEmbedder(preset="bge-large", dtype="bfloat16", batch_size=a.max_batch, max_length=512)
+    ret = VectorRetriever(st, emb, RetrieverConfig(top_k=a.k, similarity_threshold=0.0))
+    qs = queries(4096)
+    emb.encode_queries(qs[:a.max_batch])  # graph capture of the common shapes
+    print(f"# store of {a.rows} rows + embedder in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    for co in (int(x) for x in a.coalesce.split(",")):
+        emb._coalescer = _QueryCoalescer(emb, a.max_batch) if co else None
+        asyncio.run(clients(ret, qs, 64, 1.0, a.k))  # warm: the graphs of the batch shapes this mode makes
+        for C in (int(x) for x in a.clients.split(",")):
+            l0 = st._batcher.launches
+            f0 = emb._coalescer.forwards if co else 0
+            lat, wall = asyncio.run(clients(ret, qs, C, a.seconds, a.k))
+            ms = np.asarray(lat) * 1e3
+            print(json.dumps({"rows": a.rows, "coalesce": co, "clients": C, "queries": len(lat),
+                              "qps": round(len(lat) / wall, 1),
+                              "latency_ms_p50": round(float(np.percentile(ms, 50)), 2),
+                              "latency_ms_p99": round(float(np.percentile(ms, 99)), 2),
+                              "embed_forwards": (emb._coalescer.forwards - f0) if co else len(lat),
+                              "search_launches": st._batcher.launches - l0,
+                              "model": "bge-large shape (random init), bf16", "path": "VectorRetriever.retrieve"}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,10 +25,13 @@ seeded init, with the offline HashWordTokenizer below.
 """
 from __future__ import annotations
 
+import asyncio
 import itertools
 import os
 import re
+import threading
 import zlib
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -203,6 +206,74 @@ def enable_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
     return ok
 
 
+
+class _QueryCoalescer:
+    """Concurrent ``embed_query`` calls as ONE forward: the reference embeds per call (VectorRetriever.retrieve,
+    base_retriever.py:57, one HTTP request each), so N concurrent retrievals were N one-query forwards run on the
+    event loop, each blocking it.  Here a call queues its query and awaits its own future (so a caller's
+    cancellation cancels only its query); a drain task takes up to ``max_batch`` waiting queries per forward and
+    runs it in one worker thread (the GPU wait and the host list conversion off the loop), one batch at a time
+    while the next one gathers.  Each vector is the one ``encode_queries`` gives for that query (rows are
+    independent through the encoder; a different batch size can only change GEMM rounding)."""
+
+    def __init__(self, emb, max_batch: int):
+        self.emb, self.max_batch = emb, max(1, int(max_batch))
+        self.pending: list = []
+        self.running = False
+        self.forwards = 0  # diagnostics: forwards run / queries embedded through them
+        self.queries = 0
+        self._pool = None
+
+    def submit(self, query: str) -> asyncio.Future:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self.pending.append((query, fut))
+        if not self.running:
+            self.running = True
+            # drain on the next loop iteration: every task that is ready now queues its query first
+            loop.call_soon(lambda: loop.create_task(self._drain()))
+        return fut
+
+    async def _drain(self):
+        loop = asyncio.get_running_loop()
+        batch: list = []
+        try:
+            while self.pending:
+                batch, self.pending = self.pending[: self.max_batch], self.pending[self.max_batch:]
+                batch = [e for e in batch if not e[1].done()]  # (cancelled while waiting)
+                if not batch:
+                    continue
+                if self._pool is None:
+                    self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-embed")
+                try:
+                    vecs = await loop.run_in_executor(self._pool, self.emb._query_lists, [q for q, _ in batch])
+                except Exception as exc:  # noqa: BLE001 -- this batch's callers see the failure
+                    for _, f in batch:
+                        if not f.done():
+                            f.set_exception(exc)
+                    batch = []
+                    continue
+                self.forwards += 1
+                self.queries += len(batch)
+                for (_, f), v in zip(batch, vecs):
+                    if not f.done():
+                        f.set_result(v)
+                batch = []
+        except BaseException as exc:  # the drain itself stopped (loop shutdown): no caller is left waiting
+            err = exc if isinstance(exc, Exception) else RuntimeError(f"query embedding stopped: {exc!r}")
+            for _, f in batch + self.pending:
+                if not f.done():
+                    f.set_exception(err)
+            self.pending = []
+            raise
+        finally:
+            self.running = False
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+
 class TorchRocmEmbedder(BaseEmbedder):
     """BaseEmbedder running the embedding model in-process on an MI355X (provider "rocm")."""
 
@@ -211,7 +282,7 @@ class TorchRocmEmbedder(BaseEmbedder):
                  query_instruction: str | None = DEFAULT_QUERY_INSTRUCTION, seed: int = 0,
                  trust_remote_code: bool = False, fused_layernorm: bool | None = None, unpadded: bool | None = None,
                  forward_tokens: int | None = None, cuda_graphs: bool | None = None,
-                 tuned_gemms: bool | None = None, **_ignored):
+                 tuned_gemms: bool | None = None, coalesce_queries: bool = True, **_ignored):
         import torch
 
         self.torch = torch
@@ -273,6 +344,12 @@ class TorchRocmEmbedder(BaseEmbedder):
         if forward_tokens is None:
             forward_tokens = int(os.environ.get("HIPRAG_FORWARD_TOKENS", "0"))
         self.forward_tokens = max(0, int(forward_tokens))
+        # forwards from more than one thread (the query coalescer's worker, ingest on the loop) take turns: the HIP
+        # graphs' static inputs are shared (GPU order is the device's stream order either way)
+        self._fwd_lock = threading.Lock()
+        # concurrent embed_query calls share forwards of up to batch_size queries (False: one forward per call,
+        # on the calling thread, as before)
+        self._coalescer = _QueryCoalescer(self, self.batch_size) if coalesce_queries else None
 
     # ------------------------------------------------------------------ core
     def _n_instruction_tokens(self, instruction: str) -> int:
@@ -304,7 +381,7 @@ class TorchRocmEmbedder(BaseEmbedder):
         if self.unpadded is not None:  # real tokens only: packed on the host, one upload, packed K7
             return self._forward_packed([inputs], n_instr)
         inputs = {k: (v.pin_memory() if pin else v).to(self.device, non_blocking=True) for k, v in inputs.items()}
-        with torch.inference_mode():
+        with self._fwd_lock, torch.inference_mode():
             hidden = self.model(**inputs)[0]
             if hidden.dtype != getattr(torch, self.dtype_name):
                 hidden = hidden.to(getattr(torch, self.dtype_name))
@@ -315,7 +392,7 @@ class TorchRocmEmbedder(BaseEmbedder):
     def _forward_packed(self, batches: list, n_instr: int):
         """Unpadded forward of one or more tokenizer batches as ONE packed batch -> (sum B, H) float32."""
         torch = self.torch
-        with torch.inference_mode():
+        with self._fwd_lock, torch.inference_mode():
             gf = self.graphed
             ntok = sum(int(b["attention_mask"].sum()) for b in batches)
             if gf is not None and ntok + gf.granule > gf.max_tokens:
@@ -394,8 +471,13 @@ class TorchRocmEmbedder(BaseEmbedder):
     async def embed_texts(self, texts: list[str]) -> list[list[float]]:
         return self.encode_passages(list(texts)).cpu().tolist()
 
+    def _query_lists(self, queries: list[str]) -> list[list[float]]:
+        return self.encode_queries(list(queries)).cpu().numpy().tolist()
+
     async def embed_query(self, query: str) -> list[float]:
-        return self.encode_queries([query])[0].cpu().tolist()
+        if self._coalescer is None:
+            return self.encode_queries([query])[0].cpu().tolist()
+        return await self._coalescer.submit(query)
 
     async def embed_queries(self, queries: list[str]) -> list[list[float]]:
         return self.encode_queries(list(queries)).cpu().tolist()

@@ -51,7 +51,8 @@ def main():
     p.add_argument("--coalesce", default="1,0")
     p.add_argument("--seconds", type=float, default=4.0)
     p.add_argument("--k", type=int, default=10)
-    p.add_argument("--max-batch", type=int, default=64, help="store search batches and embed forwards")
+    p.add_argument("--max-batch", type=int, default=64, help="store search batches (and the embedder's batch_size)")
+    p.add_argument("--embed-batch", default="64", help="comma list: queries per coalesced forward (A/B)")
     a = p.parse_args()
 
     import numpy as np
@@ -68,15 +69,15 @@ def main():
     qs = queries(4096)
     emb.encode_queries(qs[:a.max_batch])  # graph capture of the common shapes
     print(f"# store of {a.rows} rows + embedder in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
-    for co in (int(x) for x in a.coalesce.split(",")):
-        emb._coalescer = _QueryCoalescer(emb, a.max_batch) if co else None
+    for co, eb in ((c, e) for c in (int(x) for x in a.coalesce.split(",")) for e in (int(x) for x in a.embed_batch.split(","))):
+        emb._coalescer = _QueryCoalescer(emb, eb) if co else None
         asyncio.run(clients(ret, qs, 64, 1.0, a.k))  # warm: the graphs of the batch shapes this mode makes
         for C in (int(x) for x in a.clients.split(",")):
             l0 = st._batcher.launches
             f0 = emb._coalescer.forwards if co else 0
             lat, wall = asyncio.run(clients(ret, qs, C, a.seconds, a.k))
             ms = np.asarray(lat) * 1e3
-            print(json.dumps({"rows": a.rows, "coalesce": co, "clients": C, "queries": len(lat),
+            print(json.dumps({"rows": a.rows, "coalesce": co, "embed_batch": eb if co else 1, "clients": C, "queries": len(lat),
                               "qps": round(len(lat) / wall, 1),
                               "latency_ms_p50": round(float(np.percentile(ms, 50)), 2),
                               "latency_ms_p99": round(float(np.percentile(ms, 99)), 2),

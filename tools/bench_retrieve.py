@@ -53,6 +53,7 @@ def main():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--max-batch", type=int, default=64, help="store search batches (and the embedder's batch_size)")
     p.add_argument("--embed-batch", default="64", help="comma list: queries per coalesced forward (A/B)")
+    p.add_argument("--profile", default="", help="write a cProfile summary (event-loop thread) to PATH.<clients>")
     a = p.parse_args()
 
     import numpy as np
@@ -69,13 +70,43 @@ def main():
     qs = queries(4096)
     emb.encode_queries(qs[:a.max_batch])  # graph capture of the common shapes
     print(f"# store of {a.rows} rows + embedder in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    # the worker's time per forward, split: host tokenise + pack + launch, the device wait, the host lists
+    wt = {"launch": 0.0, "wait": 0.0, "lists": 0.0, "n": 0}
+
+    def timed_lists(qs_):
+        t1 = time.perf_counter()
+        x = emb.encode_queries(list(qs_))
+        t2 = time.perf_counter()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        out = x.cpu().numpy().tolist()
+        wt["launch"] += t2 - t1
+        wt["wait"] += t3 - t2
+        wt["lists"] += time.perf_counter() - t3
+        wt["n"] += 1
+        return out
+
+    emb._query_lists = timed_lists
     for co, eb in ((c, e) for c in (int(x) for x in a.coalesce.split(",")) for e in (int(x) for x in a.embed_batch.split(","))):
         emb._coalescer = _QueryCoalescer(emb, eb) if co else None
         asyncio.run(clients(ret, qs, 64, 1.0, a.k))  # warm: the graphs of the batch shapes this mode makes
         for C in (int(x) for x in a.clients.split(",")):
             l0 = st._batcher.launches
             f0 = emb._coalescer.forwards if co else 0
+            for key in wt:
+                wt[key] = 0
+            if a.profile:
+                import cProfile
+                import pstats
+
+                prof = cProfile.Profile()
+                prof.enable()
             lat, wall = asyncio.run(clients(ret, qs, C, a.seconds, a.k))
+            if a.profile:
+                prof.disable()
+                with open(f"{a.profile}.{C}", "w") as f:
+                    pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(30)
+            n = max(1, wt["n"])
             ms = np.asarray(lat) * 1e3
             print(json.dumps({"rows": a.rows, "coalesce": co, "embed_batch": eb if co else 1, "clients": C, "queries": len(lat),
                               "qps": round(len(lat) / wall, 1),
@@ -83,6 +114,8 @@ def main():
                               "latency_ms_p99": round(float(np.percentile(ms, 99)), 2),
                               "embed_forwards": (emb._coalescer.forwards - f0) if co else len(lat),
                               "search_launches": st._batcher.launches - l0,
+                              "worker_ms_per_forward": {k: round(1e3 * wt[k] / n, 3) for k in ("launch", "wait", "lists")},
+                              "profiled": bool(a.profile),
                               "model": "bge-large shape (random init), bf16", "path": "VectorRetriever.retrieve"}),
                   flush=True)
 

@@ -124,29 +124,6 @@ def test_concurrent_embed_query_calls_share_forwards(cpu_emb):
     np.testing.assert_allclose(run(cpu_emb.embed_query(qs[0])), want[0], rtol=0, atol=1e-5)
 
 
-def test_retriever_gates_forwards_on_the_store(cpu_emb):
-    """A VectorRetriever over the in-process embedder and a store that can report its in-flight searches makes the
-    embedder's forwards wait for them (bounded), and the vectors are unchanged."""
-    from hiprag.rag import VectorRetriever
-
-    calls = []
-
-    class Store:
-        def wait_device_idle(self, timeout):
-            calls.append(timeout)
-            return True
-
-    co = cpu_emb._coalescer
-    try:
-        VectorRetriever(Store(), cpu_emb)
-        assert co.gate is not None
-        v = run(cpu_emb.embed_query("dog"))
-        assert calls and 0 < calls[0] <= 0.1
-        np.testing.assert_allclose(v, cpu_emb.encode_queries(["dog"])[0].numpy(), rtol=0, atol=1e-5)
-    finally:
-        co.gate = None
-
-
 def test_embedder_rejects_missing_local_model():
     with pytest.raises(FileNotFoundError):
         TorchRocmEmbedder("/nonexistent/model", device="cpu")

@@ -49,7 +49,6 @@ def main():
     p.add_argument("--rows", type=int, default=10_000_000)
     p.add_argument("--clients", default="64,256")
     p.add_argument("--coalesce", default="1,0")
-    p.add_argument("--gate", default="1", help="comma list: forwards wait for the store's in-flight searches (A/B)")
     p.add_argument("--seconds", type=float, default=4.0)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--max-batch", type=int, default=64, help="store search batches (and the embedder's batch_size)")
@@ -88,11 +87,8 @@ def main():
         return out
 
     emb._query_lists = timed_lists
-    for co, eb, g in ((c, e, g) for c in (int(x) for x in a.coalesce.split(","))
-                      for e in (int(x) for x in a.embed_batch.split(",")) for g in (int(x) for x in a.gate.split(","))):
+    for co, eb in ((c, e) for c in (int(x) for x in a.coalesce.split(",")) for e in (int(x) for x in a.embed_batch.split(","))):
         emb._coalescer = _QueryCoalescer(emb, eb) if co else None
-        if co and g:
-            emb._coalescer.gate = lambda: st.wait_device_idle(0.02)
         asyncio.run(clients(ret, qs, 64, 1.0, a.k))  # warm: the graphs of the batch shapes this mode makes
         for C in (int(x) for x in a.clients.split(",")):
             l0 = st._batcher.launches
@@ -112,7 +108,7 @@ def main():
                     pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(30)
             n = max(1, wt["n"])
             ms = np.asarray(lat) * 1e3
-            print(json.dumps({"rows": a.rows, "coalesce": co, "embed_batch": eb if co else 1, "gate": bool(co and g), "clients": C, "queries": len(lat),
+            print(json.dumps({"rows": a.rows, "coalesce": co, "embed_batch": eb if co else 1, "clients": C, "queries": len(lat),
                               "qps": round(len(lat) / wall, 1),
                               "latency_ms_p50": round(float(np.percentile(ms, 50)), 2),
                               "latency_ms_p99": round(float(np.percentile(ms, 99)), 2),

@@ -30,11 +30,6 @@ class VectorRetriever(BaseRetriever):
         self.embedder = embedder
         self.config = config or RetrieverConfig()
         self.reranker = reranker
-        # an in-process query embedder and a GPU store on the same device take turns: the embedder's forwards wait
-        # (bounded) for the store's in-flight searches (TorchRocmEmbedder._QueryCoalescer.gate)
-        co, wait = getattr(embedder, "_coalescer", None), getattr(vector_store, "wait_device_idle", None)
-        if co is not None and wait is not None and getattr(co, "gate", 0) is None:
-            co.gate = lambda: wait(0.02)
         if self.config.enable_reranking and self.reranker is None:
             # the reference builds RerankerFactory.create(backend="auto", model=config.reranker_model)
             # (base_retriever.py:36-40), an HTTP client; the MI355X replacement is the in-process

@@ -223,14 +223,6 @@ class _QueryCoalescer:
         self.forwards = 0  # diagnostics: forwards run / queries embedded through them
         self.queries = 0
         self._pool = None
-        # gate(): called in the worker before each forward; a retriever sets it to its store's wait_device_idle so
-        # a forward does not start beside a FILTER (which holds most CUs): the two then run back to back
-        self.gate = None
-
-    def _run(self, queries: list[str]):
-        if self.gate is not None:
-            self.gate()
-        return self.emb._query_lists(queries)
 
     def submit(self, query: str) -> asyncio.Future:
         loop = asyncio.get_running_loop()
@@ -254,7 +246,7 @@ class _QueryCoalescer:
                 if self._pool is None:
                     self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-embed")
                 try:
-                    vecs = await loop.run_in_executor(self._pool, self._run, [q for q, _ in batch])
+                    vecs = await loop.run_in_executor(self._pool, self.emb._query_lists, [q for q, _ in batch])
                 except Exception as exc:  # noqa: BLE001 -- this batch's callers see the failure
                     for _, f in batch:
                         if not f.done():

@@ -139,10 +139,6 @@ class _SearchBatcher:
         self.store, self.max_batch, self.depth = store, max(1, int(max_batch)), max(1, int(depth))
         self.pending: list = []
         self.running = False
-        # set while no launch of this batcher is in flight: a query embedder sharing the GPU waits for it before a
-        # forward (wait_device_idle), so forwards and FILTERs run back to back instead of splitting the CUs
-        self.idle = threading.Event()
-        self.idle.set()
         self.launches = 0         # diagnostics
         self.native_launches = 0  # ... of which through the asynchronous native entry point
         self.efd = -1             # eventfd of native completions (one count per finished batch)
@@ -244,7 +240,6 @@ class _SearchBatcher:
                         self._fail(batch, exc)
                         continue
                     inflight[aw] = (batch, prep, info)
-                    self.idle.clear()
                 batch = []
                 if not inflight:
                     continue
@@ -269,8 +264,6 @@ class _SearchBatcher:
                         if not e[4].done():
                             e[4].set_result(r if len(r) <= e[1] else r[: e[1]])
                 batch = []
-                if not inflight:
-                    self.idle.set()
         except BaseException as exc:  # never leave a waiter hanging: fail what this drain holds
             err = exc if isinstance(exc, Exception) else RuntimeError(f"search batcher stopped: {exc!r}")
             self._fail(batch, err)
@@ -279,7 +272,6 @@ class _SearchBatcher:
             raise
         finally:
             self.running = False
-            self.idle.set()
             self._release_loop()
 
 
@@ -805,11 +797,6 @@ class HipVectorStore(BaseVectorStore):
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
         return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, rec_l, meta_l, score_l, per_q, embs)
-
-    def wait_device_idle(self, timeout: float) -> bool:
-        """Block (a worker thread, never the event loop) until no search launch of this store is in flight, at most
-        `timeout` seconds; True when idle."""
-        return self._batcher.idle.wait(timeout)
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:

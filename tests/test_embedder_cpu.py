@@ -124,6 +124,19 @@ def test_concurrent_embed_query_calls_share_forwards(cpu_emb):
     np.testing.assert_allclose(run(cpu_emb.embed_query(qs[0])), want[0], rtol=0, atol=1e-5)
 
 
+def test_coalescer_survives_a_loop_that_stopped_before_its_drain(cpu_emb):
+    """A loop that ends right after queueing a query (its drain never ran) does not strand the next loop's calls."""
+    co = cpu_emb._coalescer
+
+    async def queue_and_leave():
+        co.submit("left behind")  # queued (never awaited); the loop closes before its drain finishes
+
+    run(queue_and_leave())
+    v = run(asyncio.wait_for(cpu_emb.embed_query("dog"), 30))
+    np.testing.assert_allclose(v, cpu_emb.encode_queries(["dog"])[0].numpy(), rtol=0, atol=1e-5)
+    assert not co.running and not co.pending
+
+
 def test_embedder_rejects_missing_local_model():
     with pytest.raises(FileNotFoundError):
         TorchRocmEmbedder("/nonexistent/model", device="cpu")

@@ -484,3 +484,33 @@ def test_cancelled_search_leaves_its_batch_alone(tmp_path):
     assert [(c.id, sc) for c, sc in again] == want[0]
     assert s._batcher.native_launches >= 1 and not holder["idx"].tickets
     s.close()
+
+
+@pytest.mark.parametrize("launched", [False, True])
+def test_a_closed_event_loop_does_not_strand_the_store(tmp_path, launched):
+    """asyncio.run ending with a search queued (or a native launch in flight) used to leave the batcher 'running'
+    for a loop that no longer exists, so every later search, on any loop, waited forever.  The next loop finishes
+    the dead loop's launches (blocking collects, their eventfd counts dropped) and serves normally."""
+    s, holder = make_async_store(tmp_path, max_batch=8)
+    s.add_chunks_sync(chunks("a", 60))
+    q = np.random.default_rng(14).standard_normal((2, 16)).astype(np.float32)
+    want = [[(c.id, sc) for c, sc in r] for r in s.search_batch(q, 3)]
+    holder["idx"].delay = 0.05 if launched else 0.0
+
+    async def leave():
+        s._batcher.submit(q[0], 3, None)  # queued, never awaited
+        if launched:
+            await asyncio.sleep(0.01)  # the drain has launched it natively; the loop then closes under it
+
+    run(leave())
+    # queued only: the dead loop's drain never ran ('running' for good); launched: the drain was cancelled with
+    # the native launch outstanding (its completion would resolve a future of the closed loop)
+    assert s._batcher.running if not launched else len(s._batcher._native) == 1
+
+    async def again():
+        return await asyncio.wait_for(asyncio.gather(*[s.search(query_embedding=x.tolist(), top_k=3) for x in q]), 10)
+
+    got = run(again())
+    assert [[(c.id, sc) for c, sc in r] for r in got] == want
+    assert not holder["idx"].tickets and not s._batcher._native and not s._batcher.running
+    s.close()

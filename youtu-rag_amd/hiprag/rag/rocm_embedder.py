@@ -223,13 +223,15 @@ class _QueryCoalescer:
         self.forwards = 0  # diagnostics: forwards run / queries embedded through them
         self.queries = 0
         self._pool = None
+        self._loop = None  # the loop the current drain runs on
 
     def submit(self, query: str) -> asyncio.Future:
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         self.pending.append((query, fut))
-        if not self.running:
-            self.running = True
+        # (a drain belongs to one loop: one that stopped before its drain ran must not strand this loop's queries)
+        if not self.running or self._loop is not loop:
+            self.running, self._loop = True, loop
             # drain on the next loop iteration: every task that is ready now queues its query first
             loop.call_soon(lambda: loop.create_task(self._drain()))
         return fut

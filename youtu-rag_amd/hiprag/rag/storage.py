@@ -144,6 +144,8 @@ class _SearchBatcher:
         self.efd = -1             # eventfd of native completions (one count per finished batch)
         self._native: deque = deque()  # completion futures of native launches, in submission order
         self._loop = None         # the loop the eventfd reader is registered with
+        self._drain_loop = None   # the loop the running drain belongs to
+        self._inflight: dict = {}  # the running drain's launches: awaitable -> (batch, prep, native info or None)
 
     def submit(self, q: np.ndarray, top_k: int, filters) -> asyncio.Future:
         """Queue one query; the future resolves to its (Chunk, score) list.  A plain call, not a coroutine: the
@@ -153,13 +155,33 @@ class _SearchBatcher:
         if dim is not None and q.shape[0] != dim:  # checked before queueing: a bad query fails alone
             raise ValueError(f"query dim {q.shape[0]} != collection dim {dim}")
         loop = asyncio.get_running_loop()
+        if self._drain_loop is not None and self._drain_loop is not loop and self._drain_loop.is_closed():
+            self._recover_from_closed_loop(loop)
         fut = loop.create_future()
         self.pending.append((q, int(top_k), filters, _filter_key(filters), fut))
         if not self.running:
-            self.running = True
+            self.running, self._drain_loop = True, loop
             # start draining on the next loop iteration: every task that is ready now enqueues first
             loop.call_soon(lambda: loop.create_task(self._drain()))
         return fut
+
+    def _recover_from_closed_loop(self, loop):
+        """The loop that ran the last drain has closed -- possibly under it (asyncio.run ending with searches queued
+        or in flight: the drain never ran, or was cancelled with native launches outstanding): finish those
+        native launches here (blocking collects: their slots free, results dropped -- nobody waits for them), drop
+        their completion counts from the eventfd, forget the dead loop's queries and start afresh on `loop`."""
+        for _batch, _prep, info in list(self._inflight.values()):
+            if info is not None:
+                with contextlib.suppress(Exception):
+                    self.store._collect_native(info, blocking=True)
+        self._inflight = {}
+        if self.efd >= 0:
+            with contextlib.suppress(BlockingIOError, OSError):
+                os.eventfd_read(self.efd)  # (the collects waited for every notify of those launches)
+        self._native.clear()
+        self._loop = None  # its reader went with the closed loop; native_fd registers one with `loop`
+        self.pending = [e for e in self.pending if e[4].get_loop() is loop]
+        self.running, self._drain_loop = False, None
 
     def _take(self):
         key = self.pending[0][3]
@@ -225,6 +247,7 @@ class _SearchBatcher:
     async def _drain(self):
         loop = asyncio.get_running_loop()
         inflight: dict = {}  # awaitable -> (batch, prep, native launch info or None)
+        self._inflight = inflight  # (seen by _recover_from_closed_loop if this loop closes under the drain)
         batch: list = []
         try:
             while self.pending or inflight:

@@ -176,6 +176,20 @@ int hr_merge_candidates_strided(int device, const void* cand_dev, const double* 
                                 int64_t bound_rank_stride, int G, int B, int kc, int k, float* scores_out_dev,
                                 int64_t* rows_out_dev, double* kth_out_dev, int32_t* fail_out_dev, void* stream);
 
+/* Exact top-m of every query over the whole shard (the exhaustive pass: canonical fp64 score of every live, allowed
+ * row + a stable sort), as B*m candidate records {score, local row + row_offset} on the device in (score desc, row
+ * asc) order, (-inf, -1) padding past the shard's rows.  The row-sharded search's path for k above the scan's kc and
+ * for collect windows larger than their buffer -- the single index's hr_index_search k > HR_MAX_K pass, per shard
+ * (Chroma's n_results has no cap, chroma_store.py:118-120; FAISS returns the exact top-k on ties,
+ * faiss_store.py:148-176).  One corpus pass and one n-row sort per query; synchronises `stream`. */
+int hr_index_search_shard_exact(hr_index* h, const float* q_dev, int B, int m, const uint64_t* row_mask_dev,
+                                int64_t row_offset, void* cand_out_dev, void* stream);
+/* Merge of G ranks' sorted exact lists (hr_index_search_shard_exact records, m per query; rank g's block at
+ * cand_dev + g * cand_rank_stride bytes, 0 = dense B*m*16) into the top-k (score desc, row asc; -inf / -1 padding).
+ * Any G * m (hr_merge_candidates is bounded by its LDS to G * kc <= 8192); ranks' rows must be disjoint. */
+int hr_merge_sorted(int device, const void* cand_dev, int64_t cand_rank_stride, int G, int B, int m, int k,
+                    float* scores_out_dev, int64_t* rows_out_dev, void* stream);
+
 /* IVF-flat lists search (BASELINE config 5 candidate generation): h holds
  * the rows in list order (list l = tiles [list_tiles_dev[l], list_tiles_dev[l+1]) of 32 rows, pad
  * rows dead), ids_dev the original id of every position (-1 for pads), centroids_dev the nlist

@@ -2,6 +2,7 @@
 through a REAL RCCL process group (backend "nccl", world size 1, one GPU).
 
 Usage: python tests/rccl_worker.py <port> <queries.npz> <out.npz> <rows> <dim>
+       python tests/rccl_worker.py ties <port> <rows.npz> <out.npz>   (duplicate rows, k = 10 / 100 / 200)
 
 At world size 1 the exchange is normally a local copy; ``force_collective=True`` sends the packed
 per-shard records through ``all_gather_into_tensor`` and src_rank batches through ``broadcast`` on the
@@ -74,5 +75,39 @@ def main(port: int, q_path: str, out_path: str, rows: int, dim: int) -> None:
     dist.destroy_process_group()
 
 
+def main_ties(port: int, in_path: str, out_path: str) -> None:
+    """The exact paths through real RCCL: a corpus with 2,000 copies of one row and k = 10 (pipelined kc 32; the
+    ties fail the guard and overflow the collect window -> the shard's exhaustive top rows), k = 100 (the scan at
+    kc_for_k(100) = 160) and k = 200 > HR_MAX_K (hr_index_search_shard_exact, all-gather, hr_merge_sorted)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    from hiprag import _native
+    from hiprag.dist import ShardedSearch
+
+    z = np.load(in_path)
+    x, q = z["x"], z["q"]
+    idx = _native.NativeIndex(x.shape[1], "bf16", "cosine", device=0)
+    idx.add(x)
+    ss = ShardedSearch(idx, 0, max_batch=q.shape[0], device=dev, max_k=16, force_collective=True)
+    qd = torch.from_numpy(q).to(dev)
+    out = {}
+    for k in (10, 100, 200):
+        s, r = ss.search(qd, k)
+        out[f"s{k}"], out[f"r{k}"] = s.cpu().numpy(), r.cpu().numpy()
+    torch.cuda.synchronize()
+    out.update(ag=np.array(ss.collective_calls["all_gather"]), transport=np.array(ss.transport),
+               fallback=np.array(ss.fallback_queries), exact=np.array(ss.exact_queries))
+    np.savez(out_path, **out)
+    ss.close()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main(int(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))
+    if sys.argv[1] == "ties":
+        main_ties(int(sys.argv[2]), sys.argv[3], sys.argv[4])
+    else:
+        main(int(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))

@@ -270,3 +270,145 @@ def test_rccl_comm_two_ranks_with_stub_library(tmp_path):
     s_ref, r_ref = oracle.c_search(stored, "bf16", R.process_queries(q, "cosine"), K)
     np.testing.assert_array_equal(got["r"], r_ref)
     np.testing.assert_array_equal(got["s"], s_ref.astype(np.float32))
+
+
+# ---------------------------------------------------------------- ties across the shard boundary, k beyond kc
+NT, DUP_LO, DUP_HI = 6000, 2000, 4000  # 2,000 copies of one row straddling the rank boundary at 3,000
+
+
+def _ties_stored(lo, hi):
+    """Stored (bf16, cosine-processed) rows [lo, hi) of the ties corpus: the synthetic rows with rows
+    [DUP_LO, DUP_HI) replaced by copies of row 77."""
+    import oracle
+
+    x = oracle.c_build_synthetic(5, lo, hi - lo, DIM, "bf16", "cosine", 1)
+    dup = oracle.c_build_synthetic(5, 77, 1, DIM, "bf16", "cosine", 1)[0]
+    a, b = max(lo, DUP_LO), min(hi, DUP_HI)
+    if a < b:
+        x[a - lo:b - lo] = dup
+    return x
+
+
+def _ties_queries():
+    import oracle
+    from oracle import ref_numpy as R
+
+    q = np.random.default_rng(3).standard_normal((B, DIM)).astype(np.float32)
+    dup = R.dequantize(oracle.c_build_synthetic(5, 77, 1, DIM, "bf16", "cosine", 1), "bf16")[0]
+    q[0] = dup          # its top-k is all ties (2,000 equal scores)
+    q[4] = dup + 0.01 * q[4]  # near-ties
+    return R.process_queries(q, "cosine")
+
+
+def _numpy_merge_sorted(cand_all, G, Bq, m, k):
+    """Reference semantics of k_merge_sorted: the top-k of the union of the ranks' sorted lists."""
+    c = cand_all.numpy().reshape(G, Bq, m, 2)
+    rows_all = c.view(np.int64)[..., 1]
+    s_out = np.full((Bq, k), -np.inf, np.float32)
+    r_out = np.full((Bq, k), -1, np.int64)
+    for q in range(Bq):
+        sc, rw = c[:, q, :, 0].reshape(-1), rows_all[:, q, :].reshape(-1)
+        sc, rw = sc[rw >= 0], rw[rw >= 0]
+        order = np.lexsort((rw, -sc))[:k]
+        s_out[q, :len(order)], r_out[q, :len(order)] = sc[order], rw[order]
+    return s_out, r_out
+
+
+def _ties_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+    from hiprag.dist import ShardedSearch
+
+    lo, hi = NT * rank // world, NT * (rank + 1) // world
+    stored = _ties_stored(lo, hi)
+    qn = _ties_queries()
+    stub = StubRccl(uid_bytes=bytes([9]) * 128 if rank == 0 else bytes(128))
+    seen = {"scan_kc": [], "collect": 0, "exact_m": []}
+
+    def qidx(qt):
+        return [int(np.nonzero((qn == qt[i].numpy()).all(1))[0][0]) for i in range(qt.shape[0])]
+
+    class CpuTies(ShardedSearch):
+        """Shard pieces with the kernels' contracts: the scan's bound is the k-th candidate's score (ties at
+        the boundary fail the guard), a collect window larger than its buffer returns the shard's exact top
+        rows (bound -inf), the exhaustive pass returns the sorted exact top-m."""
+
+        def _stream(self):
+            return 0
+
+        def _shard_search(self, qt, k, cand, bound, mask_ptr, q_ready=None, kc=None):
+            kc = kc or self.kc
+            seen["scan_kc"].append(kc)
+            s, r = oracle.c_search(stored, "bf16", qn[qidx(qt)], kc, row_offset=lo, nthreads=1)
+            cand.view(torch.int64)[..., 1] = torch.from_numpy(r)
+            cand[..., 0] = torch.from_numpy(s)
+            bound[:] = torch.from_numpy(np.where(r[:, -1] >= 0, s[:, -1], -np.inf))
+
+        def _shard_collect(self, qt, kth, cap, cand, bound, mask_ptr):
+            seen["collect"] += 1
+            s, r = oracle.c_search(stored, "bf16", qn[qidx(qt)], cap, row_offset=lo, nthreads=1)
+            keep = s >= kth.numpy()[:, None]
+            full = keep[:, -1]  # the window reaches past the buffer: the shard's exact top-cap instead
+            keep |= full[:, None]
+            cand.view(torch.int64)[..., 1] = torch.from_numpy(np.where(keep, r, -1))
+            cand[..., 0] = torch.from_numpy(np.where(keep, s, -np.inf))
+            bound[:] = -np.inf
+
+        def _shard_exact(self, qt, m, cand, mask_ptr):
+            seen["exact_m"].append(m)
+            s, r = oracle.c_search(stored, "bf16", qn[qidx(qt)], m, row_offset=lo, nthreads=1)
+            cand.view(torch.int64)[..., 1] = torch.from_numpy(r)
+            cand[..., 0] = torch.from_numpy(s)
+
+        def _merge(self, cand_all, bound_all, G, Bq, kc, k, s_out, r_out, kth, fail):
+            s, r, kt, f = _numpy_merge(cand_all, bound_all, G, Bq, kc, k)
+            s_out.copy_(torch.from_numpy(s))
+            r_out.copy_(torch.from_numpy(r))
+            kth.copy_(torch.from_numpy(kt))
+            fail.copy_(torch.from_numpy(f))
+
+        def _merge_sorted(self, cand_all, G, Bq, m, k, s_out, r_out):
+            s, r = _numpy_merge_sorted(cand_all.contiguous(), G, Bq, m, k)
+            s_out.copy_(torch.from_numpy(s))
+            r_out.copy_(torch.from_numpy(r))
+
+    ss = CpuTies(index=None, row_offset=lo, max_batch=B, device=torch.device("cpu"), max_k=16, rccl_lib=stub)
+    assert ss.kc == 32 and ss.rccl is not None
+    out = {}
+    for k in (10, 100, 200):
+        s, r = ss.search(torch.from_numpy(qn), k)
+        out[f"s{k}"], out[f"r{k}"] = s.numpy(), r.numpy()
+    s_b, r_b = ss.search(torch.from_numpy(qn) if rank == 1 else torch.zeros((B, DIM)), 200, src_rank=1)
+    assert torch.equal(r_b, torch.from_numpy(out["r200"]))
+    ss.close()
+    out["fallback"], out["exact"] = ss.fallback_queries, ss.exact_queries
+    out["scan_kc"], out["collect"], out["exact_m"] = np.array(seen["scan_kc"]), seen["collect"], np.array(seen["exact_m"])
+    if rank == 0:
+        np.savez(result_path, **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_ties_and_large_k_match_oracle(tmp_path):
+    """2,000 duplicate rows straddling the shard boundary and k in {10, 100, 200} -- k above
+    the pipelined kc (32) and above HR_MAX_K -- through the stub-RCCL exchange, identical to the single-index
+    oracle (ids and score bits); nothing raises."""
+    import oracle
+
+    path = str(tmp_path / "ties.npz")
+    mp.start_processes(_ties_worker, args=(2, _free_port(), path), nprocs=2, join=True, start_method="spawn")
+    got = np.load(path)
+    stored = _ties_stored(0, NT)
+    qn = _ties_queries()
+    for k in (10, 100, 200):
+        s_ref, r_ref = oracle.c_search(stored, "bf16", qn, k)
+        np.testing.assert_array_equal(got[f"r{k}"], r_ref, err_msg=f"k={k}")
+        np.testing.assert_array_equal(got[f"s{k}"], s_ref.astype(np.float32), err_msg=f"k={k}")
+    # (row 77 itself ties with its 2,000 copies and comes first)
+    assert list(got["r10"][0]) == [77] + list(range(DUP_LO, DUP_LO + 9))
+    assert list(got["r200"][0]) == [77] + list(range(DUP_LO, DUP_LO + 199))
+    # k = 10: the pipelined scan (kc 32), ties -> collect fallback; k = 100: the scan at kc_for_k(100) = 160, its
+    # fallback; k = 200 > HR_MAX_K: the exhaustive pass (twice: the plain and the broadcast batch)
+    assert list(got["scan_kc"]) == [32, 160] and int(got["collect"]) >= 2 and int(got["fallback"]) >= 2
+    assert list(got["exact_m"]) == [200, 200] and int(got["exact"]) == 2 * B

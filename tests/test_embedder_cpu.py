@@ -8,6 +8,7 @@
   batches spanning documents (oracle-backed index, host-list embedder).
 """
 import asyncio
+import os
 
 import numpy as np
 import pytest
@@ -134,142 +135,89 @@ def test_coalescer_survives_a_loop_that_stopped_before_its_drain(cpu_emb):
     run(queue_and_leave())
     v = run(asyncio.wait_for(cpu_emb.embed_query("dog"), 30))
     np.testing.assert_allclose(v, cpu_emb.encode_queries(["dog"])[0].numpy(), rtol=0, atol=1e-5)
-    assert not co.running and not co.pending
+    live = [lq for loop, lq in list(co._queues.items()) if not loop.is_closed()]
+    assert all(not lq.running and not lq.pending for lq in live)
 
 
-def test_embedder_rejects_missing_local_model():
-    with pytest.raises(FileNotFoundError):
-        TorchRocmEmbedder("/nonexistent/model", device="cpu")
+def test_coalescer_serves_two_running_loops_apart(cpu_emb):
+    """two event loops running at once in two threads each get their own queue and drain -- every
+    future is resolved on its own loop, and neither drain takes the other loop's queries."""
+    import threading
+
+    qs = [f"thread query {i} w{i % 5}" for i in range(12)]
+    want = cpu_emb.encode_queries(qs).numpy()
+    out, errs = {}, []
+    gate = threading.Barrier(2)
+
+    def worker(t):
+        async def main():
+            gate.wait(10)  # both loops are running before either queues
+            mine = qs[t::2]
+            got = await asyncio.gather(*[cpu_emb.embed_query(q) for q in mine])
+            assert not cpu_emb._coalescer.pending  # (this loop's queue)
+            return mine, got
+
+        try:
+            out[t] = asyncio.run(asyncio.wait_for(main(), 60))
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    assert not errs, errs
+    for t in range(2):
+        mine, got = out[t]
+        for q, v in zip(mine, got):
+            np.testing.assert_allclose(v, want[qs.index(q)], rtol=0, atol=1e-5)
 
 
-def test_make_chunks_matches_processor_convention():
-    doc = Document(id="report.pdf", content="", metadata={"source": "s3", "_private": 1})
-    ch = make_chunks(doc, ["a", "b"], {"kb": 7})
-    assert [c.id for c in ch] == ["report.pdf_chunk_0", "report.pdf_chunk_1"]
-    assert ch[1].metadata == {"source": "s3", "index_type": "index_content", "kb": 7} and ch[1].chunk_index == 1
-    doc2 = Document(id="d", content="", metadata={"index_type": "index_summary"})
-    assert make_chunks(doc2, ["x"])[0].metadata["index_type"] == "index_summary"
+def test_default_embedder_leaves_tunableop_alone(cpu_emb, monkeypatch):
+    """constructing an embedder does not touch the process's TunableOp state (tuned GEMMs are
+    opt-in), and even when asked, an application's own TunableOp setup (enabled already, or PYTORCH_TUNABLEOP_*
+    set) is left as it is; when it does act it never disables TunableOp, never renames its results file and writes
+    nothing on exit.  torch.cuda.tunable needs a GPU, so a recorder stands in for it here."""
+    import sys
+    import types
 
-
-class HashEmbedder:
-    """Host-list embedder: deterministic vectors per text."""
-    batch_size = 4
-
-    def __init__(self):
-        self.batches = []
-
-    async def embed_texts(self, texts):
-        self.batches.append(len(texts))
-        return [np.random.default_rng(abs(hash(t)) % 2**32).standard_normal(16).tolist() for t in texts]
-
-
-def test_ingestor_batches_across_documents_and_replaces_old_chunks(tmp_path):
-    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
-                            index_params={"dtype": "f32", "persist": False})
-    store = HipVectorStore(cfg, index_factory=lambda d: OracleIndex(d, "f32"))
-    emb = HashEmbedder()
-    ing = GpuIngestor(store, emb, chunking=ChunkingConfig(chunk_size=100, chunk_overlap=0))
-    docs = [Document(id=f"doc{i}", content=" ".join(f"word{j}" for j in range(30 * i + 2)), metadata={"n": i})
-            for i in range(6)]
-    n = run(ing.ingest(docs))
-    # every document's chunks + its summary vector (processors.py:559-561, :423-464)
-    assert n + 6 == run(store.count()) and sum(emb.batches) == n + 6 and max(emb.batches) == 4
-    assert all(b == 4 for b in emb.batches[:-1])
-    c = run(store.get_by_id("doc3_chunk_0"))
-    assert c.metadata["n"] == 3 and c.metadata["index_type"] == "index_content"
-    sm = run(store.get_by_id("doc3_summary"))
-    assert sm.content == "doc3\n" and sm.chunk_index == -1
-    assert sm.metadata == {"document_id": "doc3", "chunk_index": -1, "n": 3, "index_type": "index_summary"}
-    # re-ingesting a document replaces its chunks and its summary
-    before = run(store.count())
-    old = len(store._doc_rows["doc5"])
-    m = run(ing.chunk_and_store(Document(id="doc5", content="short text", metadata={"source": "s.pdf",
-                                                                                       "summary": "about x"})))
-    assert run(store.count()) == before - old + m + 1 and len(store._doc_rows["doc5"]) == m + 1
-    assert run(store.get_by_id("doc5_summary")).content == "s.pdf\nabout x"
-    no_sum = GpuIngestor(store, emb, summary_index=False)
-    assert run(no_sum.chunk_and_store(Document(id="doc9", content="a b c", metadata={}))) == 1
-    assert run(store.get_by_id("doc9_summary")) is None
-    # chunklevel.md documents take the hierarchical splitter (processors.py:371-379); "_" keys stay out
-    hc = ing.split(Document(id="h", content="# T\n## S\nline a\nline b", metadata={"_use_hierarchical_splitter": True,
-                                                                                   "source": "c.md"}))
-    assert [c.content for c in hc] == ["# T\n## S\n\nline a\nline b"]
-    assert hc[0].metadata == {"source": "c.md", "index_type": "index_content"} and hc[0].id == "h_chunk_0"
-
-
-def test_hash_tokenizer_native_text_kernel_matches_python():
-    """hr_hash_words (the host text kernel ASCII batches take) gives the ids of the re + zlib path:
-    every ASCII whitespace class, punctuation, digits, underscores, control bytes, truncation with
-    and without special tokens; batches with a non-ASCII text stay on the Python path."""
-    import random
-
-    from hiprag.rag import rocm_embedder as re_mod
-
-    rnd = random.Random(11)
-    alpha = "abcXYZ0189_ ,.!?;:'\"()-\t\n\x0b\x0c\r\x1c\x1d\x1e\x1f\x7f\x00@#$%^&*[]{}|\\/~`"
-    texts = ["".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 400))) for _ in range(60)] + ["", " \t "]
-    tok = HashWordTokenizer()
-    old = re_mod._NATIVE_TOK
-    try:
-        for max_length, special in ((8, True), (512, True), (None, True), (6, False)):
-            kw = dict(padding=True, truncation=max_length is not None, max_length=max_length, return_tensors="pt",
-                      add_special_tokens=special)
-            re_mod._NATIVE_TOK = True
-            assert tok._native_batch(texts, None, special) is not None
-            a = tok(texts, **kw)
-            re_mod._NATIVE_TOK = False
-            b = tok(texts, **kw)
-            assert torch.equal(a["input_ids"], b["input_ids"]) and torch.equal(a["attention_mask"], b["attention_mask"])
-        assert tok._native_batch(texts + ["naïve"], None, True) is None
-    finally:
-        re_mod._NATIVE_TOK = old
-
-
-def test_ingest_keeps_the_cyclic_gc_enabled(tmp_path):
-    """The ingest no longer switches the collector off for its duration (a global side effect
-    on every other coroutine of the serving process)."""
-    import gc
-
-    seen = []
-
-    class GcProbe(HashEmbedder):
-        async def embed_texts(self, texts):
-            seen.append(gc.isenabled())
-            return await super().embed_texts(texts)
-
-    cfg = VectorStoreConfig(backend="hip", collection_name="kb", persist_directory=str(tmp_path),
-                            index_params={"dtype": "f32", "persist": False})
-    store = HipVectorStore(cfg, index_factory=lambda d: OracleIndex(d, "f32"))
-    docs = [Document(id=f"d{i}", content="alpha beta gamma " * 20, metadata={}) for i in range(3)]
-    run(GpuIngestor(store, GcProbe(), chunking=ChunkingConfig(chunk_size=100, chunk_overlap=0)).ingest(docs))
-    assert seen and all(seen) and gc.isenabled()
-
-
-def test_pack_pad_sequence_changes_no_real_row():
-    """UnpaddedEncoder.pack(granule=64): one extra sequence of 1..64 pad tokens makes the token count a multiple of
-    64 (the shapes graph replays are captured for); every sequence attends only to itself, so the real tokens'
-    hidden states equal the unpadded pack's (fp32, CPU, SDPA per sequence), and `lengths` keeps the real ones."""
-    import numpy as np
     import torch
 
-    from hiprag.rag.encoder import UnpaddedEncoder
-    from hiprag.rag.rocm_embedder import build_random_bert
+    from hiprag.rag import rocm_embedder as E
 
-    model = build_random_bert("tiny", seed=3).eval()
-    enc = UnpaddedEncoder(model, use_varlen=False)
-    rng = np.random.default_rng(0)
-    lens = rng.integers(1, 20, 9)
-    ids = np.zeros((9, 20), np.int64)
-    mask = np.zeros((9, 20), np.int64)
-    for i, n in enumerate(lens):
-        ids[i, :n] = rng.integers(1, 30000, n)
-        mask[i, :n] = 1
-    with torch.inference_mode():
-        p0 = enc.pack(ids, mask, device="cpu")
-        p1 = enc.pack(ids, mask, device="cpu", granule=64)
-        h0, h1 = enc.forward_packed(p0), enc.forward_packed(p1)
-    n = int(lens.sum())
-    assert int(p1.cu_host[-1]) % 64 == 0 and 1 <= int(p1.cu_host[-1]) - n <= 64
-    np.testing.assert_array_equal(p1.lengths, lens)
-    np.testing.assert_array_equal(p1.cu_host[:-1], p0.cu_host)
-    torch.testing.assert_close(h1[:n], h0, rtol=1e-5, atol=1e-5)
+    calls = []
+    state = {"enabled": False}
+    fake = types.SimpleNamespace(
+        is_enabled=lambda: state["enabled"],
+        enable=lambda on=True: calls.append(("enable", on)),
+        tuning_enable=lambda on=True: calls.append(("tuning_enable", on)),
+        write_file_on_exit=lambda on: calls.append(("write_file_on_exit", on)),
+        set_filename=lambda *a: calls.append(("set_filename",) + a),
+        read_file=lambda path=None: calls.append(("read_file",)) or True)
+    monkeypatch.setitem(sys.modules, "torch.cuda.tunable", fake)
+    monkeypatch.setattr(torch.cuda, "tunable", fake, raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    for k in [k for k in os.environ if k.startswith("PYTORCH_TUNABLEOP_")]:
+        monkeypatch.delenv(k)
+    monkeypatch.delenv("HIPRAG_TUNED_GEMMS", raising=False)
+
+    # a default embedder never calls it
+    monkeypatch.setattr(E, "enable_tuned_gemms", lambda *a, **k: (_ for _ in ()).throw(AssertionError("called")))
+    emb = TorchRocmEmbedder(model=cpu_emb.model, tokenizer=cpu_emb.tokenizer, device="cpu", max_length=64)
+    assert emb.tuned_gemms is False
+    monkeypatch.undo()
+    monkeypatch.setitem(sys.modules, "torch.cuda.tunable", fake)
+    monkeypatch.setattr(torch.cuda, "tunable", fake, raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    for k in [k for k in os.environ if k.startswith("PYTORCH_TUNABLEOP_")]:
+        monkeypatch.delenv(k)
+
+    state["enabled"] = True  # the application enabled TunableOp itself
+    assert E.enable_tuned_gemms() is False and calls == []
+    state["enabled"] = False
+    monkeypatch.setenv("PYTORCH_TUNABLEOP_FILENAME", "/tmp/app_results.csv")  # ... or configured it
+    assert E.enable_tuned_gemms() is False and calls == []
+    monkeypatch.delenv("PYTORCH_TUNABLEOP_FILENAME")
+    assert E.enable_tuned_gemms() is True  # nothing configured: read the shipped results, tuning off, no exit write
+    assert calls == [("tuning_enable", False), ("write_file_on_exit", False), ("read_file",), ("enable", True)]

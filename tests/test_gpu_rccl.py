@@ -62,3 +62,34 @@ def test_rccl_world1_exchange_c3_vs_oracle(tmp_path, N):
     for i, h in enumerate([0, 1, 0, 1, 0, 1]):
         np.testing.assert_array_equal(got["r"][i], r_ref[h], err_msg=f"batch {i}")
         np.testing.assert_array_equal(got["s"][i], s_ref[h], err_msg=f"batch {i}")
+
+
+@pytest.mark.timeout(300)
+def test_rccl_world1_ties_and_large_k_vs_oracle(tmp_path):
+    """VERDICT r05 next #1 through real RCCL (world size 1, force_collective): 2,000 duplicate rows, k = 10 / 100 /
+    200 -- every exact path of ShardedSearch (collect overflow, k above the pipelined kc, k > HR_MAX_K) -- equal to
+    the oracle."""
+    from hiprag import synth
+
+    n, d, b = 300_000, 256, 16
+    x = synth.corpus_rows(23, np.arange(n), d)
+    x[150_000:152_000] = x[77]
+    q = np.random.default_rng(8).standard_normal((b, d)).astype(np.float32)
+    q[0] = x[77]
+    q[5] = x[77] + 0.02 * q[5]
+    inp, out = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
+    np.savez(inp, x=x, q=q)
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1"}
+    proc = subprocess.run([sys.executable, "-u", os.path.join(HERE, "rccl_worker.py"), "ties", str(_free_port()), inp,
+                           out], env=env, timeout=240, capture_output=True, text=True)
+    print(proc.stdout[-2000:], proc.stderr[-4000:])
+    assert proc.returncode == 0, proc.stderr[-4000:]
+    got = np.load(out)
+    assert str(got["transport"]).startswith("rccl")
+    assert int(got["fallback"]) >= 1 and int(got["exact"]) == b
+    stored = R.process_rows(x, "cosine", "bf16")
+    qn = R.process_queries(q, "cosine")
+    for k in (10, 100, 200):
+        s_ref, r_ref = oracle.c_search(stored, "bf16", qn, k)
+        np.testing.assert_array_equal(got[f"r{k}"], r_ref, err_msg=f"k={k}")
+        np.testing.assert_array_equal(got[f"s{k}"], s_ref.astype(np.float32), err_msg=f"k={k}")

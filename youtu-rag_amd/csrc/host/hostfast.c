@@ -7,7 +7,8 @@
 // chunk_index = meta.get("chunk_index", 0), metadata = a fresh copy of meta, embedding = embs[j] or None.
 // A batch's hits would be 2 tracked objects each (the Chunk and its pair tuple): walked by every gen-0 pass of the
 // cycle collector and promoted with the results held, the collector cost more than the assembly did
-// (tools/bench_store_host.py); see the untracking below.  The collector itself is never switched off.
+// (tools/bench_store_host.py); the caller may therefore ask for atomic-valued hits to be left untracked (see below,
+// off by default).  The collector itself is never switched off.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <structmember.h>
@@ -29,12 +30,13 @@ static int slot_offsets(PyTypeObject* cls, Py_ssize_t off[6]) {
     return 0;
 }
 
-// assemble(cls, rec_l, meta_l, score_l, per_q, embs) -> list of B lists of (cls instance, float)
+// assemble(cls, rec_l, meta_l, score_l, per_q, embs, untrack=0) -> list of B lists of (cls instance, float)
 static PyObject* assemble(PyObject* self, PyObject* args) {
     PyTypeObject* cls;
     PyObject *recs, *metas, *scores, *per_q, *embs;
-    if (!PyArg_ParseTuple(args, "O!O!O!O!O!O", &PyType_Type, &cls, &PyList_Type, &recs, &PyList_Type, &metas,
-                          &PyList_Type, &scores, &PyList_Type, &per_q, &embs))
+    int untrack = 0;
+    if (!PyArg_ParseTuple(args, "O!O!O!O!O!O|p", &PyType_Type, &cls, &PyList_Type, &recs, &PyList_Type, &metas,
+                          &PyList_Type, &scores, &PyList_Type, &per_q, &embs, &untrack))
         return NULL;
     if (cls->tp_dictoffset != 0) return PyErr_Format(PyExc_TypeError, "%s has a __dict__", cls->tp_name);
     Py_ssize_t off[6];
@@ -94,12 +96,13 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
             Py_INCREF(s);
             PyTuple_SET_ITEM(pair, 0, c);
             PyTuple_SET_ITEM(pair, 1, s);
-            if (!PyObject_GC_IsTracked(md) && (vals[5] == Py_None || !PyObject_IS_GC(vals[5]))) {
-                // a Chunk of strings, numbers and an untracked (atomic-valued) metadata dict references no container
-                // that can lead back to it, so the cycle collector is given none of a batch's hits to walk: as
-                // CPython does for tuples and dicts of atomic values (the pair tuple is one; the dict stays
-                // untracked until a container is stored in it).  What this gives up: a cycle a caller later
-                // builds THROUGH a returned Chunk (its own metadata holding the Chunk) is not collected.
+            if (untrack && !PyObject_GC_IsTracked(md) && (vals[5] == Py_None || !PyObject_IS_GC(vals[5]))) {
+                // (opt-in: index_params.untracked_results) a Chunk of strings, numbers and an untracked
+                // (atomic-valued) metadata dict references no container that can lead back to it, so the cycle
+                // collector is given none of a batch's hits to walk, as CPython does for tuples and dicts of atomic
+                // values.  What this gives up: a slotted instance is not re-tracked when a container is stored in
+                // it later, so a cycle a caller builds THROUGH a returned Chunk (its own metadata holding the
+                // Chunk) is never collected -- hence off by default.
                 PyObject_GC_UnTrack(c);
                 PyObject_GC_UnTrack(pair);
             }
@@ -125,7 +128,7 @@ fail:
 }
 
 static PyMethodDef kMethods[] = {
-    {"assemble", assemble, METH_VARARGS, "assemble(cls, rec_l, meta_l, score_l, per_q, embs) -> list[list[(cls, score)]]"},
+    {"assemble", assemble, METH_VARARGS, "assemble(cls, rec_l, meta_l, score_l, per_q, embs, untrack=False) -> list[list[(cls, score)]]"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_hostfast", NULL, -1, kMethods};

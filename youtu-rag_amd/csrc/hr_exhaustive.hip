@@ -112,7 +112,12 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
                     const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
                     size_t scratch_bytes, hipStream_t st, int sG, int ss) {
-    if (n <= 0 || m <= 0) return HR_E_INVALID;
+    if (m <= 0) return HR_E_INVALID;
+    if (n <= 0) {  // an empty shard: m padding records
+        hipLaunchKernelGGL(k_take, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, (const uint64_t*)nullptr,
+                           (const uint32_t*)nullptr, (int64_t)0, m, row_offset, sG, ss, out);
+        return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+    }
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     uint8_t* p = (uint8_t*)scratch;
     uint64_t* k_in = (uint64_t*)p;
@@ -134,6 +139,61 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
         return HR_E_HIP;
     hipLaunchKernelGGL(k_take, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, k_out, v_out, n, m, row_offset,
                        sG, ss, out);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
+// Merge of G ranks' sorted lists (the exhaustive pass's output: m records per query in (score desc, row asc) order,
+// padding (row < 0) at the tail; rank g's lists start at cand + g * cstride bytes, query q's at q * m records) into
+// the top-k: element i of rank g lands at position i + (elements of every other rank's list that precede it), found
+// by binary search -- the ranks' rows are disjoint, so the order is total and the positions a permutation.  No LDS
+// bound on G * m (k_merge's is 8192 candidates): the large-k merge of the row-sharded search.
+__global__ __launch_bounds__(256) void k_merge_sorted(const uint8_t* __restrict__ cand, int64_t cstride, int G, int B,
+                                                      int m, int k, float* __restrict__ s_out,
+                                                      int64_t* __restrict__ r_out) {
+    const int q = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= B || t >= (int64_t)G * m) return;
+    const int g = (int)(t / m), i = (int)(t % m);
+    if (i >= k) return;  // at least i elements of its own list precede it
+    const Cand e = ((const Cand*)(cand + g * cstride))[(int64_t)q * m + i];
+    if (e.row < 0) return;
+    const uint64_t ke = d2key(e.score);
+    int64_t pos = i;
+    for (int h = 0; h < G && pos < k; ++h) {
+        if (h == g) continue;
+        const Cand* L = (const Cand*)(cand + h * cstride) + (int64_t)q * m;
+        int lo = 0, hi = m;  // first index of L that does not precede e
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const Cand x = L[mid];
+            const uint64_t kx = d2key(x.score);
+            const bool before = x.row >= 0 && (kx > ke || (kx == ke && x.row < e.row));
+            if (before) lo = mid + 1;
+            else hi = mid;
+        }
+        pos += lo;
+    }
+    if (pos < k) {
+        s_out[(int64_t)q * k + pos] = (float)e.score;
+        r_out[(int64_t)q * k + pos] = e.row;
+    }
+}
+
+__global__ void k_pad_results(float* __restrict__ s_out, int64_t* __restrict__ r_out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    s_out[i] = -__builtin_inff();
+    r_out[i] = -1;
+}
+
+int launch_merge_sorted(const Cand* cand, int64_t cstride, int G, int B, int m, int k, float* s_out, int64_t* r_out,
+                        hipStream_t st) {
+    const int64_t nk = (int64_t)B * k;
+    hipLaunchKernelGGL(k_pad_results, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, st, s_out, r_out, nk);
+    if (hipGetLastError() != hipSuccess) return HR_E_HIP;
+    const int64_t per_q = (int64_t)G * m;
+    hipLaunchKernelGGL(k_merge_sorted, dim3((unsigned)((per_q + 255) / 256), (unsigned)B), dim3(256), 0, st,
+                       (const uint8_t*)cand, cstride, G, B, m, k, s_out, r_out);
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 

@@ -1597,13 +1597,11 @@ extern "C" int hr_index_host_us(hr_index* h, double* out) {
     return HR_OK;
 }
 
-// top-k beyond HR_MAX_K (Chroma's n_results has no cap, chroma_store.py:118-120): the exhaustive
-// exact pass per query -- canonical fp64 score of every live, allowed row + stable radix sort,
-// the same arithmetic and (score desc, row asc) order as the scan path -- into host records
-// out_host[B][m] (global rows; -inf / -1 padding).  One corpus pass and one n-row sort per query:
-// for the rare large-k call, not the batched hot path.
-int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, Cand* out_host,
-                    hipStream_t st) {
+// Exact top-m of every query over the whole shard into device records out_dev[B][m] (local row + row_offset;
+// -inf / -1 padding past the live, allowed rows): canonical fp64 score of every row + stable radix sort, the same
+// arithmetic and (score desc, row asc) order as the scan path.  One corpus pass and one n-row sort per query.
+static int index_exact_dev(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, int64_t row_offset,
+                           Cand* out_dev, hipStream_t st) {
     Scratch& sc = h->scr[kSyncSet];
     const int QB = (B + 31) / 32, Bp = QB * 32;
     HIP_TRY(sc.q32.ensure((size_t)Bp * h->dpad * 4));
@@ -1621,22 +1619,27 @@ int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_
     std::vector<double> qerr((size_t)Bp * 4);
     HIP_TRY(hipMemcpyAsync(qerr.data(), sc.qerr.p, qerr.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const int mm = (int)std::min<int64_t>(m, h->n);
-    for (int b = 0; b < B; ++b)
-        for (int i = 0; i < m; ++i) out_host[(int64_t)b * m + i] = Cand{-INFINITY, -1};
-    if (mm <= 0) return HR_OK;
-    HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
-    HIP_TRY(h->fb_cand.ensure((size_t)mm * sizeof(Cand)));
+    if (h->n > 0) HIP_TRY(h->exh.ensure(exhaustive_scratch_bytes(h->n)));
     for (int b = 0; b < B; ++b) {
         if (int rc = exhaustive_topm(h->rows, h->dtype, h->S, h->dpad, sc.q32.as<float>() + (int64_t)b * h->dpad,
-                                     h->metric, qerr[4 * (size_t)b + 2], h->live, (const uint32_t*)mask_dev, h->n, 0, mm,
-                                     h->fb_cand.as<Cand>(), h->exh.p, h->exh.bytes, st, h->stripe_G, h->stripe_s))
+                                     h->metric, qerr[4 * (size_t)b + 2], h->live, (const uint32_t*)mask_dev, h->n,
+                                     row_offset, m, out_dev + (int64_t)b * m, h->exh.p, h->exh.bytes, st, h->stripe_G,
+                                     h->stripe_s))
             return set_err(rc, "exhaustive exact pass failed");
-        HIP_TRY(hipMemcpyAsync(out_host + (int64_t)b * m, h->fb_cand.p, (size_t)mm * sizeof(Cand), hipMemcpyDeviceToHost,
-                               st));
-        HIP_TRY(hipStreamSynchronize(st));
-        h->n_exhaustive++;
+        if (h->n > 0) h->n_exhaustive++;
     }
+    return HR_OK;
+}
+
+// top-k beyond HR_MAX_K (Chroma's n_results has no cap, chroma_store.py:118-120): the exhaustive exact pass
+// (index_exact_dev) into host records out_host[B][m] (global rows; -inf / -1 padding).  For the rare large-k
+// call, not the batched hot path.
+int index_exact_all(hr_index* h, const float* q_dev, int B, int m, const uint64_t* mask_dev, Cand* out_host,
+                    hipStream_t st) {
+    HIP_TRY(h->fb_cand.ensure((size_t)B * m * sizeof(Cand)));
+    if (int rc = index_exact_dev(h, q_dev, B, m, mask_dev, 0, h->fb_cand.as<Cand>(), st)) return rc;
+    HIP_TRY(hipMemcpyAsync(out_host, h->fb_cand.p, (size_t)B * m * sizeof(Cand), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return HR_OK;
 }
 
@@ -1810,6 +1813,29 @@ extern "C" int hr_index_search_shard_collect(hr_index* h, const float* q_dev, in
             return rc;
     }
     return HR_OK;
+}
+
+extern "C" int hr_index_search_shard_exact(hr_index* h, const float* q_dev, int B, int m, const uint64_t* row_mask_dev,
+                                           int64_t row_offset, void* cand_out_dev, void* stream) {
+    if (!h || !q_dev || !cand_out_dev) return set_err(HR_E_INVALID, "null argument");
+    if (B <= 0 || m <= 0) return set_err(HR_E_INVALID, "B > 0 and m > 0 required");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->G > 1) return set_err(HR_E_UNSUPPORTED, "per-shard search pieces need a single-device index");
+    if (int rc = set_device(h)) return rc;
+    if (int rc = persist_close(h)) return rc;  // a running persistent FILTER leaves the CUs to this pass
+    return index_exact_dev(h, q_dev, B, m, row_mask_dev, row_offset, (Cand*)cand_out_dev, (hipStream_t)stream);
+}
+
+extern "C" int hr_merge_sorted(int device, const void* cand_dev, int64_t cand_rank_stride, int G, int B, int m, int k,
+                               float* scores_out_dev, int64_t* rows_out_dev, void* stream) {
+    if (!cand_dev || !scores_out_dev || !rows_out_dev) return set_err(HR_E_INVALID, "null argument");
+    if (G <= 0 || B <= 0 || B > 65535 || m <= 0 || k <= 0) return set_err(HR_E_INVALID, "bad sizes");
+    if (!cand_rank_stride) cand_rank_stride = (int64_t)B * m * (int64_t)sizeof(Cand);
+    if (cand_rank_stride < (int64_t)B * m * (int64_t)sizeof(Cand) || cand_rank_stride % 8)
+        return set_err(HR_E_INVALID, "rank stride smaller than one rank's records or misaligned");
+    HIP_TRY(hipSetDevice(device));
+    return launch_merge_sorted((const Cand*)cand_dev, cand_rank_stride, G, B, m, k, scores_out_dev, rows_out_dev,
+                               (hipStream_t)stream);
 }
 
 extern "C" int hr_merge_candidates(int device, const void* cand_dev, const double* bounds_dev, int G, int B, int kc,
@@ -2137,6 +2163,14 @@ extern "C" int hr_index_set_persist(hr_index* h, int mode) {
 // and the launch grids are sized for its CU count, so a compute-bound neighbour (the query embedder's forward) can
 // own the other CUs instead of contending for all of them.  n_words == 0 lifts the restriction.  The caller's own
 // streams (hr_index_search_device / _shard's stream arguments) are the caller's to mask (hr_stream_create_cu_mask).
+// forget every captured sync-search graph (their FILTER variant and grid sizes are baked in): a setting that changes
+// either must not keep replaying the old form
+static void drop_sync_graphs(hr_index* h) {
+    for (auto& g : h->sync_graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    h->sync_graphs.clear();
+}
+
 extern "C" int hr_index_set_cu_mask(hr_index* h, const uint32_t* mask, int n_words) {
     if (!h || n_words < 0 || n_words > 64 || (n_words > 0 && !mask)) return set_err(HR_E_INVALID, "bad CU mask");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -2161,6 +2195,7 @@ extern "C" int hr_index_set_cu_mask(hr_index* h, const uint32_t* mask, int n_wor
             (void)hipStreamDestroy(sc.scan);
             sc.scan = nullptr;
         }
+    drop_sync_graphs(h);  // (their grids were sized for the old CU count)
     h->cu_mask.assign(mask, mask + n_words);
     hipStream_t ns = nullptr;
     HIP_TRY(index_stream_create(h, &ns, false));
@@ -2316,6 +2351,10 @@ extern "C" int hr_index_wide_launches(hr_index* h, int64_t* out) {
 extern "C" int hr_index_set_q256(hr_index* h, int on) {
     if (!h) return set_err(HR_E_INVALID, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->q256 != (on != 0)) {
+        if (int rc = set_device(h)) return rc;
+        drop_sync_graphs(h);  // a captured 129-256-query search replays the FILTER variant it was captured with
+    }
     h->q256 = on != 0;
     for (hr_index* s : h->shards) s->q256 = on != 0;
     return HR_OK;

@@ -68,6 +68,9 @@ int exhaustive_topm(const uint8_t* rows, int dtype, int S, int dpad, const float
                     const uint32_t* live,
                     const uint32_t* mask, int64_t n, int64_t row_offset, int m, Cand* out, void* scratch,
                     size_t scratch_bytes, hipStream_t st, int sG = 1, int ss = 0);
+// G ranks' sorted exact top-m lists (rank stride cstride bytes) -> the top-k (score desc, row asc; -inf / -1 padding)
+int launch_merge_sorted(const Cand* cand, int64_t cstride, int G, int B, int m, int k, float* s_out, int64_t* r_out,
+                        hipStream_t st);
 size_t tile_list_scratch_bytes(int64_t n_tiles);
 int build_tile_list(const uint32_t* live, const uint32_t* mask, int64_t n_tiles, uint32_t* list, uint32_t* count,
                     void* scratch, size_t scratch_bytes, hipStream_t st);

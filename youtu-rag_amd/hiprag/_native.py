@@ -48,6 +48,7 @@ EXPORTS = [
     "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
     "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles", "hr_index_set_cu_mask",
     "hr_stream_create_cu_mask", "hr_stream_destroy", "hr_index_set_q256", "hr_index_q256_launches",
+    "hr_index_search_shard_exact", "hr_merge_sorted",
 ]
 
 _lib = None
@@ -144,6 +145,8 @@ def load_library(path: str | None = None):
             "hr_topk_records": [vp, vp, i64, i32, i32, vp, vp],
             "hr_ivf_search": [vp, vp, i32, vp, i64, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_index_search_shard_collect": [vp, vp, i32, vp, i32, vp, i64, vp, vp, vp],
+            "hr_index_search_shard_exact": [vp, vp, i32, i32, vp, i64, vp, vp],
+            "hr_merge_sorted": [i32, vp, i64, i32, i32, i32, i32, vp, vp, vp],
             "hr_merge_candidates": [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_merge_candidates_strided": [i32, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp, vp],
             "hr_pool_normalize": [vp, i32, vp, i32, i32, i32, i32, vp, vp],
@@ -393,6 +396,13 @@ class NativeIndex:
                                                       ctypes.c_void_p(cand_ptr), ctypes.c_void_p(bound_ptr),
                                                       ctypes.c_void_p(stream or None)))
 
+    def search_shard_exact(self, q_ptr: int, B: int, m: int, row_offset: int, cand_ptr: int, mask_ptr: int = 0,
+                           stream: int = 0) -> None:
+        """Exact top-m of every query over this shard (the exhaustive pass), B*m sorted records with global rows."""
+        _check(self.lib.hr_index_search_shard_exact(self._h, ctypes.c_void_p(q_ptr), int(B), int(m),
+                                                    ctypes.c_void_p(mask_ptr or None), int(row_offset),
+                                                    ctypes.c_void_p(cand_ptr), ctypes.c_void_p(stream or None)))
+
     def debug_approx(self, q: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
         """(approximate MFMA scores B×n, error bound E per query) -- diagnostics."""
         q = np.ascontiguousarray(q, np.float32)
@@ -542,6 +552,14 @@ def merge_candidates(device: int, cand_ptr: int, bounds_ptr: int, G: int, B: int
                                  int(G), int(B), int(kc), int(k), ctypes.c_void_p(scores_ptr),
                                  ctypes.c_void_p(rows_ptr), ctypes.c_void_p(kth_ptr),
                                  ctypes.c_void_p(fail_ptr), ctypes.c_void_p(stream or None)))
+
+
+def merge_sorted(device: int, cand_ptr: int, G: int, B: int, m: int, k: int, scores_ptr: int, rows_ptr: int,
+                 stream: int = 0, cand_rank_stride: int = 0) -> None:
+    """Merge G ranks' sorted exact top-m lists (search_shard_exact records) into the top-k (hr_merge_sorted)."""
+    _check(load_library().hr_merge_sorted(int(device), ctypes.c_void_p(cand_ptr), int(cand_rank_stride), int(G),
+                                          int(B), int(m), int(k), ctypes.c_void_p(scores_ptr),
+                                          ctypes.c_void_p(rows_ptr), ctypes.c_void_p(stream or None)))
 
 
 def pool_normalize(hidden_ptr: int, dtype: str, mask_ptr: int, B: int, T: int, H: int, n_instr: int, out_ptr: int,

@@ -11,7 +11,15 @@ merges the G·kc candidates on its own GPU with the same (score desc, row asc)
 order and the same guard, so all ranks hold identical results.  Queries whose
 guard fails (top-k not provably complete) are re-scanned in collect mode: every
 shard returns all rows whose approximate score could still reach the k-th exact
-score, and a second merge is exact by construction.
+score (a shard whose window overflows its buffer returns its exact top rows
+instead), and a second merge is exact by construction.
+
+Every k the single index serves is served here too (Chroma's ``n_results`` has no
+cap, /root/reference/utu/rag/storage/implementations/chroma_store.py:118-120;
+FAISS returns the exact top-k whatever the ties, faiss_store.py:148-176): a k above
+the pipelined kc runs as one synchronous batch -- the scan with kc_for_k(k) up to
+HR_MAX_K, above that every shard's exhaustive exact top-k (hr_index_search_shard_exact),
+all-gathered and merged by rank (hr_merge_sorted).
 
 Batches are pipelined at two levels.  On the GPU, each batch's scan runs on the caller's
 stream over all but a few CUs, while the previous batch's select/rescore, all-gather and
@@ -36,6 +44,15 @@ def fallback_cap(G: int) -> int:
     """Rows per query and shard the collect fallback may return: 1024, bounded so the merge of
     G shards' records fits the merge kernel's LDS (G * cap <= 8192)."""
     return max(64, min(1024, 8192 // max(1, G)))
+
+
+class _Done:
+    """Ticket of a batch answered inside submit (k above the pipelined kc): finalize returns its outputs."""
+
+    __slots__ = ("result",)
+
+    def __init__(self, s_out, r_out):
+        self.result = (s_out, r_out)
 
 
 def _record_len(B: int, kc: int) -> int:
@@ -179,6 +196,7 @@ class ShardedSearch:
             raise ValueError("force_collective needs an initialised process group")
         self.collective = self.G > 1 or bool(force_collective)  # the exchange goes through the process group
         self.fallback_queries = 0  # queries whose guard failed (collect fallback), cumulative
+        self.exact_queries = 0  # queries answered by the shards' exhaustive exact pass (large k), cumulative
         self.collective_calls = {"all_gather": 0, "broadcast": 0}  # exchanges through the process group's ranks
         self.wait_s = 0.0  # host time blocked on guard flags in finalize (the rest of a submit is host work)
         # candidates per shard per query: kc_for_k(max_k) keeps the guard's margin for every k <= max_k
@@ -220,12 +238,28 @@ class ShardedSearch:
                                  s_out.data_ptr(), r_out.data_ptr(), kth.data_ptr(), fail.data_ptr(), self._stream(),
                                  cand_rank_stride=cand_all.stride(0) * 8, bound_rank_stride=bound_all.stride(0) * 8)
 
-    def _shard_search(self, q, k, cand, bound, mask_ptr, q_ready=None):
+    def _shard_search(self, q, k, cand, bound, mask_ptr, q_ready=None, kc=None):
+        """This shard's exact top-kc candidates and bound.  kc None: the pipelined batch (self.kc, scan + tail
+        streams); else a synchronous scan with that kc on the current stream (k above the pipelined kc)."""
+        if kc is not None:
+            self.index.search_shard(q.data_ptr(), q.shape[0], k, kc, self.row_offset, cand.data_ptr(),
+                                    bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream())
+            return
         tail = self.tail.cuda_stream if self.tail is not None else None
         ev = q_ready.cuda_event if (q_ready is not None and tail is not None) else 0
         self.index.search_shard(q.data_ptr(), q.shape[0], k, self.kc, self.row_offset, cand.data_ptr(),
                                 bound.data_ptr(), mask_ptr=mask_ptr, stream=self._stream(), tail_stream=tail,
                                 q_ready_event=ev)
+
+    def _shard_exact(self, q, m, cand, mask_ptr):
+        """This shard's exact top-m of every query (exhaustive pass): cand (B, m, 2) float64 records, sorted."""
+        self.index.search_shard_exact(q.data_ptr(), q.shape[0], m, self.row_offset, cand.data_ptr(),
+                                      mask_ptr=mask_ptr, stream=self._stream())
+
+    def _merge_sorted(self, cand_all, G, B, m, k, s_out, r_out):
+        # cand_all (G, B, m, 2): every rank's sorted exact lists, rank stride = stride(0)
+        _native.merge_sorted(self.device.index or 0, cand_all.data_ptr(), G, B, m, k, s_out.data_ptr(),
+                             r_out.data_ptr(), self._stream(), cand_rank_stride=cand_all.stride(0) * 8)
 
     def _shard_collect(self, q, kth, cap, cand, bound, mask_ptr):
         self.index.search_shard_collect(q.data_ptr(), q.shape[0], kth.data_ptr(), cap, self.row_offset,
@@ -289,10 +323,13 @@ class ShardedSearch:
         be ready in the current stream's order."""
         torch = self.torch
         B = int(q.shape[0])
+        k = int(k)
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
-        if not 1 <= k <= self.kc:
-            raise ValueError(f"k must be in [1, {self.kc}]")
+        if k < 1:
+            raise ValueError("k must be >= 1")
+        if k > self.kc:
+            return self._submit_beyond_kc(q, k, s_out, r_out, mask_ptr, src_rank)
         slot = self.slots[self._next]
         self._next = (self._next + 1) % len(self.slots)
         if slot.ticket is not None:
@@ -338,6 +375,8 @@ class ShardedSearch:
 
     def finalize(self, slot) -> tuple:
         """Wait for a submitted batch's guard flags (only those) and run its fallback if needed."""
+        if isinstance(slot, _Done):
+            return slot.result
         if slot.ticket is None:
             raise ValueError("ticket already finalized")
         q, k, s_out, r_out, mask_ptr, B = slot.ticket
@@ -381,12 +420,77 @@ class ShardedSearch:
         self.finalize_all()
         return self.finalize(self.submit(q, k, s_out, r_out, mask_ptr, src_rank=src_rank))
 
-    def _fallback(self, q, k, failed, kth, s_out, r_out, mask_ptr):
+    def _submit_beyond_kc(self, q, k, s_out, r_out, mask_ptr, src_rank):
+        """A batch with k above the pipelined kc, answered synchronously (the batches in flight first, so every
+        rank issues its collectives in the same order): the scan with kc_for_k(k) while that fits the scan
+        (k <= HR_MAX_K), else every shard's exhaustive exact top-k.  Returns a finished ticket."""
         torch = self.torch
+        self.finalize_all()
+        q = q.contiguous()
+        if src_rank is not None and self.collective:
+            qb = torch.empty_like(q)
+            qb.copy_(q)
+            self._broadcast(qb, src_rank)
+            q = qb
+        B = int(q.shape[0])
+        s_out = s_out if s_out is not None else torch.empty((B, k), dtype=torch.float32, device=self.device)
+        r_out = r_out if r_out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
+        kc2 = _native.kc_for_k(k, int(getattr(self.index, "dim", 0) or 0))
+        if k <= _native.HR_MAX_K and k <= kc2 <= _native.HR_MAX_KC and self.G * kc2 <= 8192:
+            f64 = dict(dtype=torch.float64, device=self.device)
+            L = _record_len(B, kc2)
+            rec = torch.empty((L,), **f64)
+            cand, bound = _record_views(rec, B, kc2)
+            self._shard_search(q, k, cand, bound, mask_ptr, kc=kc2)
+            rec_all = torch.empty((self.G, L), **f64) if self.collective else rec.view(1, L)
+            if self.collective:
+                self._all_gather(rec_all, rec)
+            cand_all, bound_all = _record_views(rec_all, B, kc2)
+            kth = torch.empty((B,), **f64)
+            fail = torch.empty((B,), dtype=torch.int32, device=self.device)
+            self._merge(cand_all, bound_all, self.G, B, kc2, k, s_out, r_out, kth, fail)
+            failed = np.nonzero(fail.cpu().numpy())[0]
+            if len(failed):
+                self.fallback_queries += len(failed)
+                self._fallback(q, k, failed, kth, s_out, r_out, mask_ptr)
+        else:
+            self._exact(q, k, np.arange(B), s_out, r_out, mask_ptr)
+        return _Done(s_out, r_out)
+
+    def _exact(self, q, k, which, s_out, r_out, mask_ptr):
+        """Queries `which` of the batch answered by every shard's exhaustive exact top-k: one all-gather of the
+        sorted lists, then the rank merge (complete by construction: a row no shard returned has k rows of its
+        own shard ahead of it)."""
+        torch = self.torch
+        idx = torch.as_tensor(np.asarray(which, np.int64), device=self.device)
+        qf = q[idx].contiguous()
+        Bf = len(which)
+        rec = torch.empty((Bf, k, 2), dtype=torch.float64, device=self.device)
+        self._shard_exact(qf, k, rec, mask_ptr)
+        if self.collective:
+            rec_all = torch.empty((self.G, Bf, k, 2), dtype=torch.float64, device=self.device)
+            self._all_gather(rec_all, rec)
+        else:
+            rec_all = rec.unsqueeze(0)
+        s2 = torch.empty((Bf, k), dtype=torch.float32, device=self.device)
+        r2 = torch.empty((Bf, k), dtype=torch.int64, device=self.device)
+        self._merge_sorted(rec_all, self.G, Bf, k, k, s2, r2)
+        s_out[idx] = s2
+        r_out[idx] = r2
+        self.exact_queries += Bf
+
+    def _fallback(self, q, k, failed, kth, s_out, r_out, mask_ptr):
+        """Collect re-scan of the queries whose guard failed.  Each shard's window is complete (a window larger
+        than the buffer returns that shard's exact top-cap rows), so with k <= cap the merge is exact; k above
+        the cap goes to the exhaustive pass."""
+        torch = self.torch
+        Bf, cap = len(failed), fallback_cap(self.G)
+        if k > cap:
+            self._exact(q, k, failed, s_out, r_out, mask_ptr)
+            return
         idx = torch.as_tensor(failed, device=self.device)
         qf = q[idx].contiguous()
         kf = kth[idx].contiguous()
-        Bf, cap = len(failed), fallback_cap(self.G)
         L = _record_len(Bf, cap)
         rec = torch.empty((L,), dtype=torch.float64, device=self.device)
         cand, bound = _record_views(rec, Bf, cap)
@@ -399,7 +503,8 @@ class ShardedSearch:
         kth2 = torch.empty((Bf,), dtype=torch.float64, device=self.device)
         fail2 = torch.empty((Bf,), dtype=torch.int32, device=self.device)
         self._merge(cand_all, bound_all, self.G, Bf, cap, k, s2, r2, kth2, fail2)
-        if int(fail2.sum().item()):
-            raise RuntimeError("exact fallback overflowed its candidate buffer (massive ties?)")
         s_out[idx] = s2
         r_out[idx] = r2
+        still = np.nonzero(fail2.cpu().numpy())[0]
+        if len(still):  # (a shard reported an incomplete window: the exhaustive pass settles it; same on every rank)
+            self._exact(q, k, np.asarray(failed)[still], s_out, r_out, mask_ptr)

@@ -272,7 +272,10 @@ class GraphedForward:
                     self.enc.forward_packed(spk)
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            # thread-local capture: the query coalescer captures on its worker thread while the event loop's thread
+            # keeps making HIP calls for the store's searches; under the global mode those calls would
+            # invalidate the capture or fail themselves
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                 out = self.enc.forward_packed(spk)
         finally:
             self.enc.observers = obs

@@ -188,23 +188,36 @@ TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableo
 
 
 def enable_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
-    """Load TunableOp GEMM results (read-only: tuning stays off, and the process's own results file is a private temp
-    path, so nothing rewrites the shipped one).  Returns whether the results were accepted (their validators --
-    torch, HIP, hipBLASLt, rocBLAS versions and the GPU arch -- must match this process)."""
-    import tempfile
-
+    """Use the TunableOp GEMM results shipped for gfx950 (opt-in: TorchRocmEmbedder(tuned_gemms=True)).  TunableOp is
+    process-wide state, so this leaves an application's own setup alone: if TunableOp is already enabled, or any
+    PYTORCH_TUNABLEOP_* variable is set, nothing is changed and False is returned.  Otherwise the results are read
+    (their validators -- torch, HIP, hipBLASLt, rocBLAS versions and the GPU arch -- must match this process),
+    tuning stays off, nothing is written on exit (the shipped file is never rewritten, no temp file is left), and
+    TunableOp is enabled only if the results were accepted.  Returns whether they were."""
     import torch
 
     if not (os.path.exists(path) and torch.cuda.is_available()):
         return False
     import torch.cuda.tunable as tun
 
+    if tun.is_enabled() or any(k.startswith("PYTORCH_TUNABLEOP_") for k in os.environ):
+        return False
     tun.tuning_enable(False)
-    tun.set_filename(os.path.join(tempfile.gettempdir(), f"hiprag_tunableop_{os.getpid()}.csv"))
+    tun.write_file_on_exit(False)
     ok = bool(tun.read_file(path))
-    tun.enable(ok)
+    if ok:
+        tun.enable(True)
     return ok
 
+
+class _LoopQueue:
+    """One event loop's waiting queries and whether its drain task is running."""
+
+    __slots__ = ("pending", "running", "__weakref__")
+
+    def __init__(self):
+        self.pending: list = []
+        self.running = False
 
 
 class _QueryCoalescer:
@@ -214,41 +227,68 @@ class _QueryCoalescer:
     cancellation cancels only its query); a drain task takes up to ``max_batch`` waiting queries per forward and
     runs it in one worker thread (the GPU wait and the host list conversion off the loop), one batch at a time
     while the next one gathers.  Each vector is the one ``encode_queries`` gives for that query (rows are
-    independent through the encoder; a different batch size can only change GEMM rounding)."""
+    independent through the encoder; a different batch size can only change GEMM rounding).
+
+    Every event loop has its own queue and drain (asyncio futures are not thread-safe: a drain only ever resolves
+    its own loop's futures, on that loop); the loops share the one worker thread, so forwards still run one at a
+    time.  A loop that is closed leaves its queue behind with it."""
 
     def __init__(self, emb, max_batch: int):
+        import weakref
+
         self.emb, self.max_batch = emb, max(1, int(max_batch))
-        self.pending: list = []
-        self.running = False
+        self._queues: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # loop -> _LoopQueue
+        self._qlock = threading.Lock()
         self.forwards = 0  # diagnostics: forwards run / queries embedded through them
         self.queries = 0
         self._pool = None
-        self._loop = None  # the loop the current drain runs on
+        self._pool_lock = threading.Lock()
+
+    def _queue(self, loop) -> _LoopQueue:
+        with self._qlock:
+            lq = self._queues.get(loop)
+            if lq is None:
+                lq = self._queues[loop] = _LoopQueue()
+            return lq
+
+    @property
+    def pending(self) -> list:
+        """The waiting queries of the calling thread's running loop (diagnostics / tests)."""
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            return []
+        lq = self._queues.get(loop)
+        return lq.pending if lq is not None else []
 
     def submit(self, query: str) -> asyncio.Future:
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        self.pending.append((query, fut))
-        # (a drain belongs to one loop: one that stopped before its drain ran must not strand this loop's queries)
-        if not self.running or self._loop is not loop:
-            self.running, self._loop = True, loop
+        lq = self._queue(loop)
+        lq.pending.append((query, fut))
+        if not lq.running:
+            lq.running = True
             # drain on the next loop iteration: every task that is ready now queues its query first
-            loop.call_soon(lambda: loop.create_task(self._drain()))
+            loop.call_soon(lambda: loop.create_task(self._drain(lq)))
         return fut
 
-    async def _drain(self):
+    def _executor(self):
+        with self._pool_lock:
+            if self._pool is None:
+                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-embed")
+            return self._pool
+
+    async def _drain(self, lq: _LoopQueue):
         loop = asyncio.get_running_loop()
         batch: list = []
         try:
-            while self.pending:
-                batch, self.pending = self.pending[: self.max_batch], self.pending[self.max_batch:]
+            while lq.pending:
+                batch, lq.pending = lq.pending[: self.max_batch], lq.pending[self.max_batch:]
                 batch = [e for e in batch if not e[1].done()]  # (cancelled while waiting)
                 if not batch:
                     continue
-                if self._pool is None:
-                    self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-embed")
                 try:
-                    vecs = await loop.run_in_executor(self._pool, self.emb._query_lists, [q for q, _ in batch])
+                    vecs = await loop.run_in_executor(self._executor(), self.emb._query_lists, [q for q, _ in batch])
                 except Exception as exc:  # noqa: BLE001 -- this batch's callers see the failure
                     for _, f in batch:
                         if not f.done():
@@ -263,18 +303,20 @@ class _QueryCoalescer:
                 batch = []
         except BaseException as exc:  # the drain itself stopped (loop shutdown): no caller is left waiting
             err = exc if isinstance(exc, Exception) else RuntimeError(f"query embedding stopped: {exc!r}")
-            for _, f in batch + self.pending:
+            for _, f in batch + lq.pending:
                 if not f.done():
                     f.set_exception(err)
-            self.pending = []
+            lq.pending = []
             raise
         finally:
-            self.running = False
+            lq.running = False
 
     def close(self):
-        if self._pool is not None:
-            self._pool.shutdown(wait=True)
-            self._pool = None
+        with self._pool_lock:
+            if self._pool is not None:
+                self._pool.shutdown(wait=True)
+                self._pool = None
+
 
 class TorchRocmEmbedder(BaseEmbedder):
     """BaseEmbedder running the embedding model in-process on an MI355X (provider "rocm")."""
@@ -313,9 +355,11 @@ class TorchRocmEmbedder(BaseEmbedder):
         self.model = model.to(self.device, tdt).eval()
         # encoder GEMMs from the TunableOp results shipped for gfx950 (tools/embed_tune.py: every hipBLASLt / rocBLAS
         # solution of the bge shapes at each 64-token count benchmarked, the fastest kept), read-only; shapes not in
-        # the file, or a file whose library versions do not match, keep the heuristic choice
+        # the file, or a file whose library versions do not match, keep the heuristic choice.  Opt-in (TunableOp is
+        # process-wide state): tuned_gemms=True, or HIPRAG_TUNED_GEMMS=1
         if tuned_gemms is None:
-            tuned_gemms = self.device.type == "cuda" and self.dtype_name != "float32"
+            tuned_gemms = os.environ.get("HIPRAG_TUNED_GEMMS", "0") == "1"
+        tuned_gemms = bool(tuned_gemms) and self.device.type == "cuda" and self.dtype_name != "float32"
         self.tuned_gemms = enable_tuned_gemms() if tuned_gemms else False
         # K8: fused residual add + LayerNorm in every encoder layer (HIPRAG_FUSED_LN=0: PyTorch's two kernels)
         self.fused_layers = fuse_encoder_layers(self.model) if (fused_layernorm and self.device.type == "cuda") else 0

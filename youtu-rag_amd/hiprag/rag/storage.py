@@ -66,8 +66,9 @@ except ImportError:  # pragma: no cover - a source tree without the build: the P
     _hostfast = None
 
 
-def _assemble_py(C, rec_l, meta_l, score_l, per_q, embs):
-    """The per-query (Chunk, score) lists of a batch's gathered hits; _hostfast.assemble is the same in C."""
+def _assemble_py(C, rec_l, meta_l, score_l, per_q, embs, untrack=False):
+    """The per-query (Chunk, score) lists of a batch's gathered hits; _hostfast.assemble is the same in C
+    (`untrack` only applies there)."""
     out, i = [], 0
     for cnt in per_q:  # one pass: each query's hits straight into its list
         res = []
@@ -315,6 +316,9 @@ class HipVectorStore(BaseVectorStore):
         self.capacity = int(params.get("capacity", 0))
         self.include_embeddings = bool(params.get("include_embeddings", False))
         self.keep_embeddings = bool(params.get("keep_embeddings", False))
+        # returned Chunks with atomic-valued metadata left off the cycle collector (faster under heavy load; a cycle
+        # a caller later builds through such a Chunk is then never collected).  Off: ordinary tracked objects.
+        self.untracked_results = bool(params.get("untracked_results", False))
         self.persist = bool(params.get("persist", True))
         self.fsync = bool(params.get("fsync", True))
         self.journal_fraction = float(params.get("journal_fraction", 0.25))
@@ -819,7 +823,8 @@ class HipVectorStore(BaseVectorStore):
             embs = [None] * len(rec_l)
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
-        return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, rec_l, meta_l, score_l, per_q, embs)
+        return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, rec_l, meta_l, score_l, per_q, embs,
+                                                                               self.untracked_results)
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:

@@ -977,8 +977,8 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
         stored = oracle.c_build_synthetic(9, 0, n, dim, dtype, metric)
         qn = R.process_queries(q, metric)
         allowed = rng.random(n) < 0.7
-        # 129-256 queries with one row part on 16-bit rows: the 256-query FILTER (hr_q256.hip) instead
-        q256_expected = dtype != "f32" and n_parts == 1 and B > 128
+        # 129-256 queries with one row part: the 256-query FILTER (hr_q256.hip) instead
+        q256_expected = n_parts == 1 and B > 128
         for m in (None, allowed):
             mk = None if m is None else oracle.mask_from_bool(m)
             w0, x0 = idx.wide_launches(), idx.q256_launches()
@@ -1005,14 +1005,20 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
 @pytest.mark.parametrize("dim,dtype,n,B,k", [(1024, "bf16", 200_003, 256, 10), (768, "bf16", 150_001, 256, 16),
                                              (512, "f16", 100_000, 200, 10), (256, "bf16", 70_001, 129, 5),
                                              (1024, "bf16", 5_000, 256, 10), (1024, "f16", 64, 256, 3),
-                                             (768, "bf16", 1_000_003, 256, 10)])
+                                             (768, "bf16", 1_000_003, 256, 10),
+                                             # fp32 rows (the store's default dtype): f16 MFMA for cosine, bf16 for
+                                             # ip / euclidean; every depth S = 16 / 32 / 48 / 64
+                                             (1024, "f32", 100_003, 256, 10), (768, "f32", 50_001, 200, 16),
+                                             (512, "f32", 30_011, 256, 10), (256, "f32", 40_009, 129, 5),
+                                             (1024, "f32", 3_000, 256, 10), (1024, "f32", 1_000_003, 256, 10)])
 def test_q256_filter_vs_oracle(native, dim, dtype, n, B, k):
-    """129-256 queries, one row part, 16-bit rows: ONE launch of the 256-query FILTER scores every tile for four
-    64-query groups (two tiles per wave, query windows through LDS-DMA).  Fewer tiles than one round (5k and 64
-    rows: waves on zero-record V#s), padded groups (B = 129, 200), cosine / ip / euclidean, a dense mask, deleted
-    rows -- identical to the oracle and to the same batch through two 128-query FILTER launches (set_q256(False))."""
+    """129-256 queries, one row part: ONE launch of the 256-query FILTER scores every tile for four 64-query groups
+    (two tiles per wave, query windows through LDS-DMA).  Fewer tiles than one round (5k, 3k and 64 rows: waves on
+    zero-record V#s), padded groups (B = 129, 200), 16-bit and fp32 rows, cosine / ip / euclidean, a dense mask,
+    deleted rows -- identical to the oracle and to the same batch through two 128-query FILTER launches
+    (set_q256(False))."""
     rng = np.random.default_rng(dim + B + n + 1)
-    metrics = ("cosine", "ip", "euclidean") if dtype == "bf16" and n < 500_000 else ("cosine",)
+    metrics = ("cosine", "ip", "euclidean") if dtype in ("bf16", "f32") and n < 500_000 else ("cosine",)
     for metric in metrics:
         idx = native.NativeIndex(dim, dtype, metric)
         idx.add_synthetic(31, 0, n)

@@ -25,7 +25,11 @@
 //  * candidates go to k_scan's private per-(query group, wave) regions, so k_select reads them unchanged.
 // Exactness: the same invariant as the 128-query FILTER -- every row at or above a query's final threshold was
 // appended when scanned (thresholds only grow), and each group key is the score of an appended (or SAMPLE) row.
-// Scope: bf16 / f16 rows, D = 256 / 512 / 768 / 1024, one row part (k <= 16), no tile list; cosine / ip / l2.
+//  * fp32 rows (the drop-in store's default dtype, faiss_store.py:98; Chroma float32): a k-step's chunk is 2 KiB, two
+//    16-byte loads per lane, rounded to the MFMA type on use (as k_scan's XFrag<F32> and the 128-query FILTER), so
+//    the ring holds half the k-steps in the same registers -- the same 16 KiB in flight per wave -- and the query
+//    windows are still staged 8 k-steps ahead.
+// Scope: bf16 / f16 / fp32 rows, D = 256 / 512 / 768 / 1024, one row part (k <= 16), no tile list; cosine / ip / l2.
 #include "hr_internal.hpp"
 #include "hr_kernels.hpp"
 
@@ -60,13 +64,16 @@ constexpr int kQT = 256;              // threads per workgroup: 4 waves, one per
 constexpr int kWin = 2;               // k-steps per query window
 constexpr int kWQ = kWin * 8 * 64;    // u32x4 per window buffer: [k-step][block][lane]
 constexpr int kDma = kWQ / kQT;       // LDS-DMA instructions per thread per window
-// corpus ring depth in k-steps per tile: 8 (16 KiB in flight per wave; 16 measured within 1.5 % at D = 1024 and
-// its registers are worth more as the partial refresh's: a refresh that drains the ring costs 7 %), 16 at D = 256
+// corpus ring depth in 16-bit k-steps per tile: 8 (16 KiB in flight per wave; 16 measured within 1.5 % at D = 1024 and
+// its registers are worth more as the partial refresh's: a refresh that drains the ring costs 7 %), 16 at D = 256;
+// fp32 rows (LPC = 2 loads per k-step) hold half as many k-steps in the same registers
 constexpr int ring_for(int S) { return S == 16 ? 16 : 8; }
-template <int S_>
+template <int S_, int LPC>
 struct Q256Geom {
-    static constexpr int kRing = ring_for(S_);
-    static constexpr int kLook = kRing / kWin;  // windows a window is staged ahead of its first use
+    static constexpr int kRing = ring_for(S_) / LPC;
+    // windows a window is staged ahead of its first use: 8 k-steps (the 16-bit ring's reach), 8 windows at D = 256
+    // for 16-bit rows (4 for fp32: the wait's count below must fit vmcnt)
+    static constexpr int kLook = S_ == 16 ? kRing / kWin : 8 / kWin;
     // a workgroup barrier every kBar windows: with kLook + kBar buffers the DMA at window w refills the buffer of
     // window w - kBar, which every wave has left by the last barrier (kBar = 2: half the barriers; one per window at
     // D = 256, whose 16-deep ring leaves no LDS for two spare buffers)
@@ -75,7 +82,7 @@ struct Q256Geom {
     // vmcnt at a barrier window that retires this wave's DMAs of the next kBar windows (the windows read before the
     // next barrier): younger than the last of them are the ring loads of kLook - kBar windows (2 tiles x kWin
     // k-steps each) and the DMAs of kLook - kBar - 1 windows
-    static constexpr int kVmNext = (kLook - kBar) * 2 * kWin + (kLook - kBar - 1) * kDma;
+    static constexpr int kVmNext = (kLook - kBar) * 2 * kWin * LPC + (kLook - kBar - 1) * kDma;
     static_assert(kVmNext <= 63, "vmcnt field");
 };
 
@@ -178,10 +185,12 @@ __device__ __forceinline__ uint64_t q256_stamp() {  // (diagnostic builds only: 
 #define HR_STAMP(var)
 #endif
 
-template <int MT, int S_>
+template <int MT, int DT, int S_>
 __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
-    constexpr int kRing = Q256Geom<S_>::kRing, kLook = Q256Geom<S_>::kLook, kNB = Q256Geom<S_>::kNB;
-    constexpr int kVmNext = Q256Geom<S_>::kVmNext, kBar = Q256Geom<S_>::kBar;
+    constexpr int LPC = DT == F32 ? 2 : 1;  // 16-byte loads per lane per k-step chunk
+    using Geom = Q256Geom<S_, LPC>;
+    constexpr int kRing = Geom::kRing, kLook = Geom::kLook, kNB = Geom::kNB;
+    constexpr int kVmNext = Geom::kVmNext, kBar = Geom::kBar;
     static_assert(S_ % kRing == 0 && S_ % kWin == 0, "tile depth");
     __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
     __shared__ __attribute__((aligned(16))) float th_lds[256];
@@ -208,12 +217,26 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
         return wave_uniform(t < n_tiles ? t : -1);
     };
     auto rsrc = [&](int64_t t) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024)), (short)0,
-                                                 t < 0 ? 0 : S_ * 1024, 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024 * LPC)), (short)0,
+                                                 t < 0 ? 0 : S_ * 1024 * LPC, 0x00020000);
     };
     const int voff = lane * 16;
-    auto ld = [&](__amdgpu_buffer_rsrc_t r, int ks) -> u32x4 {
-        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024, HR_Q256_NT);  // nt
+    // ring slot i (k-step i of a span) holds LPC 16-byte loads: ring[i * LPC + l]
+    auto ld = [&](u32x4* ring, int i, __amdgpu_buffer_rsrc_t r, int ks) {
+#pragma unroll
+        for (int l = 0; l < LPC; ++l)
+            ring[i * LPC + l] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, ks * 1024 * LPC + l * 1024, HR_Q256_NT);
+    };
+    auto xfrag = [&](const u32x4* ring, int i) -> u32x4 {  // the MFMA B operand of ring slot i
+        if constexpr (LPC == 1) {
+            return ring[i];
+        } else {  // fp32: eight elements rounded to the MFMA type (RNE, as k_scan's XFrag<F32>)
+            typedef float f32x8 __attribute__((ext_vector_type(8)));
+            const f32x8 f = __builtin_shufflevector(__builtin_bit_cast(f32x4, ring[2 * i]),
+                                                    __builtin_bit_cast(f32x4, ring[2 * i + 1]), 0, 1, 2, 3, 4, 5, 6, 7);
+            if constexpr (MT == BF16) return __builtin_bit_cast(u32x4, __builtin_convertvector(f, bf16x8));
+            else return __builtin_bit_cast(u32x4, __builtin_convertvector(f, f16x8));
+        }
     };
     // query windows: window gw holds k-steps (gw kWin) mod S of every block; qfrag = [group 4][S][2 blocks][64][16 B]
     const __amdgpu_buffer_rsrc_t qr =
@@ -300,14 +323,14 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     refresh();
 
     // ---- prologue: the first kLook windows and the first ring of both tiles of round 0
-    u32x4 ra[kRing], rb[kRing];
+    u32x4 ra[kRing * LPC], rb[kRing * LPC];
     for (int w = 0; w < kLook; ++w) stage(w, (w * kWin) % S_);  // (window w in buffer w)
     {
         const auto r0 = rsrc(tile_of(0, 0)), r1 = rsrc(tile_of(0, 1));
 #pragma unroll
         for (int i = 0; i < kRing; ++i) {
-            ra[i] = ld(r0, i);
-            rb[i] = ld(r1, i);
+            ld(ra, i, r0, i);
+            ld(rb, i, r1, i);
         }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -409,13 +432,13 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
                     qcur = qbase(wb);
                     qnext = qbase(wb + 1 == kNB ? 0 : wb + 1);
                 }
-                const u32x4 xa = ra[i], xb = rb[i];
+                const u32x4 xa = xfrag(ra, i), xb = xfrag(rb, i);
                 if (!(HR_Q256_DIAG & 2)) {
-                    ra[i] = ld(sA, kb + i);
-                    rb[i] = ld(sB, kb + i);
+                    ld(ra, i, sA, kb + i);
+                    ld(rb, i, sB, kb + i);
                 } else {  // (timing build: the ring registers stay live without loads)
-                    ra[i] ^= xb;
-                    rb[i] ^= xa;
+                    ra[i * LPC] ^= xb;
+                    rb[i * LPC] ^= xa;
                 }
                 static_for<8>([&](auto B_) {
                     constexpr int b = decltype(B_)::value;
@@ -538,24 +561,29 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the look-ahead DMAs land before the workgroup's LDS goes)
 }
 
-template <int MT, int S_>
+template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((k_filter_q256<MT, S_>), dim3((unsigned)cus), dim3(kQT), 0, st, a);
+    hipLaunchKernelGGL((k_filter_q256<MT, DT, S_>), dim3((unsigned)cus), dim3(kQT), 0, st, a);
     return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
 }
 
 }  // namespace
 
-bool q256_filter_ok(int dtype, int S) { return dtype != F32 && (S == 16 || S == 32 || S == 48 || S == 64); }
+bool q256_filter_ok(int dtype, int S) {
+    return (dtype == BF16 || dtype == F16 || dtype == F32) && (S == 16 || S == 32 || S == 48 || S == 64);
+}
 
 int launch_filter_q256(int mt, int dtype, int S, int cus, const ScanArgs& a, hipStream_t st) {
     if (!q256_filter_ok(dtype, S)) return HR_E_UNSUPPORTED;
-#define HR_Q256_CASE(MTv, Sv) \
-    if (mt == MTv && S == Sv) return launch_t<MTv, Sv>(cus, a, st);
-    HR_Q256_CASE(BF16, 64)
+#define HR_Q256_CASE(MTv, DTv, Sv) \
+    if (mt == MTv && dtype == DTv && S == Sv) return launch_t<MTv, DTv, Sv>(cus, a, st);
+    HR_Q256_CASE(BF16, BF16, 64)
 #ifndef HR_Q256_ONE  // (register-allocation studies compile one instantiation)
-    HR_Q256_CASE(BF16, 48) HR_Q256_CASE(BF16, 32) HR_Q256_CASE(BF16, 16)
-    HR_Q256_CASE(F16, 64) HR_Q256_CASE(F16, 48) HR_Q256_CASE(F16, 32) HR_Q256_CASE(F16, 16)
+    HR_Q256_CASE(BF16, BF16, 48) HR_Q256_CASE(BF16, BF16, 32) HR_Q256_CASE(BF16, BF16, 16)
+    HR_Q256_CASE(F16, F16, 64) HR_Q256_CASE(F16, F16, 48) HR_Q256_CASE(F16, F16, 32) HR_Q256_CASE(F16, F16, 16)
+    // fp32 rows: f16 MFMA for cosine (normalised rows), bf16 for raw inner product / euclidean (mfma_type)
+    HR_Q256_CASE(F16, F32, 64) HR_Q256_CASE(F16, F32, 48) HR_Q256_CASE(F16, F32, 32) HR_Q256_CASE(F16, F32, 16)
+    HR_Q256_CASE(BF16, F32, 64) HR_Q256_CASE(BF16, F32, 48) HR_Q256_CASE(BF16, F32, 32) HR_Q256_CASE(BF16, F32, 16)
 #endif
 #undef HR_Q256_CASE
     return HR_E_UNSUPPORTED;

@@ -361,14 +361,9 @@ def embed_search_cu_split(args, searcher, emb, texts, dev, K, B, s_out, r_out) -
             torch.cuda.synchronize()
             searcher.tail = tail0
             searcher.index.set_cu_mask(None)
-            # the masked streams stay alive to process exit: torch's caching allocator keeps per-stream records of the
-            # embedder's blocks, and destroying a stream under them aborted the interpreter at exit
-            # (std::bad_variant_access)
-            _KEEP_STREAMS.extend(raw)
+            for r in raw:  # (nothing of torch's remembers them: the search copies its flags through the library)
+                _native.destroy_stream(r)
     return out
-
-
-_KEEP_STREAMS: list = []
 
 
 def isotropic_queries(B: int, D: int, seed: int = 7) -> np.ndarray:

@@ -259,7 +259,13 @@ int hr_index_persist_trace(hr_index* h, int n, double* out, int* n_out);
  * embedder streams), released with hr_stream_destroy. */
 int hr_index_set_cu_mask(hr_index* h, const uint32_t* mask, int n_words);
 int hr_stream_create_cu_mask(int device, const uint32_t* mask, int n_words, void** stream_out);
+/* Waits for the work queued on the stream, then destroys it.  Nothing may use the stream afterwards -- including a
+ * framework that remembers it: PyTorch's pinned-host allocator records every stream a non_blocking copy to or from a
+ * pinned tensor ran on, and touches those streams again when that tensor is freed, so such tensors must be freed
+ * before the stream is destroyed (hiprag's own code copies through hr_memcpy_async instead). */
 int hr_stream_destroy(void* stream);
+/* Asynchronous copy of `bytes` bytes on `stream` (direction from the pointers: unified addressing). */
+int hr_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream);
 /* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
  * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
 int hr_index_set_scan_timing(hr_index* h, int every);

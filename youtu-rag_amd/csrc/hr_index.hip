@@ -2217,7 +2217,19 @@ extern "C" int hr_stream_create_cu_mask(int device, const uint32_t* mask, int n_
 }
 
 extern "C" int hr_stream_destroy(void* stream) {
-    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    if (stream) {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // (work still queued on it finishes first)
+        HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    }
+    return HR_OK;
+}
+
+// an asynchronous copy of `bytes` on `stream` (any direction: unified addressing), ordered like a kernel on it --
+// the row-sharded search's guard-flag copy to pinned host memory without going through torch's pinned-memory
+// allocator, which would remember the stream and touch it again when the host block is freed
+extern "C" int hr_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream) {
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return set_err(HR_E_INVALID, "bad copy");
+    if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream));
     return HR_OK;
 }
 

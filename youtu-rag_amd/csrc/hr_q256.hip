@@ -52,6 +52,9 @@ namespace hr {
 #ifndef HR_Q256_STAMPS  // diagnostic build: per-wave cycle shares of the round's phases, printed
 #define HR_Q256_STAMPS 0
 #endif
+#ifndef HR_Q256_VMEXACT
+#define HR_Q256_VMEXACT 1
+#endif
 #ifndef HR_Q256_NT
 #define HR_Q256_NT 2
 #endif
@@ -64,13 +67,15 @@ constexpr int kQT = 256;              // threads per workgroup: 4 waves, one per
 constexpr int kWin = 2;               // k-steps per query window
 constexpr int kWQ = kWin * 8 * 64;    // u32x4 per window buffer: [k-step][block][lane]
 constexpr int kDma = kWQ / kQT;       // LDS-DMA instructions per thread per window
-// corpus ring depth in 16-bit k-steps per tile: 8 (16 KiB in flight per wave; 16 measured within 1.5 % at D = 1024 and
-// its registers are worth more as the partial refresh's: a refresh that drains the ring costs 7 %), 16 at D = 256;
-// fp32 rows (LPC = 2 loads per k-step) hold half as many k-steps in the same registers
-constexpr int ring_for(int S) { return S == 16 ? 16 : 8; }
+// corpus ring depth in k-steps per tile: 8 for 16-bit rows (16 KiB in flight per wave; 16 measured within 1.5 % at
+// D = 1024 and its registers are worth more as the partial refresh's: a refresh that drains the ring costs 7 %), 16
+// at D = 256.  fp32 rows: 8 k-steps too, twice the registers (128) and 32 KiB in flight per wave -- a k-step's MFMA
+// time covers twice the bytes, and 4 k-steps (16 KiB) left the pass latency-bound at 4.6 TB/s; the epilogue then
+// reads its thresholds one block at a time to stay within the VGPRs
+constexpr int ring_for(int S, int LPC) { return LPC == 2 ? 8 : (S == 16 ? 16 : 8); }
 template <int S_, int LPC>
 struct Q256Geom {
-    static constexpr int kRing = ring_for(S_) / LPC;
+    static constexpr int kRing = ring_for(S_, LPC);
     // windows a window is staged ahead of its first use: 8 k-steps (the 16-bit ring's reach), 8 windows at D = 256
     // for 16-bit rows (4 for fp32: the wait's count below must fit vmcnt)
     static constexpr int kLook = S_ == 16 ? kRing / kWin : 8 / kWin;
@@ -80,9 +85,13 @@ struct Q256Geom {
     static constexpr int kBar = S_ == 16 ? 1 : 2;
     static constexpr int kNB = kLook + kBar;  // window buffers
     // vmcnt at a barrier window that retires this wave's DMAs of the next kBar windows (the windows read before the
-    // next barrier): younger than the last of them are the ring loads of kLook - kBar windows (2 tiles x kWin
-    // k-steps each) and the DMAs of kLook - kBar - 1 windows
-    static constexpr int kVmNext = (kLook - kBar) * 2 * kWin * LPC + (kLook - kBar - 1) * kDma;
+    // next barrier).  The last of them, window w + kBar - 1, was staged at the start of window w + kBar - 1 - kLook,
+    // ahead of that window's ring loads: younger than it are the ring loads of kLook - kBar + 1 windows (2 tiles x
+    // kWin k-steps x LPC loads each) and the DMAs of kLook - kBar windows (anything else issued since -- keys,
+    // appends, maxima -- only adds younger operations).  HR_Q256_VMEXACT 0: the earlier count, one window of each
+    // fewer, which also retired ring loads a window before their use.
+    static constexpr int kVmNext = HR_Q256_VMEXACT ? (kLook - kBar + 1) * 2 * kWin * LPC + (kLook - kBar) * kDma
+                                                   : (kLook - kBar) * 2 * kWin * LPC + (kLook - kBar - 1) * kDma;
     static_assert(kVmNext <= 63, "vmcnt field");
 };
 
@@ -232,8 +241,12 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             return ring[i];
         } else {  // fp32: eight elements rounded to the MFMA type (RNE, as k_scan's XFrag<F32>)
             typedef float f32x8 __attribute__((ext_vector_type(8)));
-            const f32x8 f = __builtin_shufflevector(__builtin_bit_cast(f32x4, ring[2 * i]),
-                                                    __builtin_bit_cast(f32x4, ring[2 * i + 1]), 0, 1, 2, 3, 4, 5, 6, 7);
+            // pinned to the point of use: left to itself the scheduler converts each load right after issuing it
+            // (half the registers while in flight) and so waits for it there -- vmcnt(0) every k-step, no ring
+            u32x4 r0 = ring[2 * i], r1 = ring[2 * i + 1];
+            asm volatile("" : "+v"(r0), "+v"(r1));
+            const f32x8 f = __builtin_shufflevector(__builtin_bit_cast(f32x4, r0), __builtin_bit_cast(f32x4, r1), 0, 1, 2,
+                                                    3, 4, 5, 6, 7);
             if constexpr (MT == BF16) return __builtin_bit_cast(u32x4, __builtin_convertvector(f, bf16x8));
             else return __builtin_bit_cast(u32x4, __builtin_convertvector(f, f16x8));
         }
@@ -478,9 +491,9 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
             const int rgA = slot_row(tA < 0 ? 0 : tA, g), rgB = slot_row(tB < 0 ? 0 : tB, g);
             const bool okA = (allowA >> rgA) & 1u, okB = (allowB >> rgB) & 1u;
             const uint32_t rowA = (uint32_t)(tA * 32 + rgA), rowB = (uint32_t)(tB * 32 + rgB);
-            // thresholds four blocks at a time (one LDS round trip per four blocks; one per block at D = 256, whose
-            // 16-deep ring leaves no room for 64 more registers)
-            constexpr int kTB = S_ == 16 ? 1 : 4;
+            // thresholds four blocks at a time (one LDS round trip per four blocks; one per block at D = 256 and for
+            // fp32 rows, whose rings leave no room for 64 more registers)
+            constexpr int kTB = (S_ == 16 || LPC == 2) ? 1 : 4;
             u32x4 t4b[4 * kTB];
             static_for<8>([&](auto B_) {
                 constexpr int b = decltype(B_)::value;
@@ -577,8 +590,12 @@ int launch_filter_q256(int mt, int dtype, int S, int cus, const ScanArgs& a, hip
     if (!q256_filter_ok(dtype, S)) return HR_E_UNSUPPORTED;
 #define HR_Q256_CASE(MTv, DTv, Sv) \
     if (mt == MTv && dtype == DTv && S == Sv) return launch_t<MTv, DTv, Sv>(cus, a, st);
+#ifdef HR_Q256_ONE_F32  // (code studies of the fp32 form: that instantiation only)
+    HR_Q256_CASE(F16, F32, 64)
+#else
     HR_Q256_CASE(BF16, BF16, 64)
-#ifndef HR_Q256_ONE  // (register-allocation studies compile one instantiation)
+#endif
+#if !defined(HR_Q256_ONE) && !defined(HR_Q256_ONE_F32)  // (register-allocation studies compile one instantiation)
     HR_Q256_CASE(BF16, BF16, 48) HR_Q256_CASE(BF16, BF16, 32) HR_Q256_CASE(BF16, BF16, 16)
     HR_Q256_CASE(F16, F16, 64) HR_Q256_CASE(F16, F16, 48) HR_Q256_CASE(F16, F16, 32) HR_Q256_CASE(F16, F16, 16)
     // fp32 rows: f16 MFMA for cosine (normalised rows), bf16 for raw inner product / euclidean (mfma_type)

@@ -48,7 +48,7 @@ EXPORTS = [
     "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
     "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles", "hr_index_set_cu_mask",
     "hr_stream_create_cu_mask", "hr_stream_destroy", "hr_index_set_q256", "hr_index_q256_launches",
-    "hr_index_search_shard_exact", "hr_merge_sorted",
+    "hr_index_search_shard_exact", "hr_merge_sorted", "hr_memcpy_async",
 ]
 
 _lib = None
@@ -75,7 +75,16 @@ def create_cu_stream(device: int, cus) -> int:
 
 
 def destroy_stream(stream: int) -> None:
+    """Wait for the stream's work and destroy it (hr_stream_destroy).  Free first every pinned host tensor that a
+    non_blocking torch copy ran on this stream for: torch's pinned-memory allocator records those streams and uses
+    them again when the tensor is freed (a destroyed stream there crashed the interpreter at exit)."""
     _check(load_library().hr_stream_destroy(ctypes.c_void_p(stream)))
+
+
+def memcpy_async(dst_ptr: int, src_ptr: int, nbytes: int, stream: int = 0) -> None:
+    """Asynchronous copy on `stream` (hr_memcpy_async), outside torch's allocators' stream bookkeeping."""
+    _check(load_library().hr_memcpy_async(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), int(nbytes),
+                                          ctypes.c_void_p(stream or None)))
 
 
 class NativeError(RuntimeError):
@@ -130,6 +139,7 @@ def load_library(path: str | None = None):
             "hr_index_set_cu_mask": [vp, vp, i32],
             "hr_stream_create_cu_mask": [i32, vp, i32, pp],
             "hr_stream_destroy": [vp],
+            "hr_memcpy_async": [vp, vp, i64, vp],
             "hr_index_set_q256": [vp, i32],
             "hr_index_q256_launches": [vp, vp],
             "hr_index_size": [vp, vp, vp],

@@ -368,7 +368,10 @@ class ShardedSearch:
             self._all_gather(rec_all, rec)
         self._merge(cand_all, bound_all, self.G, B, self.kc, k, s_out, r_out, kth, fail)
         if slot.event is not None:
-            slot.fail_h[:B].copy_(fail, non_blocking=True)
+            # the flags to pinned memory by a library copy, not torch's non_blocking copy_: torch's pinned-memory
+            # allocator would record this (possibly caller-owned, e.g. CU-masked) stream and use it again when
+            # fail_h is freed, after the caller may have destroyed it
+            _native.memcpy_async(slot.fail_h.data_ptr(), fail.data_ptr(), B * 4, self._stream())
             slot.event.record(torch.cuda.current_stream(self.device))
         else:
             slot.fail_h[:B].copy_(fail)

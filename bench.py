@@ -241,7 +241,8 @@ def gpu_embed_plus_search(args, searcher, dev, D, K, B, n_batches: int = 16) -> 
     sys.path.insert(0, os.path.join(REPO, "tools"))
     from flops import EncoderFlops
 
-    emb = TorchRocmEmbedder(preset=args.cpu_embed_preset, dtype="bfloat16", batch_size=B, device=dev, seed=0)
+    emb = TorchRocmEmbedder(preset=args.cpu_embed_preset, dtype="bfloat16", batch_size=B, device=dev, seed=0,
+                            tuned_gemms=True)  # (the shipped gfx950 GEMM results: an application opt-in)
     if emb.dim != D:
         return {"skipped": f"embedder dim {emb.dim} != corpus dim {D}"}
     fl = EncoderFlops(emb.model, emb.unpadded)

@@ -65,7 +65,8 @@ def main():
 
     t0 = time.perf_counter()
     st, _ = build_store(a.rows, a.max_batch)
-    emb = TorchRocmEmbedder(preset="bge-large", dtype="bfloat16", batch_size=a.max_batch, max_length=512)
+    emb = TorchRocmEmbedder(preset="bge-large", dtype="bfloat16", batch_size=a.max_batch, max_length=512,
+                            tuned_gemms=True)
     ret = VectorRetriever(st, emb, RetrieverConfig(top_k=a.k, similarity_threshold=0.0))
     qs = queries(4096)
     emb.encode_queries(qs[:a.max_batch])  # graph capture of the common shapes

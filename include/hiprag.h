@@ -234,6 +234,19 @@ int hr_hash_words(const char* text, const int64_t* offsets, int64_t n_texts, int
 int hr_add_layernorm(const void* x_dev, const void* r_dev, const void* gamma_dev, const void* beta_dev, void* out_dev,
                      int64_t rows, int H, float eps, int dtype, void* stream);
 
+/* The query embedder's short-sequence attention (hr_attn.hip): for each sequence b (tokens [cu[b], cu[b+1]) of the
+ * packed batch, cu: B+1 int32 on the device) and head h, softmax(scale * Q K^T) V over the sequence's own tokens, from
+ * the fused QKV projection qkv_dev [N][3][nH][d] (row stride 3 nH d) into out_dev [N][nH][d]: Q K^T and P V on MFMA
+ * with fp32 accumulation, the softmax in fp32, P rounded to the input type for the P V product (as the flash
+ * kernel), the output rounded once.  BertSelfAttention (modeling_bert.py) on the real tokens, as
+ * scaled_dot_product_attention per sequence.  HR_E_UNSUPPORTED outside its scope (d != 64, max_len > 64, fp32,
+ * rows not 16-byte aligned): the caller's flash varlen kernel serves those. */
+int hr_attn_varlen(const void* qkv_dev, int dtype, const int32_t* cu_dev, int B, int nH, int d, int max_len,
+                   float scale, void* out_dev, void* stream);
+/* In place: x = 0.5 x (1 + erf(x / sqrt 2)) (BertIntermediate's "gelu", torch.nn.functional.gelu with
+ * approximate='none'; fp32 per element, rounded once), n elements of bf16 / f16. */
+int hr_gelu_erf(void* x_dev, int dtype, int64_t n, void* stream);
+
 /* The persistent FILTER (pipelined shard batches of <= 64 queries, k <= 16, no mask, early SAMPLE: the per-GPU
  * step of a row-sharded node).  One long-lived launch streams the corpus batch after batch -- no per-batch launch
  * ramp and tail; replaces the per-batch FILTER launch behind hr_index_search_shard_async_ev (same results).

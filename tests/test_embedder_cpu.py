@@ -221,3 +221,7 @@ def test_default_embedder_leaves_tunableop_alone(cpu_emb, monkeypatch):
     monkeypatch.delenv("PYTORCH_TUNABLEOP_FILENAME")
     assert E.enable_tuned_gemms() is True  # nothing configured: read the shipped results, tuning off, no exit write
     assert calls == [("tuning_enable", False), ("write_file_on_exit", False), ("read_file",), ("enable", True)]
+    calls.clear()
+    del fake.write_file_on_exit  # (torch 2.10 has no write_file_on_exit: tuning off is what keeps the file unwritten)
+    assert E.enable_tuned_gemms() is True
+    assert calls == [("tuning_enable", False), ("read_file",), ("enable", True)]

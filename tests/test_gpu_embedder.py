@@ -144,7 +144,8 @@ def test_fused_layernorm_embedder_matches_unfused(dtype, atol):
     texts = [f"passage {i}: " + " ".join(f"w{(i * 5 + j) % 89}" for j in range(3 + 9 * i)) for i in range(6)]
     fused = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=4, fused_layernorm=True)
     plain = TorchRocmEmbedder(preset="bge-base", dtype=dtype, batch_size=8, max_length=128, seed=4, fused_layernorm=False)
-    assert fused.fused_layers == 24 and plain.fused_layers == 0
+    # 24 add+LayerNorm blocks (K8), and for the half model also its 12 exact-GELU intermediate blocks (hr_gelu_erf)
+    assert fused.fused_layers == (24 if dtype == "float32" else 36) and plain.fused_layers == 0
     torch.testing.assert_close(fused.encode_passages(texts), plain.encode_passages(texts), rtol=0, atol=atol)
 
 
@@ -227,3 +228,65 @@ def test_graph_replayed_forward_matches_eager(dtype):
     n = a.graphed.replays
     torch.testing.assert_close(a.encode_queries(texts[:32]), b.encode_queries(texts[:32]), rtol=0, atol=2e-2)
     assert a.graphed.replays == n
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_short_attention_matches_sdpa(dtype):
+    """hr_attn_varlen (one workgroup per sequence and head; S^T = K Q^T and O^T = V^T P^T on MFMA, fp32 softmax, P
+    rounded to the input type as the flash kernel does) vs scaled_dot_product_attention of each sequence in fp32 on
+    the same half-precision projections: within the rounding of P and of the output (2 ulps of the output type
+    relative, plus an absolute floor).  Lengths 1..64 (a graph pack's pad sequence included), 70 sequences, 16 heads
+    of 64; a sequence longer than 64 tokens is not its shape (None: the flash kernel's)."""
+    import torch.nn.functional as F
+
+    td = getattr(torch, dtype)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    lengths = [1, 2, 7, 29, 31, 32, 33, 63, 64] + [int(x) for x in torch.randint(1, 60, (61,), generator=g)]
+    nH, d = 16, 64
+    cu_h = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    n = int(cu_h[-1])
+    qkv = (torch.randn((n, 3 * nH * d), generator=g) * 2.0).to(DEV, td)
+    cu = torch.from_numpy(cu_h.astype(np.int32)).to(DEV)
+    scale = d ** -0.5
+    out = _native.attn_varlen(qkv, cu, len(lengths), nH, d, max(lengths), scale)
+    assert out is not None and out.shape == (n, nH * d) and out.dtype == td
+    x = qkv.float().view(n, 3, nH, d)
+    ref = torch.empty((n, nH, d), dtype=torch.float32, device=DEV)
+    for s, e in zip(cu_h[:-1], cu_h[1:]):
+        qs, ks, vs = (x[s:e, i].transpose(0, 1) for i in range(3))
+        ref[s:e] = F.scaled_dot_product_attention(qs, ks, vs, scale=scale).transpose(0, 1)
+    ref = ref.reshape(n, nH * d)
+    ulp = 2.0 ** (-8 if dtype == "bfloat16" else -11)
+    err = (out.float() - ref).abs()
+    floor = ulp * float(ref.abs().max())  # (P rounded to the input type: an absolute error of order ulp * max |v|)
+    assert bool((err <= 2 * ulp * ref.abs() + floor).all()), float(err.max())
+    assert float((out == ref.to(td)).float().mean()) > 0.5
+    assert _native.attn_varlen(qkv, cu, len(lengths), nH, d, 65, scale) is None
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_gelu_erf_matches_torch(dtype):
+    """hr_gelu_erf in place vs torch.nn.functional.gelu (approximate='none') on the same half-precision tensor:
+    bf16 bit-identical (the same fp32 formula, rounded once); f16, whose 3 more bits expose last-bit differences of
+    the fp32 intermediate, within one f16 ulp and identical on >= 99.9 % of the elements; a length that is not a
+    multiple of 8 takes the tail path."""
+    td = getattr(torch, dtype)
+    g = torch.Generator(device="cpu").manual_seed(12)
+    for n in (1, 13, 4096 * 1856, 1_000_003):
+        x = (torch.randn(n, generator=g) * 3.0).to(DEV, td)
+        want = torch.nn.functional.gelu(x)
+        got = x.clone()
+        assert _native.gelu_erf_(got) is got
+        if dtype == "bfloat16":
+            assert torch.equal(got, want), (n, float((got.float() - want.float()).abs().max()))
+            continue
+        diff = (got.float() - want.float()).abs()
+        ulp = torch.where(want.float().abs() < 2.0 ** -14, torch.full_like(diff, 2.0 ** -24),
+                          2.0 ** (torch.floor(torch.log2(want.float().abs().clamp_min(2.0 ** -14))) - 10))
+        bad = diff > ulp
+        if n > 1000:
+            i = torch.nonzero(got != want)[:4, 0]
+            print("f16 gelu differs at", x[i].tolist(), "ours", got[i].tolist(), "torch", want[i].tolist(),
+                  "torch fp32", torch.nn.functional.gelu(x[i].float()).tolist())
+        assert not bool(bad.any()), float(diff.max())
+        assert float((got == want).float().mean()) >= 0.999

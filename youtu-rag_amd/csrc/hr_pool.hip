@@ -188,6 +188,14 @@ __global__ __launch_bounds__(256) void k_add_layernorm_w(const void* __restrict_
     const int lane = threadIdx.x & 63;
     float v[N][C];
     float s = 0.f;
+    // gamma / beta loaded with x and r (one memory round trip, not one after the reductions)
+    float gg[N][C], bb[N][C];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        const int col = (n * 64 + lane) * C;
+        ld_vec<DT, C>(g, col, gg[n]);
+        ld_vec<DT, C>(bta, col, bb[n]);
+    }
 #pragma unroll
     for (int n = 0; n < N; ++n) {
         const int64_t off = row * H + (int64_t)(n * 64 + lane) * C;
@@ -215,11 +223,9 @@ __global__ __launch_bounds__(256) void k_add_layernorm_w(const void* __restrict_
 #pragma unroll
     for (int n = 0; n < N; ++n) {
         const int col = (n * 64 + lane) * C;
-        float gg[C], bb[C], o_[C];
-        ld_vec<DT, C>(g, col, gg);
-        ld_vec<DT, C>(bta, col, bb);
+        float o_[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) o_[c] = (v[n][c] - mean) * rstd * gg[c] + bb[c];
+        for (int c = 0; c < C; ++c) o_[c] = (v[n][c] - mean) * rstd * gg[n][c] + bb[n][c];
         st_vec<DT, C>(y, row * H + col, o_);
     }
 }

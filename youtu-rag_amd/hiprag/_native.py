@@ -48,7 +48,7 @@ EXPORTS = [
     "hr_index_search_collect", "hr_index_search_poll", "hr_index_set_persist", "hr_index_persist_close",
     "hr_index_persist_stats", "hr_index_persist_trace", "hr_index_wave_tiles", "hr_index_set_cu_mask",
     "hr_stream_create_cu_mask", "hr_stream_destroy", "hr_index_set_q256", "hr_index_q256_launches",
-    "hr_index_search_shard_exact", "hr_merge_sorted", "hr_memcpy_async",
+    "hr_index_search_shard_exact", "hr_merge_sorted", "hr_memcpy_async", "hr_attn_varlen", "hr_gelu_erf",
 ]
 
 _lib = None
@@ -140,6 +140,8 @@ def load_library(path: str | None = None):
             "hr_stream_create_cu_mask": [i32, vp, i32, pp],
             "hr_stream_destroy": [vp],
             "hr_memcpy_async": [vp, vp, i64, vp],
+            "hr_attn_varlen": [vp, i32, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp],
+            "hr_gelu_erf": [vp, i32, i64, vp],
             "hr_index_set_q256": [vp, i32],
             "hr_index_q256_launches": [vp, vp],
             "hr_index_size": [vp, vp, vp],
@@ -602,6 +604,45 @@ def hash_words(data: bytes, offsets, first_id: int, span: int, cap: int = -1, cl
                                         ids.ctypes.data_as(ctypes.c_void_p), int(cap_ids),
                                         lengths.ctypes.data_as(ctypes.c_void_p)))
     return ids[:int(lengths.sum())], lengths
+
+
+_ATTN_DT = {"bfloat16": "bf16", "float16": "f16"}
+
+
+def attn_varlen(qkv, cu, B: int, nH: int, d: int, max_len: int, scale: float, out=None):
+    """Short-sequence attention of a packed batch (hr_attn_varlen): qkv (N, 3 nH d) bf16 / f16 device tensor, cu
+    (B + 1,) int32 device offsets -> (N, nH d).  Returns None where the kernel does not apply (d != 64, a sequence
+    longer than 64 tokens, ...): the caller runs the flash varlen kernel instead."""
+    import torch
+
+    dt = _ATTN_DT.get(str(qkv.dtype).replace("torch.", ""))
+    if dt is None or d != 64 or max_len > 64 or not qkv.is_contiguous():
+        return None
+    n = qkv.shape[0]
+    out = out if out is not None else torch.empty((n, nH * d), dtype=qkv.dtype, device=qkv.device)
+    rc = load_library().hr_attn_varlen(ctypes.c_void_p(qkv.data_ptr()), DTYPES[dt], ctypes.c_void_p(cu.data_ptr()),
+                                       int(B), int(nH), int(d), int(max_len), float(scale),
+                                       ctypes.c_void_p(out.data_ptr()),
+                                       ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream))
+    if rc == E_UNSUPPORTED:
+        return None
+    _check(rc)
+    return out
+
+
+def gelu_erf_(x):
+    """In-place exact GELU of a bf16 / f16 device tensor (hr_gelu_erf); returns x, or None if it does not apply."""
+    import torch
+
+    dt = _ATTN_DT.get(str(x.dtype).replace("torch.", ""))
+    if dt is None or not x.is_contiguous():
+        return None
+    rc = load_library().hr_gelu_erf(ctypes.c_void_p(x.data_ptr()), DTYPES[dt], x.numel(),
+                                    ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc == E_UNSUPPORTED:
+        return None
+    _check(rc)
+    return x
 
 
 def add_layernorm(x, r, weight, bias, eps: float):

@@ -27,6 +27,7 @@ from typing import Any, NamedTuple
 import numpy as np
 
 _ENV = os.environ.get("HIPRAG_UNPADDED", "1") != "0"  # A/B switch
+_SHORT = os.environ.get("HIPRAG_SHORT_ATTN", "1") != "0"  # A/B switch: hr_attn_varlen for short sequences
 
 
 def _varlen():
@@ -77,6 +78,11 @@ class UnpaddedEncoder:
         if use_varlen and va is None:
             raise RuntimeError("torch.nn.attention.varlen is not available")
         self.varlen = va if use_varlen else None
+        # batches whose sequences are all at most 64 tokens (queries; the graph-replayed query forwards) take the
+        # short-sequence attention kernel (hr_attn_varlen: one workgroup per sequence and head, S and P V on MFMA)
+        # instead of the flash kernel, whose tiles are sized for long sequences (19 us + a 5 us fill per layer at
+        # 64 queries)
+        self.short_attn = _SHORT and p.is_cuda and p.dtype in (torch.float16, torch.bfloat16)
         self.observers = []  # callables (B, T, lengths) per forward (tools/flops.py counts FLOPs with it)
 
     @staticmethod
@@ -169,13 +175,21 @@ class UnpaddedEncoder:
 
     def _layers(self, h, cu_t, cu_host, max_len, n):
         torch = self.torch
+        from .. import _native
+
+        n_seq = int(cu_t.shape[0]) - 1
         for w, b, nH, d, scale, attn_out, inter, out in self.layers:
-            qkv = torch.nn.functional.linear(h, w, b).view(n, 3, nH, d)
-            q, k, v = qkv.unbind(1)  # strided views: the flash kernel takes them as they are (no copies)
-            if self._varlen_layer(scale, d):
-                a = self.varlen(q, k, v, cu_t, cu_t, max_len, max_len)
-            else:
-                a = _sdpa_per_sequence(q, k, v, cu_host, max_len, scale)
+            qkv2 = torch.nn.functional.linear(h, w, b)
+            a = None
+            if self.short_attn and max_len <= 64 and self._varlen_layer(scale, d):
+                a = _native.attn_varlen(qkv2, cu_t, n_seq, nH, d, max_len, scale)  # None: not its shape
+            if a is None:
+                qkv = qkv2.view(n, 3, nH, d)
+                q, k, v = qkv.unbind(1)  # strided views: the flash kernel takes them as they are (no copies)
+                if self._varlen_layer(scale, d):
+                    a = self.varlen(q, k, v, cu_t, cu_t, max_len, max_len)
+                else:
+                    a = _sdpa_per_sequence(q, k, v, cu_host, max_len, scale)
             h = attn_out(a.reshape(n, nH * d), h)
             h = out(inter(h), h)
         return h

@@ -154,17 +154,36 @@ def _fused_output_forward(self, hidden_states, input_tensor):
     return _native.add_layernorm(self.dense(hidden_states), input_tensor, ln.weight, ln.bias, ln.eps)
 
 
+def _fused_intermediate_forward(self, hidden_states):
+    """BertIntermediate (and the XLM-R twin) with the exact GELU applied in place by hr_gelu_erf on the dense
+    output (the bias is already in the GEMM's epilogue); torch's kernel where it does not apply."""
+    h = self.dense(hidden_states)
+    if _native.gelu_erf_(h) is None:
+        h = self.intermediate_act_fn(h)
+    return h
+
+
 def fuse_encoder_layers(model) -> int:
     """Route every encoder layer's dense -> dropout -> LayerNorm(x + residual) block of a BERT /
-    XLM-R model (modeling_bert.py BertSelfOutput / BertOutput) through K8.  Eval-mode models only.
-    Returns the number of blocks patched."""
+    XLM-R model (modeling_bert.py BertSelfOutput / BertOutput) through K8, and, for half-precision models whose
+    activation is the exact GELU (hidden_act "gelu"), the intermediate block's GELU through hr_gelu_erf.  Eval-mode
+    models only.  Returns the number of blocks patched."""
     import types
 
+    import torch
+
     n = 0
+    p = next(model.parameters(), None)
+    half = p is not None and p.dtype in (torch.float16, torch.bfloat16)
+    exact_gelu = getattr(getattr(model, "config", None), "hidden_act", None) == "gelu"
     for m in model.modules():
         if type(m).__name__.endswith(("SelfOutput", "Output")) and hasattr(m, "dense") and hasattr(m, "LayerNorm") \
                 and getattr(m.LayerNorm, "elementwise_affine", True):
             m.forward = types.MethodType(_fused_output_forward, m)
+            n += 1
+        elif half and exact_gelu and type(m).__name__.endswith("Intermediate") and hasattr(m, "dense") \
+                and hasattr(m, "intermediate_act_fn") and type(m.intermediate_act_fn).__name__ == "GELUActivation":
+            m.forward = types.MethodType(_fused_intermediate_forward, m)
             n += 1
     return n
 
@@ -202,8 +221,9 @@ def enable_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
 
     if tun.is_enabled() or any(k.startswith("PYTORCH_TUNABLEOP_") for k in os.environ):
         return False
-    tun.tuning_enable(False)
-    tun.write_file_on_exit(False)
+    tun.tuning_enable(False)  # (TunableOp writes its results file at exit only while tuning is enabled)
+    if hasattr(tun, "write_file_on_exit"):  # (newer torch: say so explicitly)
+        tun.write_file_on_exit(False)
     ok = bool(tun.read_file(path))
     if ok:
         tun.enable(True)

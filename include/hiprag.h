@@ -36,6 +36,7 @@
  * return after synchronising it.  Scores follow the
  * reference's similarity convention (cosine/dot: inner product; euclidean: 1 - |q - x|^2).  Result order:
  * score descending, then row ascending; unfilled slots hold score -inf, row -1.
+ * Diagnostic / measurement entry points (kernel counters, scan timing, stamps) are in include/hiprag_diag.h.
  */
 #ifndef HIPRAG_H
 #define HIPRAG_H
@@ -121,9 +122,6 @@ int hr_index_search_collect(hr_index* h, int64_t ticket, float* scores_out, int6
  * queries need the exact fallback (collect then runs a corpus pass: call it off the event loop).  HR_E_BUSY
  * while another call holds the handle. */
 int hr_index_search_poll(hr_index* h, int64_t ticket, int* state_out);
-/* Diagnostics of the pipelined search: out[0] = caller host time per submit (us), out[1] = host time
- * per batch of the busiest shard thread (us), out[2] = batches submitted. */
-int hr_index_host_us(hr_index* h, double* out);
 int hr_index_size(hr_index* h, int64_t* n_out, int64_t* n_live_out);
 /* Shape of a handle (e.g. one returned by hr_index_load): dim, storage dtype, metric, devices. */
 int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* metric_out, int* n_dev_out);
@@ -252,18 +250,10 @@ int hr_gelu_erf(void* x_dev, int dtype, int64_t n, void* stream);
  * ramp and tail; replaces the per-batch FILTER launch behind hr_index_search_shard_async_ev (same results).
  * set_persist: 0 off, 1 shards of 4.2M-5.1M rows (default: where it measured faster than per-batch launches),
  * 2 every shard size.  persist_close: no further batch
- * for now (the running instance exits once through its batches instead of after its 300 us idle timeout).
- * persist_stats: out[0] = batches served, out[1] = error word (a bounded wait gave up; 0 = none), out[2] =
- * instances that ran.  persist_trace: per epoch of the last n (oldest first), 5 device stamps in us relative to the
- * first one's post -- post, first / last workgroup start, first / last workgroup arrival (blocking). */
-/* Diagnostics: tiles each wave of the most recent k_scan FILTER launch scanned ([query group][wave], blocking;
- * up to cap counts, the number in n_out).  Every unit is scanned exactly once per group, so the counts sum to
- * groups x units -- the invariant of the round-robin dealing, its rotation and the dynamic tail. */
-int hr_index_wave_tiles(hr_index* h, uint32_t* out, int cap, int* n_out);
+ * for now (the running instance exits once through its batches instead of after its 300 us idle timeout).  (Its
+ * counters and stamps: hr_index_persist_stats / _trace, include/hiprag_diag.h.) */
 int hr_index_set_persist(hr_index* h, int mode);
 int hr_index_persist_close(hr_index* h);
-int hr_index_persist_stats(hr_index* h, int64_t out[3]);
-int hr_index_persist_trace(hr_index* h, int n, double* out, int* n_out);
 /* CU partitioning (no reference counterpart: the reference's embedder and store are separate services, here the
  * query embedder's forward and the scan share one GPU -- base_retriever.py:57-63 embed_query -> search).
  * set_cu_mask: this index's internal streams run on the CUs of `mask` only (bit i of word j = CU 32 j + i;
@@ -279,38 +269,16 @@ int hr_stream_create_cu_mask(int device, const uint32_t* mask, int n_words, void
 int hr_stream_destroy(void* stream);
 /* Asynchronous copy of `bytes` bytes on `stream` (direction from the pointers: unified addressing). */
 int hr_memcpy_async(void* dst, const void* src, int64_t bytes, void* stream);
-/* Scan timing is off by default (each recorded event leaves a ~6 us bubble on the stream);
- * set_scan_timing(h, N) records HIP events around every N-th main pass (0 = off). */
-int hr_index_set_scan_timing(hr_index* h, int every);
-/* Timing of the main-pass scans (ms, HIP events recorded on the search stream).
- * take_scan_times harvests, in launch order, every (SAMPLE, FILTER) pair launched since the
- * previous harvest (blocking on the pending events; up to cap entries; count in n_out);
- * last_scan_ms harvests everything and reports the most recent pair.  A batch of the persistent FILTER reports
- * as its FILTER time the period between its last workgroup arrival and the previous batch's (device clock). */
-int hr_index_take_scan_times(hr_index* h, float* sample_ms, float* filter_ms, int cap, int* n_out);
-int hr_index_last_scan_ms(hr_index* h, float* sample_ms, float* filter_ms);
 int hr_device_count(int* n_out);
-/* Diagnostics: approximate MFMA scores of every row (B <= 64; approx_out B×n) and the
- * per-query error bound E_q that the exactness guard uses (e_out, B). */
-int hr_index_debug_approx(hr_index* h, const float* q, int B, float* approx_out, double* e_out);
-/* Diagnostics: candidates appended by the most recent FILTER scan (sum, max per query). */
-int hr_index_last_candidates(hr_index* h, int64_t* total, int64_t* max_per_query);
-/* Diagnostics: cumulative counters since creation -- out[0] main scan passes, out[1] queries that
+/* Cumulative counters since creation (the store's metrics) -- out[0] main scan passes, out[1] queries that
  * failed the exactness guard (collect fallback), out[2] queries answered by the exhaustive pass. */
 int hr_index_stats(hr_index* h, int64_t out[3]);
-/* Diagnostics: hr_index_search calls answered by replaying a captured HIP graph (an unmasked,
- * untimed search with k <= HR_MAX_K, from the second call of a (B, k) shape on; HIPRAG_SYNC_GRAPH=0
- * turns the graphs off).  The results are those of the normal path: the graph is that path, captured. */
-int hr_index_graph_replays(hr_index* h, int64_t* out);
-/* Diagnostics: 128-query FILTER launches issued so far (65..256-query chunks at D = 256..1024; graph replays
- * not counted) -- tests use it to check which FILTER served a batch. */
-int hr_index_wide_launches(hr_index* h, int64_t* out);
-/* The 256-query FILTER (hr_q256.hip: 129-256-query batches, bf16 / f16 rows, D = 256..1024, k <= 16, no tile
- * list -- one corpus pass for four 64-query groups, VectorRetriever.batch_retrieve / the store's micro-batches of up
- * to 256 single-query calls, base_retriever.py:96-98, chroma_store.py:118-120).  set_q256(h, 0) sends those batches
- * to two 128-query FILTER launches instead (A/B); q256_launches counts its launches (graph replays not counted). */
+/* The 256-query FILTER (hr_q256.hip: 129-256-query batches, bf16 / f16 / fp32 rows, D = 256..1024, k <= 16, no
+ * tile list -- one corpus pass for four 64-query groups, VectorRetriever.batch_retrieve / the store's micro-batches of
+ * up to 256 single-query calls, base_retriever.py:96-98, chroma_store.py:118-120).  set_q256(h, 0) sends those
+ * batches to two 128-query FILTER launches instead (A/B; hr_index_q256_launches in include/hiprag_diag.h counts
+ * its launches). */
 int hr_index_set_q256(hr_index* h, int on);
-int hr_index_q256_launches(hr_index* h, int64_t* out);
 const char* hr_last_error(void);
 int hr_abi_version(void);
 

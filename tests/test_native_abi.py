@@ -1,5 +1,5 @@
-"""CPU: libhiprag.so loads and exports every entry point include/hiprag.h declares
-(no compute call is made without a GPU)."""
+"""CPU: libhiprag.so loads and exports every entry point include/hiprag.h (the drop-in boundary) and
+include/hiprag_diag.h (diagnostics) declare (no compute call is made without a GPU)."""
 import os
 import re
 import subprocess
@@ -9,16 +9,25 @@ import pytest
 from conftest import REPO
 
 HEADER = os.path.join(REPO, "include", "hiprag.h")
+DIAG_HEADER = os.path.join(REPO, "include", "hiprag_diag.h")
+
+
+def _decls(path):
+    return set(re.findall(r"^\s*(?:int|void|const char\*)\s+(hr_\w+)\s*\(", open(path).read(), re.M))
 
 
 def declared_symbols():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(hr_\w+)\s*\(", text, re.M)))
+    return sorted(_decls(HEADER) | _decls(DIAG_HEADER))
 
 
 def test_header_declares_the_abi():
     syms = declared_symbols()
     assert "hr_index_search" in syms and "hr_merge_candidates" in syms and len(syms) >= 20
+    # the boundary header holds no diagnostics, and no symbol is declared twice
+    boundary, diag = _decls(HEADER), _decls(DIAG_HEADER)
+    assert not boundary & diag
+    assert {"hr_index_debug_approx", "hr_index_last_candidates", "hr_index_set_scan_timing", "hr_index_wave_tiles",
+            "hr_index_persist_trace"} <= diag
 
 
 def test_library_exports_every_declared_symbol():

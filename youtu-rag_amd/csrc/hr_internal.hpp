@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/hiprag.h"
+#include "../../include/hiprag_diag.h"
 #include "hr_common.hpp"
 
 using namespace hr;

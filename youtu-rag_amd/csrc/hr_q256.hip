@@ -49,6 +49,9 @@ namespace hr {
 #ifndef HR_Q256_ADJ
 #define HR_Q256_ADJ 1
 #endif
+#ifndef HR_Q256_CLOCK  // diagnostic build: the in-kernel clock (shader cycles / 100 MHz ticks around the round loop)
+#define HR_Q256_CLOCK 0
+#endif
 #ifndef HR_Q256_STAMPS  // diagnostic build: per-wave cycle shares of the round's phases, printed
 #define HR_Q256_STAMPS 0
 #endif
@@ -402,6 +405,11 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     uint64_t c_loop = 0, c_wait = 0, c_epi = 0, c_ref = 0;
     uint32_t c_blocks = 0, c_regs = 0;  // passing tile-blocks and walked registers
 #endif
+#if HR_Q256_CLOCK
+    // (MI355X_MICROARCH.md "DVFS give-back" item 6: clock = d(s_memtime) / d(s_memrealtime) x 100 MHz; the values go
+    // to printf only, never to an output)
+    const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int64_t u = 0; u < rounds; ++u) {
         HR_STAMP(s_r0);
         if (u >= 2 && !(HR_Q256_DIAG & 32)) part_load((int)(u % kParts));
@@ -562,6 +570,14 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
         c_ref += s_r3 - s_r2;
 #endif
     }
+#if HR_Q256_CLOCK
+    {
+        const uint64_t clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && wv == 0 && (blockIdx.x % 64) == 0)
+            printf("q256clock blk %d cycles %lu ticks %lu\n", (int)blockIdx.x, (unsigned long)(clk_t1 - clk_t0),
+                   (unsigned long)(clk_r1 - clk_r0));
+    }
+#endif
     if constexpr ((HR_Q256_DIAG & 8) != 0) mycnt[0] += dsink;
 #if HR_Q256_STAMPS
     if (lane == 0 && (blockIdx.x % 32) == 0)

@@ -225,3 +225,43 @@ def test_default_embedder_leaves_tunableop_alone(cpu_emb, monkeypatch):
     del fake.write_file_on_exit  # (torch 2.10 has no write_file_on_exit: tuning off is what keeps the file unwritten)
     assert E.enable_tuned_gemms() is True
     assert calls == [("tuning_enable", False), ("read_file",), ("enable", True)]
+
+
+def test_fused_retrieve_matches_two_step_path(cpu_emb, tmp_path):
+    """VectorRetriever over hiprag's embedder and store fuses concurrent retrieve() calls into cohorts (one forward
+    whose output goes straight into one store search, retriever._FusedRetrieve): same chunks, ranks and scores as
+    the reference's two awaits (embed_query, then store.search) for the same queries, per-call top_k and
+    thresholds respected, filtered calls and a reranker keep the two-step path."""
+    from hiprag.rag import RetrieverConfig, VectorRetriever
+    from hiprag.rag.base import Chunk
+
+    store = HipVectorStore(VectorStoreConfig(backend="hip", collection_name="fused", persist_directory=str(tmp_path),
+                                             index_params={"dtype": "f32", "persist": False}),
+                           index_factory=lambda d: OracleIndex(d, "f32"))
+    docs = [f"document {i} about w{i % 13} and w{(i * 7) % 31} with details {i * 3}" for i in range(120)]
+    vecs = cpu_emb.encode_passages(docs).numpy()
+    store.add_chunks_sync([Chunk(id=f"c{i}", document_id=f"d{i // 10}", content=docs[i], chunk_index=i % 10,
+                                 metadata={"grp": f"g{i % 2}"}, embedding=vecs[i].tolist()) for i in range(120)])
+    cfg = RetrieverConfig(top_k=5, similarity_threshold=0.0)
+    ret = VectorRetriever(store, cpu_emb, cfg)
+    two = VectorRetriever(store, cpu_emb, cfg)
+    two._fused = None
+    assert ret._fused is not None
+    qs = [(f"what about w{i % 13} and details {i}", 3 + i % 5) for i in range(11)]
+
+    async def fused():
+        return await asyncio.gather(*[ret.retrieve(q, top_k=k) for q, k in qs],
+                                    ret.retrieve(qs[0][0], top_k=4, filters={"grp": "g1"}))
+
+    got = run(fused())
+    assert ret._fused.queries == len(qs) and ret._fused.cohorts < len(qs)  # the filtered call took the two-step path
+    for (q, k), res in zip(qs, got):
+        want = run(two.retrieve(q, top_k=k))
+        assert [r.chunk.id for r in res] == [r.chunk.id for r in want] and [r.rank for r in res] == list(range(1, k + 1))
+        np.testing.assert_allclose([r.score for r in res], [r.score for r in want], rtol=0, atol=1e-5)
+    want_f = run(two.retrieve(qs[0][0], top_k=4, filters={"grp": "g1"}))
+    assert [r.chunk.id for r in got[-1]] == [r.chunk.id for r in want_f]
+    assert all(r.chunk.metadata["grp"] == "g1" for r in got[-1])
+    high = run(ret.retrieve(qs[1][0], top_k=5, similarity_threshold=0.99))  # threshold filtering after the ranks
+    assert all(r.score >= 0.99 for r in high)
+    ret._fused.close()

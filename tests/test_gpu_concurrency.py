@@ -71,3 +71,39 @@ def test_cu_masked_streams_destroyed_then_clean_exit():
     print(proc.stdout[-2000:], proc.stderr[-3000:])
     assert proc.returncode == 0, (proc.returncode, proc.stderr[-3000:])
     assert "destroyed" in proc.stdout and "exiting" in proc.stdout
+
+
+@pytest.mark.timeout(300)
+def test_fused_retrieve_on_gpu_matches_two_step(tmp_path):
+    """The retriever's fused cohorts on the GPU (one bf16 forward whose (B, dim) output feeds hr_index_search_device
+    directly) vs the reference's two awaits (embed_query lists -> store.search) over the same store: the same top-k
+    wherever the two forwards' roundings do not reorder a near tie, scores within the bf16 forward's rounding."""
+    from hiprag.rag import HipVectorStore, RetrieverConfig, VectorRetriever, VectorStoreConfig
+    from hiprag.rag.base import Chunk
+    from hiprag.rag.rocm_embedder import TorchRocmEmbedder
+
+    emb = TorchRocmEmbedder(preset="tiny", dtype="bfloat16", batch_size=32, max_length=128, seed=5)
+    docs = [f"passage {i} on subject w{i % 41} with w{(i * 11) % 97} and w{(i * 5) % 13}" for i in range(3000)]
+    vecs = emb.encode_passages(docs).cpu().numpy()
+    cfg = VectorStoreConfig(backend="hip", collection_name="fused", persist_directory=str(tmp_path),
+                            index_params={"dtype": "f32", "persist": False, "max_batch": 32})
+    store = HipVectorStore(cfg)
+    store.add_chunks_sync([Chunk(id=f"c{i}", document_id=f"d{i // 30}", content=docs[i], chunk_index=i % 30,
+                                 metadata={}, embedding=vecs[i].tolist()) for i in range(len(docs))])
+    rc = RetrieverConfig(top_k=8, similarity_threshold=0.0)
+    ret, two = VectorRetriever(store, emb, rc), VectorRetriever(store, emb, rc)
+    two._fused = None
+    assert ret._fused is not None
+    qs = [f"what is said on subject w{i % 41} and w{(i * 3) % 97}" for i in range(100)]
+
+    async def many(r):
+        return await asyncio.gather(*[r.retrieve(q) for q in qs])
+
+    got, want = asyncio.run(many(ret)), asyncio.run(many(two))
+    assert ret._fused.cohorts >= 4 and ret._fused.queries == len(qs)
+    same = sum([x.chunk.id for x in g] == [x.chunk.id for x in w] for g, w in zip(got, want))
+    assert same >= 0.9 * len(qs), same
+    for g, w in zip(got, want):
+        assert len(g) == 8 and abs(g[0].score - w[0].score) < 2e-2
+    store.close()
+    ret._fused.close()

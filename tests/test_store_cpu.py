@@ -397,10 +397,10 @@ def test_native_async_fallback_collected_off_loop(tmp_path):
     out = run(main())
     assert [[(c.id, sc) for c, sc in r] for r in out] == want
     # 4 batches; a submit that finds the store lock held by the fallback's worker-thread collect takes the worker
-    # path itself (never waits on the loop), so at least batch 1 and one more are native
-    assert s._batcher.launches == 4 and s._batcher.native_launches >= 2 and not idx.tickets
+    # path itself (never waits on the loop) -- how many do depends on the timing (a loaded host: all three), so
+    # only batch 1 is certain to be native
+    assert s._batcher.launches == 4 and s._batcher.native_launches >= 1 and not idx.tickets
     assert where[1] != where["loop"]                                   # the fallback batch: never on the loop
-    assert any(where[t] == where["loop"] for t in (2, 3, 4))           # (others may find the lock held by it)
     s.close()
 
 

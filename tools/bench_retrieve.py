@@ -2,9 +2,11 @@
 """The reference's query path under concurrent callers: C client coroutines each call
 ``VectorRetriever.retrieve(query)`` in a loop (base_retriever.py:53-59: embed_query, then store.search with
 ``query_embedding=``), against a HipVectorStore of N synthetic rows and the in-process bge-large-shaped embedder
-(random init, bf16).  One JSON line per (coalesce, clients): throughput, latency, forwards and launches.
-``--coalesce 0`` is the per-call forward (one query per forward, on the event loop).
-Usage: python tools/bench_retrieve.py [--rows 10000000 --clients 64,256 --coalesce 1,0 --seconds 4]"""
+(random init, bf16).  One JSON line per (mode, clients): throughput, latency, forwards and launches.  Modes: ``fused`` -- the retriever's
+cohorts (one forward whose output goes straight into one device-query store search, retriever._FusedRetrieve);
+``coalesce`` -- the reference's two awaits with the embedder's query coalescer and the store's micro-batcher;
+``percall`` -- one forward per call on the event loop.
+Usage: python tools/bench_retrieve.py [--rows 10000000 --clients 64,256 --modes fused,coalesce --seconds 4]"""
 from __future__ import annotations
 
 import argparse
@@ -48,7 +50,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rows", type=int, default=10_000_000)
     p.add_argument("--clients", default="64,256")
-    p.add_argument("--coalesce", default="1,0")
+    p.add_argument("--modes", default="fused,coalesce")
     p.add_argument("--seconds", type=float, default=4.0)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--max-batch", type=int, default=64, help="store search batches (and the embedder's batch_size)")
@@ -88,12 +90,18 @@ def main():
         return out
 
     emb._query_lists = timed_lists
-    for co, eb in ((c, e) for c in (int(x) for x in a.coalesce.split(",")) for e in (int(x) for x in a.embed_batch.split(","))):
-        emb._coalescer = _QueryCoalescer(emb, eb) if co else None
+    fused = ret._fused
+    for mode, eb in ((m, e) for m in a.modes.split(",") for e in (int(x) for x in a.embed_batch.split(","))):
+        co = mode != "percall"
+        ret._fused = fused if mode == "fused" else None
+        if fused is not None:
+            fused.max_batch = eb
+        emb._coalescer = _QueryCoalescer(emb, eb) if mode == "coalesce" else None
         asyncio.run(clients(ret, qs, 64, 1.0, a.k))  # warm: the graphs of the batch shapes this mode makes
         for C in (int(x) for x in a.clients.split(",")):
             l0 = st._batcher.launches
-            f0 = emb._coalescer.forwards if co else 0
+            f0 = emb._coalescer.forwards if emb._coalescer else 0
+            c0 = fused.cohorts if fused is not None else 0
             for key in wt:
                 wt[key] = 0
             if a.profile:
@@ -105,17 +113,19 @@ def main():
             lat, wall = asyncio.run(clients(ret, qs, C, a.seconds, a.k))
             if a.profile:
                 prof.disable()
-                with open(f"{a.profile}.{C}", "w") as f:
+                with open(f"{a.profile}.{mode}.{C}", "w") as f:
                     pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(30)
             n = max(1, wt["n"])
             ms = np.asarray(lat) * 1e3
-            print(json.dumps({"rows": a.rows, "coalesce": co, "embed_batch": eb if co else 1, "clients": C, "queries": len(lat),
-                              "qps": round(len(lat) / wall, 1),
+            fw = (fused.cohorts - c0) if mode == "fused" else (emb._coalescer.forwards - f0) if co else len(lat)
+            print(json.dumps({"rows": a.rows, "mode": mode, "embed_batch": eb if co else 1, "clients": C,
+                              "queries": len(lat), "qps": round(len(lat) / wall, 1),
                               "latency_ms_p50": round(float(np.percentile(ms, 50)), 2),
                               "latency_ms_p99": round(float(np.percentile(ms, 99)), 2),
-                              "embed_forwards": (emb._coalescer.forwards - f0) if co else len(lat),
-                              "search_launches": st._batcher.launches - l0,
-                              "worker_ms_per_forward": {k: round(1e3 * wt[k] / n, 3) for k in ("launch", "wait", "lists")},
+                              "embed_forwards": fw,
+                              "search_launches": (st._batcher.launches - l0) if mode != "fused" else fw,
+                              "worker_ms_per_forward": {k: round(1e3 * wt[k] / n, 3) for k in ("launch", "wait", "lists")}
+                              if mode == "coalesce" else None,
                               "profiled": bool(a.profile),
                               "model": "bge-large shape (random init), bf16", "path": "VectorRetriever.retrieve"}),
                   flush=True)

@@ -15,12 +15,113 @@ producing the same per-query results.
 """
 from __future__ import annotations
 
+import asyncio
 import logging
+import os
+import threading
+import weakref
+from concurrent.futures import ThreadPoolExecutor
 
 from .base import BaseEmbedder, BaseReranker, BaseRetriever, BaseVectorStore, RetrievalResult
 from .config import RetrieverConfig
 
 logger = logging.getLogger(__name__)
+
+
+class _Cohort:
+    """One event loop's waiting retrieve calls and whether its drain is running."""
+
+    __slots__ = ("pending", "running", "__weakref__")
+
+    def __init__(self):
+        self.pending: list = []
+        self.running = False
+
+
+class _FusedRetrieve:
+    """Concurrent ``retrieve`` calls (base_retriever.py:53-63: embed_query, then store.search) as cohorts of up to
+    ``max_batch`` queries, each cohort ONE embedder forward whose (B, dim) output stays on the GPU and goes straight
+    into ONE store search (HipVectorStore.search_device_sync) -- no per-query vector lists through the host, no
+    second batching stage, and the cohort's forward and FILTER run back to back on one stream instead of
+    interleaving with other cohorts' work.  A worker thread runs the forward + search; the Chunk objects are built
+    on the caller's loop.  Results are those of the two-step path for the same vectors (the same store search;
+    embed_query returns this forward's rows as lists).  Each event loop has its own queue and drain (futures are
+    resolved only on their own loop); the loops share the one worker."""
+
+    def __init__(self, retriever: "VectorRetriever", max_batch: int):
+        self.r, self.max_batch = retriever, max(1, int(max_batch))
+        self._queues: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+        self._qlock = threading.Lock()
+        self._pool = None
+        self._pool_lock = threading.Lock()
+        self.cohorts = 0  # diagnostics: cohorts run / queries through them
+        self.queries = 0
+
+    def submit(self, query: str, top_k: int, threshold: float) -> asyncio.Future:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        with self._qlock:
+            c = self._queues.get(loop)
+            if c is None:
+                c = self._queues[loop] = _Cohort()
+        c.pending.append((query, int(top_k), float(threshold), fut))
+        if not c.running:
+            c.running = True
+            loop.call_soon(lambda: loop.create_task(self._drain(c)))
+        return fut
+
+    def _executor(self):
+        with self._pool_lock:
+            if self._pool is None:
+                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-retrieve")
+            return self._pool
+
+    def _run(self, texts: list[str], k: int):
+        """Worker thread: the cohort's forward and its search (device queries), the host records back."""
+        # (the embedder's forwards take its lock themselves: graph inputs are shared with its other callers)
+        q = self.r.embedder.encode_queries(texts)
+        return self.r.vector_store.search_device_sync(q, k)
+
+    async def _drain(self, c: _Cohort):
+        loop = asyncio.get_running_loop()
+        batch: list = []
+        try:
+            while c.pending:
+                batch, c.pending = c.pending[: self.max_batch], c.pending[self.max_batch:]
+                batch = [e for e in batch if not e[3].done()]
+                if not batch:
+                    continue
+                k = max(e[1] for e in batch)
+                try:
+                    ran = await loop.run_in_executor(self._executor(), self._run, [e[0] for e in batch], k)
+                    hits = self.r.vector_store._assemble(([None] * len(batch), k, None), ran)
+                except Exception as exc:  # noqa: BLE001 -- this cohort's callers see the failure
+                    for e in batch:
+                        if not e[3].done():
+                            e[3].set_exception(exc)
+                    batch = []
+                    continue
+                self.cohorts += 1
+                self.queries += len(batch)
+                for (_, kq, th, f), h in zip(batch, hits):
+                    if not f.done():
+                        f.set_result(self.r._to_results(h[:kq], th))
+                batch = []
+        except BaseException as exc:  # the drain itself stopped (loop shutdown): no caller is left waiting
+            err = exc if isinstance(exc, Exception) else RuntimeError(f"retrieval stopped: {exc!r}")
+            for e in batch + c.pending:
+                if not e[3].done():
+                    e[3].set_exception(err)
+            c.pending = []
+            raise
+        finally:
+            c.running = False
+
+    def close(self):
+        with self._pool_lock:
+            if self._pool is not None:
+                self._pool.shutdown(wait=True)
+                self._pool = None
 
 
 class VectorRetriever(BaseRetriever):
@@ -37,6 +138,16 @@ class VectorRetriever(BaseRetriever):
             from .rerankers import RerankerFactory
 
             self.reranker = RerankerFactory.create(backend="rocm", model_name_or_path=self.config.reranker_model)
+        # the fused path (one forward + one device-query search per cohort of concurrent calls) where both halves are
+        # hiprag's: the in-process embedder and the HIP store; anything else keeps the reference's two awaits
+        self._fused = _FusedRetrieve(self, getattr(embedder, "batch_size", 64)) if self._fusable() else None
+
+    def _fusable(self) -> bool:
+        if os.environ.get("HIPRAG_FUSED_RETRIEVE", "1") == "0":  # (A/B switch: the reference's two awaits)
+            return False
+        return (self.reranker is None and callable(getattr(self.vector_store, "search_device_sync", None))
+                and callable(getattr(self.embedder, "encode_queries", None))
+                and hasattr(self.embedder, "_fwd_lock") and getattr(self.embedder, "fused_retrieve", True))
 
     def _to_results(self, hits, threshold: float) -> list[RetrievalResult]:
         out = []
@@ -53,6 +164,8 @@ class VectorRetriever(BaseRetriever):
     async def retrieve(self, query: str, top_k: int | None = None, **kwargs) -> list[RetrievalResult]:
         top_k = top_k or self.config.top_k
         threshold = kwargs.get("similarity_threshold", self.config.similarity_threshold)
+        if self._fused is not None and not kwargs.get("filters") and self.reranker is None:
+            return await self._fused.submit(query, top_k, threshold)
         qv = await self.embedder.embed_query(query)
         hits = await self.vector_store.search(query_embedding=qv, top_k=top_k * 2 if self.reranker else top_k,
                                               filters=kwargs.get("filters"))

@@ -745,6 +745,36 @@ class HipVectorStore(BaseVectorStore):
             # search takes its exhaustive exact path (same results, one corpus pass per query)
             return self._index.search(q, min(top_k, n_live), self.filter_bitmap(filters)), tables
 
+    def search_device_sync(self, q, top_k: int):
+        """(raw, tables) of an unfiltered search of the queries in `q`, a (B, dim) float32 torch tensor that may live
+        on the GPU (the in-process embedder's output): the native search reads it in place and only the B * k results
+        come back to the host -- no query vectors through host memory (the fused retrieve, retriever.py).  Pass the
+        result with prep = (q, top_k, None) to _assemble.  An index without a device entry point (tests) gets a host
+        copy."""
+        import torch
+
+        if q.dim() != 2 or (self.dim is not None and q.shape[1] != self.dim):
+            raise ValueError(f"queries must be (B, {self.dim})")
+        with self._lock:  # ordered against mutations, as _run_search
+            tables = (self._records, self._metas, self._epoch)
+            n_live = self.count_sync()
+            idx = self._index
+            if idx is None or n_live == 0 or top_k <= 0:
+                return None, tables
+            k = min(int(top_k), n_live)
+            if (not q.is_cuda or not hasattr(idx, "search_device") or k > _native.HR_MAX_K
+                    or len(getattr(idx, "devices", (0,))) > 1):
+                return idx.search(q.detach().cpu().numpy(), k, None), tables
+            q = q.to(torch.float32).contiguous()
+            B = q.shape[0]
+            ns = (B * k + 1) // 2 * 2  # scores, then the rows 8-byte aligned: one buffer, one copy back
+            out = torch.empty((ns + 2 * B * k,), dtype=torch.float32, device=q.device)
+            s_out, r_out = out[:B * k], out[ns:].view(torch.int64)
+            st = torch.cuda.current_stream(q.device)
+            idx.search_device(q.data_ptr(), B, k, s_out.data_ptr(), r_out.data_ptr(), stream=st.cuda_stream)
+            host = out.cpu().numpy()  # (after the search, on the same stream)
+            return (host[:B * k].reshape(B, k).copy(), host[ns:].view(np.int64).reshape(B, k).copy()), tables
+
     def _submit_native(self, prep, batcher: _SearchBatcher, loop):
         """Launch an unfiltered batch through the asynchronous native entry point from the event loop
         (None: this batch takes the worker-thread path -- a filter, no async-capable index, k beyond

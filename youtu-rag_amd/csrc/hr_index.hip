@@ -380,6 +380,18 @@ extern "C" int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* met
 }
 
 // ---------------------------------------------------------------- search pieces
+// A/B knobs of the scan plan, read once (timing studies; the defaults are the measured choices):
+// HIPRAG_TAIL_CUS (32), HIPRAG_SAMPLE_MIN (1024: sampled tiles of a shard <= 80k tiles), HIPRAG_DYN_PCT (10),
+// HIPRAG_REFRESH_EVERY (4)
+static int knob(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+static const int kTailCus = knob("HIPRAG_TAIL_CUS", 32);
+static const int kSampleMin = knob("HIPRAG_SAMPLE_MIN", 1024);
+static const int kDynPct = knob("HIPRAG_DYN_PCT", 10);
+static const int kRefreshEvery = std::max(1, knob("HIPRAG_REFRESH_EVERY", 4));
+
 struct Plan {
     int QB, Bp, P;
     int NG;  // query groups per corpus pass (each QB*32 queries in one workgroup's LDS); Bp = NG*QB*32
@@ -427,7 +439,7 @@ static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list)
 // dynamic tail of a FILTER over W waves: the last 10 % of the units go out in 2-unit runs from the counter, but
 // only when every wave still gets a long static run (DESIGN.md "Dynamic tail"; profiles/r03_shard1.25M_knob_sweep.log)
 static void set_dyn_tail(ScanArgs& args, int64_t W, uint32_t* dyn_q) {
-    constexpr int pct = 10;
+    const int pct = kDynPct;
     const int64_t per_wave = args.n_units / W;
     args.dyn_start = args.n_units;
     if (per_wave >= 8 && dyn_q) {
@@ -591,7 +603,7 @@ static int launch_scan(hr_index* h, Scratch& sc, int cus, const Plan& pl, const 
 // on 224 of the 256 CUs (measured: 6.85 vs 6.81 TB/s at 10M rows, 0.434 vs 0.427 ms at 1.25M),
 // so select/rescore, the RCCL all-gather and the merge of the previous batch run beside it
 static int tail_cus(const hr_index* h) {
-    return std::max(0, std::min(32, h->n_cu - 8));
+    return std::max(0, std::min(kTailCus, h->n_cu - 8));
 }
 
 // ---- persistent FILTER: configuration, quiesce, close
@@ -772,7 +784,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
         // a shard sharing its GPU with other shards of a group samples 512 tiles: the co-located shards'
         // SAMPLEs add up (8 x 1.25M rows on one GPU: 3.387 / 3.308 / 3.297 ms per batch at 2048 / 1024 /
         // 512, profiles/r03_group_scan_streams.log)
-        const int64_t smin = h->shared_dev ? 512 : (n <= 80 * 1024 ? 1024 : 2048);
+        const int64_t smin = h->shared_dev ? 512 : (n <= 80 * 1024 ? kSampleMin : 2048);
         // beyond the dual-FILTER range n/256: the SAMPLE beside the FILTER reads half as much (10M rows 2.958-2.968
         // -> 2.944-2.956 ms/step, k = 100 -0.35 %; profiles/r04_sample_size_10M_ab.jsonl)
         return std::max<int64_t>(smin, n > 160 * 1024 ? n / 256 : n / 128);
@@ -957,7 +969,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     // positions, not tiles) parts keep contiguous per-wave ranges, as does the SAMPLE pass.
     a.strided = 1;
     a.teams = tl_ptr ? 0 : 1;
-    a.refresh_every = 4;
+    a.refresh_every = kRefreshEvery;
     // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
     // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->
     // 3.05-3.07 ms (two alternating repeats on one box), so big shards keep the epilogue loads ...

@@ -20,7 +20,6 @@ import logging
 import os
 import threading
 import weakref
-from concurrent.futures import ThreadPoolExecutor
 
 from .base import BaseEmbedder, BaseReranker, BaseRetriever, BaseVectorStore, RetrievalResult
 from .config import RetrieverConfig
@@ -41,21 +40,30 @@ class _Cohort:
 class _FusedRetrieve:
     """Concurrent ``retrieve`` calls (base_retriever.py:53-63: embed_query, then store.search) as cohorts of up to
     ``max_batch`` queries, each cohort ONE embedder forward whose (B, dim) output stays on the GPU and goes straight
-    into ONE store search (HipVectorStore.search_device_sync) -- no per-query vector lists through the host, no
-    second batching stage, and the cohort's forward and FILTER run back to back on one stream instead of
-    interleaving with other cohorts' work.  A worker thread runs the forward + search; the Chunk objects are built
-    on the caller's loop.  Results are those of the two-step path for the same vectors (the same store search;
-    embed_query returns this forward's rows as lists).  Each event loop has its own queue and drain (futures are
-    resolved only on their own loop); the loops share the one worker."""
+    into ONE store search -- no per-query vector lists through the host, no second batching stage.
+
+    One worker thread pipelines the cohorts: it enqueues cohort i+1's forward and its search (the pipelined shard
+    search of hiprag.dist.ShardedSearch on the store's index: scan + tail streams, guard flags copied asynchronously)
+    BEFORE it waits for cohort i's results, so the GPU always has the next cohort queued behind the current one while
+    the host tokenises, finalizes and hands results back.  The store's lock is held from a cohort's submit to its
+    finalize (a mutation must not move rows under a search in flight).  The Chunk objects are built on the caller's
+    loop.  Results are those of the two-step path for the same vectors (the same exact search).  Each event loop has
+    its own queue and drain (futures are resolved on their own loop only)."""
 
     def __init__(self, retriever: "VectorRetriever", max_batch: int):
+        import queue
+
         self.r, self.max_batch = retriever, max(1, int(max_batch))
         self._queues: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
         self._qlock = threading.Lock()
-        self._pool = None
-        self._pool_lock = threading.Lock()
-        self.cohorts = 0  # diagnostics: cohorts run / queries through them
+        self._work: "queue.Queue" = queue.Queue()  # cohorts from every loop, to the worker
+        self._thread = None
+        self._tlock = threading.Lock()
+        self._searcher = None  # (index, ShardedSearch) of the store's current index
+        self._k = 0  # the current cohort's largest top_k (worker thread)
+        self.cohorts = 0  # diagnostics: cohorts run / queries through them / cohorts overlapped with the next
         self.queries = 0
+        self.pipelined = 0
 
     def submit(self, query: str, top_k: int, threshold: float) -> asyncio.Future:
         loop = asyncio.get_running_loop()
@@ -67,61 +75,144 @@ class _FusedRetrieve:
         c.pending.append((query, int(top_k), float(threshold), fut))
         if not c.running:
             c.running = True
-            loop.call_soon(lambda: loop.create_task(self._drain(c)))
+            loop.call_soon(self._form, c, loop)
         return fut
 
-    def _executor(self):
-        with self._pool_lock:
-            if self._pool is None:
-                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hiprag-retrieve")
-            return self._pool
+    def _form(self, c: _Cohort, loop):
+        """On the loop, one iteration after the first call: hand the waiting calls to the worker in cohorts."""
+        c.running = False
+        while c.pending:
+            batch, c.pending = c.pending[: self.max_batch], c.pending[self.max_batch:]
+            batch = [e for e in batch if not e[3].done()]
+            if batch:
+                self._work.put((loop, batch))  # (before the check: a worker that is just leaving sees it)
+                self._ensure_worker()
 
-    def _run(self, texts: list[str], k: int):
-        """Worker thread: the cohort's forward and its search (device queries), the host records back."""
-        # (the embedder's forwards take its lock themselves: graph inputs are shared with its other callers)
-        q = self.r.embedder.encode_queries(texts)
-        return self.r.vector_store.search_device_sync(q, k)
+    def _ensure_worker(self):
+        with self._tlock:
+            if self._thread is None or not self._thread.is_alive():
+                self._thread = threading.Thread(target=self._worker, name="hiprag-retrieve", daemon=True)
+                self._thread.start()
 
-    async def _drain(self, c: _Cohort):
-        loop = asyncio.get_running_loop()
-        batch: list = []
+    # ---- worker thread
+    def _search(self, q):
+        """Launch the cohort's search (store lock held by the caller).  Returns a finisher -> (raw, tables)."""
+        store = self.r.vector_store
+        tables = (store._records, store._metas, store._epoch)
+        idx, n_live = store._index, store.count_sync()
+        B, k = q.shape[0], self._k
+        if idx is None or n_live == 0 or k <= 0:
+            return lambda: (None, tables)
+        k = min(k, n_live)
+        ss = self._sharded(idx, B) if q.is_cuda else None
+        if ss is None:  # (CPU tests, multi-device handles, k beyond the pipelined path: the synchronous search)
+            ran = store.search_device_sync(q, k)
+            return lambda: ran
+        slot = ss.submit(q, k)
+
+        def finish():
+            s_out, r_out = ss.finalize(slot)
+            return (s_out.cpu().numpy(), r_out.cpu().numpy()), tables
+        return finish
+
+    def _sharded(self, idx, B):
+        from .. import _native
+
+        if not hasattr(idx, "search_shard") or len(getattr(idx, "devices", (0,))) > 1 or self._k > _native.HR_MAX_K:
+            return None
+        if self._searcher is None or self._searcher[0] is not idx or self._searcher[1].max_batch < B:
+            import torch
+
+            from ..dist import ShardedSearch
+
+            self._drop_searcher()
+            dev = torch.device("cuda", idx.device)
+            self._searcher = (idx, ShardedSearch(idx, 0, max_batch=max(B, self.max_batch), device=dev, max_k=16))
+        return self._searcher[1]
+
+    def _deliver(self, loop, batch, ran, exc=None):
+        """Back on the caller's loop: Chunks from the finished search, each call's top_k and threshold."""
+        if exc is None:
+            try:
+                hits = self.r.vector_store._assemble(([None] * len(batch), max(e[1] for e in batch), None), ran)
+            except Exception as e:  # noqa: BLE001
+                exc = e
+        for i, (_, kq, th, f) in enumerate(batch):
+            if f.done():
+                continue
+            if exc is not None:
+                f.set_exception(exc)
+            else:
+                f.set_result(self.r._to_results(hits[i][:kq], th))
+
+    def _post(self, loop, batch, ran, exc=None):
+        if loop.is_closed():
+            return  # (the caller's loop ended: nobody waits for these)
         try:
-            while c.pending:
-                batch, c.pending = c.pending[: self.max_batch], c.pending[self.max_batch:]
-                batch = [e for e in batch if not e[3].done()]
-                if not batch:
-                    continue
-                k = max(e[1] for e in batch)
+            loop.call_soon_threadsafe(self._deliver, loop, batch, ran, exc)
+        except RuntimeError:  # closed between the check and the call
+            pass
+
+    def _worker(self):
+        import queue
+
+        store = self.r.vector_store
+        inflight = None  # (loop, batch, finisher) of the cohort whose search is on the GPU
+        locked = False
+        while True:
+            try:
+                item = self._work.get(timeout=0.5) if inflight is None else self._work.get_nowait()
+            except queue.Empty:
+                item = None
+            if item is None and inflight is None:
+                with self._tlock:  # (under the lock _ensure_worker takes: a cohort put now starts a new worker)
+                    if self._work.empty():
+                        self._thread = None
+                        return  # idle: the thread ends
+                continue
+            nxt = None
+            if item is not None:
+                loop, batch = item
                 try:
-                    ran = await loop.run_in_executor(self._executor(), self._run, [e[0] for e in batch], k)
-                    hits = self.r.vector_store._assemble(([None] * len(batch), k, None), ran)
-                except Exception as exc:  # noqa: BLE001 -- this cohort's callers see the failure
-                    for e in batch:
-                        if not e[3].done():
-                            e[3].set_exception(exc)
-                    batch = []
-                    continue
+                    self._k = max(e[1] for e in batch)
+                    q = self.r.embedder.encode_queries([e[0] for e in batch])  # (device, enqueued)
+                    if not locked:
+                        store._lock.acquire()
+                        locked = True
+                    nxt = (loop, batch, self._search(q))
+                except Exception as e:  # noqa: BLE001 -- this cohort's callers see the failure
+                    self._post(loop, batch, None, e)
+            if inflight is not None:
+                loop0, batch0, finish = inflight
+                try:
+                    ran = finish()
+                    self._post(loop0, batch0, ran)
+                except Exception as e:  # noqa: BLE001
+                    self._post(loop0, batch0, None, e)
                 self.cohorts += 1
-                self.queries += len(batch)
-                for (_, kq, th, f), h in zip(batch, hits):
-                    if not f.done():
-                        f.set_result(self.r._to_results(h[:kq], th))
-                batch = []
-        except BaseException as exc:  # the drain itself stopped (loop shutdown): no caller is left waiting
-            err = exc if isinstance(exc, Exception) else RuntimeError(f"retrieval stopped: {exc!r}")
-            for e in batch + c.pending:
-                if not e[3].done():
-                    e[3].set_exception(err)
-            c.pending = []
-            raise
-        finally:
-            c.running = False
+                self.queries += len(batch0)
+                if nxt is not None:
+                    self.pipelined += 1
+            inflight = nxt
+            if inflight is None and locked:
+                store._lock.release()
+                locked = False
+
+    def _drop_searcher(self):
+        """Release the pipelined searcher of a previous index (nothing is in flight: the worker finalizes every
+        cohort before it takes the next index); a store that closed its index already released what it held."""
+        if self._searcher is None:
+            return
+        idx, ss = self._searcher
+        self._searcher = None
+        if getattr(idx, "_h", None):
+            ss.close()
 
     def close(self):
-        with self._pool_lock:
-            if self._pool is not None:
-                self._pool.shutdown(wait=True)
-                self._pool = None
+        t = self._thread
+        if t is not None:
+            t.join(timeout=10)
+        self._drop_searcher()
 
 
 class VectorRetriever(BaseRetriever):

@@ -55,6 +55,17 @@ namespace hr {
 #ifndef HR_Q256_STAMPS  // diagnostic build: per-wave cycle shares of the round's phases, printed
 #define HR_Q256_STAMPS 0
 #endif
+// the 16x16x32 form (k_filter_q256_m16) for 16-bit rows at D = 512..1024 (0: the 32x32x16 k_filter_q256 for them);
+// its A prefetch distance in 16-query blocks and the register rotation that holds them (2 / 4: +0.5-1 %, 6 / 8 kept)
+#ifndef HR_Q256_MFMA16
+#define HR_Q256_MFMA16 1
+#endif
+#ifndef HR_Q256_PF16
+#define HR_Q256_PF16 6
+#endif
+#ifndef HR_Q256_SLOTS16
+#define HR_Q256_SLOTS16 8
+#endif
 #ifndef HR_Q256_VMEXACT
 #define HR_Q256_VMEXACT 1
 #endif
@@ -590,6 +601,432 @@ __global__ __launch_bounds__(kQT, 1) void k_filter_q256(ScanArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the look-ahead DMAs land before the workgroup's LDS goes)
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// The same FILTER on v_mfma_f32_16x16x32 (HR_Q256_MFMA16; 16-bit rows).  MI355X_MICROARCH.md "DVFS give-back" item 7:
+// under the clock this MFMA-dense body holds (~1.63 GHz, measured), the 16x16x32 shape delivers ~1.12-1.15x the
+// FLOP/s of 32x32x16 at equal cycles per FLOP.  Same corpus layout, windows, barriers and vmcnt accounting; what
+// changes is the operand and accumulator mapping:
+//  * a k32 step (= one query window of 2 k-steps) of a tile is two 16-row blocks rb: lane l = n + 16 q loads row slot
+//    16 rb + n, k = 8 q .. 8 q + 7 of the k32 step -- from k-step chunk q / 2, lane slot 16 rb + n + 32 (q % 2) of the
+//    tiled layout (16-byte loads at per-lane offsets; 4 x 256 contiguous bytes per load instruction);
+//  * the A fragment of a 16-query block: lane (m, q) reads query m of the block, the same k -- from the window buffer
+//    at k-step q / 2, 32-query block b / 2, lane 16 (b % 2) + m + 32 (q % 2);
+//  * 2 tiles x 2 row blocks x 16 query blocks x 4 = 256 accumulators; a lane holds row slot 16 rb + n (its group)
+//    against queries 16 b + 4 q + r in register r.
+// Measured (10M x 1024 bf16, B = 256, A/B on one box, profiles/r06_q256_m16_ab.jsonl): the chip holds 1.84 GHz
+// against 1.60 under the 32x32x16 form (GRBM_GUI_ACTIVE / 8 / duration), but the round takes more cycles -- twice the
+// MFMA instructions to issue, and an epilogue of 64 four-register items.  With one ballot per block (the four items of
+// a block share their thresholds) and the A fragments 6 blocks ahead it is 2-3 % faster per launch; the pass is then
+// bound by the corpus stream (no-ring-load timing build: -0.87 ms of 4.9) more than by the matrix pipe.
+template <int OFF>
+__device__ __forceinline__ void lds_read4s64_wait(uint32_t base, u32x4 (&t)[4]) {  // 4 x ds_read_b128, 64 B apart
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:%5\n\t"
+        "ds_read_b128 %1, %4 offset:%6\n\t"
+        "ds_read_b128 %2, %4 offset:%7\n\t"
+        "ds_read_b128 %3, %4 offset:%8\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+        : "v"(base), "n"(OFF), "n"(OFF + 64), "n"(OFF + 128), "n"(OFF + 192));
+}
+
+template <int I>
+__device__ __forceinline__ float acc_read4(const f32x4& v) {
+    float r;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(v[I]));
+    return r;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_sub(f32x2 x, f32x2 y) {  // x - y on both halves (one VALU op; the compiler emits two)
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+__device__ __forceinline__ float max3_raw(float x, float y, float z) {  // (no NaN canonicalisation of the inputs)
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+}
+
+template <int MT>
+__device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f32x4& c) {
+    if constexpr (MT == BF16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                       0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                      0);
+}
+
+template <int MT, int S_>
+__global__ __launch_bounds__(kQT, 1) void k_filter_q256_m16(ScanArgs a) {
+    using Geom = Q256Geom<S_, 1>;
+    constexpr int kRing = Geom::kRing, kLook = Geom::kLook, kNB = Geom::kNB;
+    constexpr int kVmNext = Geom::kVmNext, kBar = Geom::kBar;
+    constexpr int kR32 = kRing / kWin;  // k32 steps (windows) per ring span
+    static_assert(S_ % kRing == 0 && kRing % kWin == 0 && kWin == 2, "tile depth");
+    __shared__ __attribute__((aligned(16))) u32x4 qw[kNB * kWQ];
+    __shared__ __attribute__((aligned(16))) float th_lds[256];
+    constexpr int NQ = S_ / kRing;
+
+    const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, g = lane & 31;
+    const int n16 = lane & 15, q4 = lane >> 4;  // 16x16x32 lane roles: row / column n16, k-group q4
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t W2 = 2 * W;
+    const int64_t wr = (int64_t)wv * gridDim.x + blockIdx.x;
+    const int64_t n_tiles = a.n_units;
+    const int64_t rounds = (n_tiles + W2 - 1) / W2;
+    const int64_t full_rounds = n_tiles / W2;
+    auto tile_of = [&](int64_t u, int which) -> int64_t {
+        if (u >= rounds) return -1;
+        int64_t pos = wr;
+        if (HR_ROTATE_ROUNDS && u < full_rounds) {
+            pos += (int64_t)((uint32_t)((uint64_t)u * 2654435761ull) % (uint32_t)W);
+            if (pos >= W) pos -= W;
+        }
+        const int64_t t = HR_Q256_ADJ ? u * W2 + 2 * pos + which : u * W2 + which * W + pos;
+        return wave_uniform(t < n_tiles ? t : -1);
+    };
+    auto rsrc = [&](int64_t t) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(a.rows + (t < 0 ? 0 : t) * (S_ * 1024)), (short)0,
+                                                 t < 0 ? 0 : S_ * 1024, 0x00020000);
+    };
+    // per-lane byte offsets of the two row blocks of a k32 step (chunk q4 / 2, lane slot 16 rb + n16 + 32 (q4 % 2))
+    const int voff0 = (q4 >> 1) * 1024 + (n16 + 32 * (q4 & 1)) * 16;
+    const int voff1 = voff0 + 16 * 16;
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int k32, int rb) -> u32x4 {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, rb ? voff1 : voff0, k32 * 2048, HR_Q256_NT);
+    };
+    const int voff = lane * 16;
+    const __amdgpu_buffer_rsrc_t qr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.qfrag, (short)0, 4 * S_ * 2048, 0x00020000);
+    const uint32_t qw_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)qw;
+    auto stage = [&](int bi, int s0) {
+        u32x4* buf = qw + bi * kWQ;
+#pragma unroll
+        for (int j = 0; j < kDma; ++j) {
+            const int i = j >> 1, blk = (j & 1) * 4 + wv;
+            const int soff = (((blk >> 1) * S_ + s0 + i) * 2 + (blk & 1)) * 1024;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(buf + j * 256 + wv * 64),
+                                                     16, voff, soff, 0, 0);
+        }
+    };
+    // A fragment of 16-query block b in window buffer bi: this lane's address (k-step q4 / 2, lane 32 (q4 % 2) + n16;
+    // block b adds (b / 2) KiB + (b % 2) 256 B as an immediate)
+    const uint32_t lane_a = qw_base + (uint32_t)((q4 >> 1) * 8 * 1024 + (n16 + 32 * (q4 & 1)) * 16);
+    auto qbase = [&](int bi) -> uint32_t { return lane_a + (uint32_t)(bi * kWQ * 16); };
+    const uint32_t th_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)th_lds;
+    const uint32_t th_lane4 = th_base + (uint32_t)(4 * q4) * 4u;  // thresholds of queries 16 b + 4 q4 .. + 3 at + 64 b
+
+    // ---- thresholds: as k_filter_q256
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)a.mkeys, (short)0, kQT * 32 * 4, 0x00020000);
+    const uint32_t key_lane = (uint32_t)(((64 * wv + half) * 32 + g) * 4);
+    const uint32_t th_q = th_base + (uint32_t)(64 * wv + half) * 4u;
+    auto refresh = [&]() {
+        uint32_t key[32];
+        static_for<32>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(kr, key_lane, j * 256, 16);
+        });
+        static_for<32>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            const float f = half_min32(key2f(key[j] > HR_KEY_NEG_INF ? key[j] : HR_KEY_NEG_INF));
+            lds_write_f32<8 * j>(th_q, fmaxf(lds_read_f32o<8 * j>(th_q), f));
+        });
+    };
+    constexpr int kKR = 8;
+    constexpr int kParts = 32 / kKR;
+    uint32_t qkey[kKR];
+    auto part_load = [&](int p) {
+        static_for<kKR>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            qkey[j] = __builtin_amdgcn_raw_buffer_load_b32(kr, key_lane, p * (kKR * 256) + j * 256, 16);
+        });
+    };
+    auto part_apply = [&](int p) {
+        const uint32_t base = th_q + (uint32_t)p * (kKR * 8u);
+        uint32_t m[kKR];
+        static_for<kKR>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            m[j] = qkey[j] > HR_KEY_NEG_INF ? qkey[j] : HR_KEY_NEG_INF;
+        });
+        auto step = [&](auto CTRL_) {
+            static_for<kKR>([&](auto J_) {
+                constexpr int j = decltype(J_)::value;
+                m[j] = min(m[j], dpp_u32<decltype(CTRL_)::value>(m[j]));
+            });
+        };
+        step(std::integral_constant<int, 0xB1>{});
+        step(std::integral_constant<int, 0x4E>{});
+        step(std::integral_constant<int, 0x141>{});
+        step(std::integral_constant<int, 0x140>{});
+        float t[kKR];
+        lds_read8_stride8_wait(base, t);
+        static_for<kKR>([&](auto J_) {
+            constexpr int j = decltype(J_)::value;
+            const auto r = __builtin_amdgcn_permlane16_swap(m[j], m[j], false, false);
+            const uint32_t x = r[0], y = r[1];
+            lds_write_f32<8 * j>(base, fmaxf(t[j], key2f(min(x, y))));
+        });
+    };
+    th_lds[tid] = a.floor_q[tid];
+    __syncthreads();
+    refresh();
+
+    // ---- prologue
+    u32x4 ra[kRing], rb[kRing];  // slot 2 w + rb_: row block rb_ of the span's k32 step w
+    for (int w = 0; w < kLook; ++w) stage(w, (w * kWin) % S_);
+    {
+        const auto r0 = rsrc(tile_of(0, 0)), r1 = rsrc(tile_of(0, 1));
+#pragma unroll
+        for (int w = 0; w < kR32; ++w)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                ra[2 * w + h] = ld(r0, w, h);
+                rb[2 * w + h] = ld(r1, w, h);
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    uint32_t mycnt[4] = {0u, 0u, 0u, 0u};
+    // a passing (tile, row block, 16-query block)'s registers: rows of this lane's slot against queries 16 b + 4 q4 + r
+    auto walk = [&](int b, bool ok, uint32_t row, int slot, const f32x4& V, const f32x4& TH, uint32_t regs) {
+        const int gq = b >> 2;
+        uint32_t& cnt = mycnt[gq];
+        float2* const reg = a.pbuf + ((gq * W + wr) * 64) * a.capw;
+        while (regs) {
+            const int r = __builtin_amdgcn_readfirstlane(__builtin_ctz(regs));
+            regs &= regs - 1u;
+            const float v = V[r];
+            const int qm = (b & 3) * 16 + r;  // query (within the group) of lane quad 0
+            const bool pass = ok && v >= TH[r];
+            const uint64_t msk = __ballot(pass);
+            if (pass) atomicMax(a.mkeys + (int64_t)(gq * 64 + qm + 4 * q4) * 32 + slot, f2key(v));
+#pragma unroll
+            for (int hh = 0; hh < 4; ++hh) {
+                const uint32_t mh = (uint32_t)(msk >> (16 * hh)) & 0xFFFFu;
+                if (!mh) continue;
+                const int ql = qm + 4 * hh;
+                const uint32_t basepos = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ql);
+                if (pass && q4 == hh) {
+                    const uint32_t pos = basepos + __builtin_popcount(mh & ((1u << n16) - 1u));
+                    if (pos < (uint32_t)a.capw) reg[ql * a.capw + pos] = make_float2(v, __builtin_bit_cast(float, row));
+                }
+                cnt += (lane == ql) ? (uint32_t)__builtin_popcount(mh) : 0u;
+            }
+        }
+    };
+    auto allow_word = [&](int64_t t) -> uint32_t {
+        if (t < 0) return 0u;
+        uint32_t w0 = scalar_word(a.live, t);
+        if (a.mask) w0 &= scalar_word(a.mask, t);
+        return w0;
+    };
+    // A fragments kPf blocks ahead (one ds_read_b128 per 4 MFMAs, 64 cycles of matrix work) in a kSlots rotation
+    constexpr int kPf = HR_Q256_PF16;
+    constexpr int kSlots = HR_Q256_SLOTS16;
+    static_assert(kPf >= 1 && kPf < kSlots && (kSlots & (kSlots - 1)) == 0 && 16 % kSlots == 0, "A prefetch");
+    u32x4 pf[kSlots];
+    static_for<kPf>([&](auto P_) {  // (window 0's first reads: blocks 0 .. kPf - 1)
+        constexpr int pn = decltype(P_)::value;
+        pf[pn] = lds_read<(pn >> 1) * 1024 + (pn & 1) * 256>(qbase(0));
+    });
+    int wb = 0;
+    uint32_t qcur = qbase(0), qnext = qbase(1);
+    uint32_t dsink = 0;  // (HR_Q256_DIAG & 8 timing builds only)
+#if HR_Q256_STAMPS
+    uint64_t c_loop = 0, c_wait = 0, c_epi = 0, c_ref = 0;
+    uint32_t c_blocks = 0, c_regs = 0;
+#endif
+
+    for (int64_t u = 0; u < rounds; ++u) {
+        HR_STAMP(s_r0);
+        if (u >= 2) part_load((int)(u % kParts));
+        const int64_t tA = tile_of(u, 0), tB = tile_of(u, 1);
+        const int64_t nA = tile_of(u + 1, 0), nB = tile_of(u + 1, 1);
+        const uint32_t allowA = allow_word(tA), allowB = allow_word(tB);
+        float xs[2][2];  // (euclidean) |x|^2 of this lane's row in each (tile, row block)
+        static_for<2>([&](auto T_) {
+            constexpr int T = decltype(T_)::value;
+            const int64_t t = T ? tB : tA;
+            static_for<2>([&](auto R_) {
+                constexpr int rb_ = decltype(R_)::value;
+                xs[T][rb_] = (a.xnorm && t >= 0) ? a.xnorm[t * 32 + slot_row(t, 16 * rb_ + n16)] : 0.0f;
+            });
+        });
+        f32x4 acc[2][2][16];
+        static_for<2>([&](auto T_) {
+            static_for<2>([&](auto R_) {
+                static_for<16>([&](auto B_) {
+                    acc[decltype(T_)::value][decltype(R_)::value][decltype(B_)::value] = f32x4{};
+                });
+            });
+        });
+#pragma unroll
+        for (int qs = 0; qs < NQ; ++qs) {
+            const bool last = qs + 1 == NQ;
+            const auto sA = rsrc(last ? nA : tA), sB = rsrc(last ? nB : tB);
+            const int kb = last ? 0 : (qs + 1) * kR32;
+            static_for<kR32>([&](auto W_) {
+                constexpr int w = decltype(W_)::value;  // k32 step (window) within the span
+                if (w > 0 || qs > 0 || u > 0) wb = wb + 1 == kNB ? 0 : wb + 1;
+                if constexpr (w % kBar == 0) {
+                    HR_STAMP(s_w0);
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVmNext) : "memory");
+                    if (!(HR_Q256_DIAG & 4)) __builtin_amdgcn_s_barrier();
+#if HR_Q256_STAMPS
+                    HR_STAMP(s_w1);
+                    c_wait += s_w1 - s_w0;
+#endif
+                }
+                if (!(HR_Q256_DIAG & 1)) stage(wb >= kBar ? wb - kBar : wb - kBar + kNB, (qs * kRing + w * kWin + kLook * kWin) % S_);
+                qcur = qbase(wb);
+                qnext = qbase(wb + 1 == kNB ? 0 : wb + 1);
+                const u32x4 xa0 = ra[2 * w], xa1 = ra[2 * w + 1], xb0 = rb[2 * w], xb1 = rb[2 * w + 1];
+                if (!(HR_Q256_DIAG & 2)) {
+                    ra[2 * w] = ld(sA, kb + w, 0);
+                    ra[2 * w + 1] = ld(sA, kb + w, 1);
+                    rb[2 * w] = ld(sB, kb + w, 0);
+                    rb[2 * w + 1] = ld(sB, kb + w, 1);
+                } else {  // (timing build: the ring registers stay live without loads)
+                    ra[2 * w] ^= xb0;
+                    rb[2 * w + 1] ^= xa1;
+                }
+                static_for<16>([&](auto B_) {
+                    constexpr int b = decltype(B_)::value;
+                    constexpr int p = w * 16 + b;
+                    constexpr int pn = p + kPf;
+                    constexpr int wn = pn >> 4, bn = pn & 15;  // window (possibly the next span's first) and block read now
+                    const uint32_t base = wn != w ? qnext : qcur;
+                    pf[pn % kSlots] = lds_read<(bn >> 1) * 1024 + (bn & 1) * 256>(base);
+                    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(pf[p % kSlots]) : "n"(kPf));
+                    if constexpr ((HR_Q256_DIAG & 8) != 0) {  // (timing build: operands consumed, no MFMA)
+                        dsink ^= pf[p % kSlots].x ^ pf[p % kSlots].w ^ xa0.x ^ xb1.y;
+                    } else {
+                        acc[0][0][b] = mfma16<MT>(pf[p % kSlots], xa0, acc[0][0][b]);
+                        acc[0][1][b] = mfma16<MT>(pf[p % kSlots], xa1, acc[0][1][b]);
+                        acc[1][0][b] = mfma16<MT>(pf[p % kSlots], xb0, acc[1][0][b]);
+                        acc[1][1][b] = mfma16<MT>(pf[p % kSlots], xb1, acc[1][1][b]);
+                    }
+                });
+            });
+        }
+
+        // ---- epilogue: per 16-query block, the lane's 4 thresholds (4 blocks per LDS round trip) are the same for both
+        // tiles and both row blocks, so the block's 16 scores reduce to one max of (score - threshold) (packed
+        // subtracts, max3) and ONE ballot; a passing block (rare after the first rounds) is walked per (tile, row block)
+        auto epilogue = [&](auto EUC_) {
+            constexpr bool EUC = decltype(EUC_)::value;
+            bool ok[2][2];
+            float pen[2][2];  // 0 for an allowed row, -inf otherwise: the reduction stays branch-free
+            uint32_t rowv[2][2];
+            static_for<2>([&](auto T_) {
+                constexpr int T = decltype(T_)::value;
+                const int64_t t = T ? tB : tA;
+                const uint32_t allow = T ? allowB : allowA;
+                static_for<2>([&](auto R_) {
+                    constexpr int rb_ = decltype(R_)::value;
+                    const int rg = slot_row(t < 0 ? 0 : t, 16 * rb_ + n16);
+                    ok[T][rb_] = (allow >> rg) & 1u;
+                    pen[T][rb_] = ok[T][rb_] ? 0.0f : -__builtin_inff();
+                    rowv[T][rb_] = (uint32_t)(t * 32 + rg);
+                });
+            });
+            static_for<4>([&](auto G_) {
+                constexpr int gb = decltype(G_)::value;
+                u32x4 t4[4];
+                lds_read4s64_wait<gb * 256>(th_lane4, t4);
+                static_for<4>([&](auto J_) {
+                    constexpr int b = 4 * gb + decltype(J_)::value;
+                    const f32x4 TH = __builtin_bit_cast(f32x4, t4[decltype(J_)::value]);
+                    f32x4 V[2][2];
+                    float e = -__builtin_inff();
+                    static_for<2>([&](auto T_) {
+                        constexpr int T = decltype(T_)::value;
+                        static_for<2>([&](auto R_) {
+                            constexpr int rb_ = decltype(R_)::value;
+                            f32x4 r;
+                            static_for<4>([&](auto I_) {
+                                constexpr int i = decltype(I_)::value;
+                                r[i] = acc_read4<i>(acc[T][rb_][b]);
+                            });
+                            if constexpr (EUC) r = 2.0f * r - xs[T][rb_];
+                            V[T][rb_] = r;
+                            const f32x2 d0 = pk_sub(__builtin_shufflevector(r, r, 0, 1), __builtin_shufflevector(TH, TH, 0, 1));
+                            const f32x2 d1 = pk_sub(__builtin_shufflevector(r, r, 2, 3), __builtin_shufflevector(TH, TH, 2, 3));
+                            const float m = max3_raw(d0[0], d0[1], d1[0]) + pen[T][rb_];
+                            e = max3_raw(e, m, d1[1] + pen[T][rb_]);
+                        });
+                    });
+                    if (!__ballot(e >= 0.0f)) return;
+                    static_for<2>([&](auto T_) {
+                        constexpr int T = decltype(T_)::value;
+                        static_for<2>([&](auto R_) {
+                            constexpr int rb_ = decltype(R_)::value;
+                            const bool okv = ok[T][rb_];
+                            uint32_t regs = 0;
+                            static_for<4>([&](auto I_) {
+                                constexpr int i = decltype(I_)::value;
+                                regs |= (__ballot(okv && V[T][rb_][i] >= TH[i]) != 0 ? 1u : 0u) << i;
+                            });
+                            if (!regs) return;
+                            walk(b, okv, rowv[T][rb_], 16 * rb_ + n16, V[T][rb_], TH, regs);
+#if HR_Q256_STAMPS
+                            c_blocks += 1;
+                            c_regs += __builtin_popcount(regs);
+#endif
+                        });
+                    });
+                });
+            });
+        };
+        HR_STAMP(s_r1);
+        if constexpr ((HR_Q256_DIAG & 24) != 0) {  // (timing build: no epilogue, the accumulators kept live)
+            float z = 0.0f;
+            static_for<2>([&](auto T_) {
+                static_for<2>([&](auto R_) {
+                    static_for<16>([&](auto B_) {
+                        z += acc_read4<0>(acc[decltype(T_)::value][decltype(R_)::value][decltype(B_)::value]);
+                    });
+                });
+            });
+            mycnt[0] += __builtin_bit_cast(uint32_t, z) + allowA + allowB;
+        } else {
+            if (a.xnorm) epilogue(std::true_type{});
+            else epilogue(std::false_type{});
+        }
+        HR_STAMP(s_r2);
+        if (u < 2) refresh();
+        else part_apply((int)(u % kParts));
+#if HR_Q256_STAMPS
+        HR_STAMP(s_r3);
+        c_loop += s_r1 - s_r0;
+        c_epi += s_r2 - s_r1;
+        c_ref += s_r3 - s_r2;
+#endif
+    }
+#if HR_Q256_STAMPS
+    if (lane == 0 && (blockIdx.x % 32) == 0)
+        printf("q256 stamps blk %d wave %d rounds %ld loop %lu (window waits %lu) epilogue %lu refresh %lu blocks %u regs %u\n",
+               (int)blockIdx.x, wv, (long)rounds, (unsigned long)c_loop, (unsigned long)c_wait, (unsigned long)c_epi,
+               (unsigned long)c_ref, c_blocks, c_regs);
+#endif
+    if constexpr ((HR_Q256_DIAG & 8) != 0) mycnt[0] += dsink;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) a.pcnt[(x * W + wr) * 64 + lane] = mycnt[x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int MT, int S_>
+int launch_m16(int cus, const ScanArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_filter_q256_m16<MT, S_>), dim3((unsigned)cus), dim3(kQT), 0, st, a);
+    return hipGetLastError() == hipSuccess ? HR_OK : HR_E_HIP;
+}
+
 template <int MT, int DT, int S_>
 int launch_t(int cus, const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_filter_q256<MT, DT, S_>), dim3((unsigned)cus), dim3(kQT), 0, st, a);
@@ -606,18 +1043,30 @@ int launch_filter_q256(int mt, int dtype, int S, int cus, const ScanArgs& a, hip
     if (!q256_filter_ok(dtype, S)) return HR_E_UNSUPPORTED;
 #define HR_Q256_CASE(MTv, DTv, Sv) \
     if (mt == MTv && dtype == DTv && S == Sv) return launch_t<MTv, DTv, Sv>(cus, a, st);
-#ifdef HR_Q256_ONE_F32  // (code studies of the fp32 form: that instantiation only)
+#define HR_Q256_M16(MTv, Sv) \
+    if (mt == MTv && dtype == MTv && S == Sv) return launch_m16<MTv, Sv>(cus, a, st);
+    // 16-bit rows at D = 512..1024: the 16x16x32 form (HR_Q256_MFMA16 0 builds the 32x32x16 one for them instead);
+    // D = 256 keeps the 16-deep-ring 32x32x16 form
+#if defined(HR_Q256_ONE_F32)  // (code studies of the fp32 form: that instantiation only)
     HR_Q256_CASE(F16, F32, 64)
+#elif HR_Q256_MFMA16
+    HR_Q256_M16(BF16, 64)
 #else
     HR_Q256_CASE(BF16, BF16, 64)
 #endif
 #if !defined(HR_Q256_ONE) && !defined(HR_Q256_ONE_F32)  // (register-allocation studies compile one instantiation)
-    HR_Q256_CASE(BF16, BF16, 48) HR_Q256_CASE(BF16, BF16, 32) HR_Q256_CASE(BF16, BF16, 16)
-    HR_Q256_CASE(F16, F16, 64) HR_Q256_CASE(F16, F16, 48) HR_Q256_CASE(F16, F16, 32) HR_Q256_CASE(F16, F16, 16)
+#if HR_Q256_MFMA16
+    HR_Q256_M16(BF16, 48) HR_Q256_M16(BF16, 32) HR_Q256_M16(F16, 64) HR_Q256_M16(F16, 48) HR_Q256_M16(F16, 32)
+#else
+    HR_Q256_CASE(BF16, BF16, 48) HR_Q256_CASE(BF16, BF16, 32)
+    HR_Q256_CASE(F16, F16, 64) HR_Q256_CASE(F16, F16, 48) HR_Q256_CASE(F16, F16, 32)
+#endif
+    HR_Q256_CASE(BF16, BF16, 16) HR_Q256_CASE(F16, F16, 16)
     // fp32 rows: f16 MFMA for cosine (normalised rows), bf16 for raw inner product / euclidean (mfma_type)
     HR_Q256_CASE(F16, F32, 64) HR_Q256_CASE(F16, F32, 48) HR_Q256_CASE(F16, F32, 32) HR_Q256_CASE(F16, F32, 16)
     HR_Q256_CASE(BF16, F32, 64) HR_Q256_CASE(BF16, F32, 48) HR_Q256_CASE(BF16, F32, 32) HR_Q256_CASE(BF16, F32, 16)
 #endif
+#undef HR_Q256_M16
 #undef HR_Q256_CASE
     return HR_E_UNSUPPORTED;
 }

@@ -56,6 +56,10 @@ def main():
     p.add_argument("--max-batch", type=int, default=64, help="store search batches (and the embedder's batch_size)")
     p.add_argument("--embed-batch", default="64", help="comma list: queries per coalesced forward (A/B)")
     p.add_argument("--profile", default="", help="write a cProfile summary (event-loop thread) to PATH.<clients>")
+    # application choices, not library policy (A/B of the cycle collector's share): the store's opt-in untracked results
+    # (index_params.untracked_results), or the application's own gc.freeze() after its setup
+    p.add_argument("--untracked", action="store_true")
+    p.add_argument("--gc-freeze", action="store_true")
     a = p.parse_args()
 
     import numpy as np
@@ -72,6 +76,12 @@ def main():
     ret = VectorRetriever(st, emb, RetrieverConfig(top_k=a.k, similarity_threshold=0.0))
     qs = queries(4096)
     emb.encode_queries(qs[:a.max_batch])  # graph capture of the common shapes
+    st.untracked_results = bool(a.untracked)
+    if a.gc_freeze:
+        import gc
+
+        gc.collect()
+        gc.freeze()
     print(f"# store of {a.rows} rows + embedder in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
     # the worker's time per forward, split: host tokenise + pack + launch, the device wait, the host lists
     wt = {"launch": 0.0, "wait": 0.0, "lists": 0.0, "n": 0}
@@ -102,6 +112,8 @@ def main():
             l0 = st._batcher.launches
             f0 = emb._coalescer.forwards if emb._coalescer else 0
             c0 = fused.cohorts if fused is not None else 0
+            if fused is not None:
+                fused.timing = {k: 0 for k in fused.timing}
             for key in wt:
                 wt[key] = 0
             if a.profile:
@@ -125,8 +137,11 @@ def main():
                               "embed_forwards": fw,
                               "search_launches": (st._batcher.launches - l0) if mode != "fused" else fw,
                               "worker_ms_per_forward": {k: round(1e3 * wt[k] / n, 3) for k in ("launch", "wait", "lists")}
-                              if mode == "coalesce" else None,
-                              "profiled": bool(a.profile),
+                              if mode == "coalesce" else
+                              {k: (round(1e3 * v / max(1, fused.cohorts - c0), 3) if k != "bubbles" else v)
+                               for k, v in fused.timing.items()} if mode == "fused" else None,
+                              "profiled": bool(a.profile), "untracked_results": bool(a.untracked),
+                              "app_gc_freeze": bool(a.gc_freeze),
                               "model": "bge-large shape (random init), bf16", "path": "VectorRetriever.retrieve"}),
                   flush=True)
 

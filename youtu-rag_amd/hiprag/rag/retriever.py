@@ -19,6 +19,7 @@ import asyncio
 import logging
 import os
 import threading
+import time
 import weakref
 
 from .base import BaseEmbedder, BaseReranker, BaseRetriever, BaseVectorStore, RetrievalResult
@@ -64,6 +65,9 @@ class _FusedRetrieve:
         self.cohorts = 0  # diagnostics: cohorts run / queries through them / cohorts overlapped with the next
         self.queries = 0
         self.pipelined = 0
+        # diagnostics (worker thread, seconds): forward tokenise + launch, search submit, finalize (the device wait
+        # included), and cohorts finalized with no next cohort queued behind them (pipeline bubbles)
+        self.timing = {"encode": 0.0, "submit": 0.0, "finalize": 0.0, "bubbles": 0}
 
     def submit(self, query: str, top_k: int, threshold: float) -> asyncio.Future:
         loop = asyncio.get_running_loop()
@@ -171,24 +175,33 @@ class _FusedRetrieve:
                         return  # idle: the thread ends
                 continue
             nxt = None
+            tm = self.timing
             if item is not None:
                 loop, batch = item
                 try:
                     self._k = max(e[1] for e in batch)
+                    t0 = time.perf_counter()
                     q = self.r.embedder.encode_queries([e[0] for e in batch])  # (device, enqueued)
+                    t1 = time.perf_counter()
                     if not locked:
                         store._lock.acquire()
                         locked = True
                     nxt = (loop, batch, self._search(q))
+                    tm["encode"] += t1 - t0
+                    tm["submit"] += time.perf_counter() - t1
                 except Exception as e:  # noqa: BLE001 -- this cohort's callers see the failure
                     self._post(loop, batch, None, e)
             if inflight is not None:
                 loop0, batch0, finish = inflight
+                if nxt is None:
+                    tm["bubbles"] += 1
+                t0 = time.perf_counter()
                 try:
                     ran = finish()
                     self._post(loop0, batch0, ran)
                 except Exception as e:  # noqa: BLE001
                     self._post(loop0, batch0, None, e)
+                tm["finalize"] += time.perf_counter() - t0
                 self.cohorts += 1
                 self.queries += len(batch0)
                 if nxt is not None:

@@ -101,3 +101,36 @@ def test_assemble_rejects_bad_input():
     with pytest.raises((TypeError, AttributeError)):
         hostfast.assemble(NoSlots, rec, meta, sc, [10], None)
     assert gc.isenabled()  # the collector is re-enabled on every error path
+
+
+def _flat_results(res):
+    return [[(r.chunk.id, r.chunk.document_id, r.chunk.content, r.chunk.chunk_index, r.chunk.metadata, r.chunk.embedding,
+              r.score, r.rank) for r in q] for q in res]
+
+
+@pytest.mark.parametrize("with_embs", [False, True])
+def test_assemble_results_matches_retriever_path(with_embs):
+    """assemble_results (the fused retrieve's delivery) = VectorRetriever._to_results over assemble's pairs cut to each
+    call's top_k (base_retriever.py:66-80): ranks before the threshold, deleted rows skipped without a rank, a
+    threshold <= 0 keeping every hit; in C, in the Python fallback, and through the two-step path."""
+    from hiprag.rag.base import RetrievalResult
+    from hiprag.rag.retriever import VectorRetriever
+
+    rec, meta, sc = _hits(600, seed=11)
+    per_q = [10, 0, 37, 3, 250, 0, 300]
+    ks = [10, 5, 20, 1, 16, 3, 300]
+    ths = [0.0, 0.5, 0.5, -1.0, 0.9, 0.0, 0.25]
+    embs = [[float(i), -1.0] for i in range(600)] if with_embs else None
+    a = hostfast.assemble_results(Chunk, RetrievalResult, rec, meta, sc, per_q, embs, ks, ths)
+    b = storage._assemble_results_py(Chunk, RetrievalResult, rec, meta, sc, per_q, embs, ks, ths)
+    pairs = storage._assemble_py(Chunk, rec, meta, sc, per_q, embs)
+    ref = [VectorRetriever._to_results(None, pairs[q][:ks[q]], ths[q]) for q in range(len(per_q))]
+    assert _flat_results(a) == _flat_results(b) == _flat_results(ref)
+    assert any(len(q) for q in a) and all(type(r) is RetrievalResult for q in a for r in q)
+    assert all(gc.is_tracked(r) and gc.is_tracked(r.chunk) for q in a for r in q)
+    u = hostfast.assemble_results(Chunk, RetrievalResult, rec, meta, sc, per_q, None, ks, ths, True)
+    assert not any(gc.is_tracked(r) or gc.is_tracked(r.chunk) for q in u for r in q)
+    with pytest.raises(ValueError):
+        hostfast.assemble_results(Chunk, RetrievalResult, rec, meta, sc, per_q, None, ks[:3], ths)
+    del a, b, u
+    gc.collect()

@@ -138,7 +138,8 @@ class _FusedRetrieve:
         """Back on the caller's loop: Chunks from the finished search, each call's top_k and threshold."""
         if exc is None:
             try:
-                hits = self.r.vector_store._assemble(([None] * len(batch), max(e[1] for e in batch), None), ran)
+                res = self.r.vector_store._assemble_results(ran, [e[1] for e in batch], [e[2] for e in batch],
+                                                            RetrievalResult)
             except Exception as e:  # noqa: BLE001
                 exc = e
         for i, (_, kq, th, f) in enumerate(batch):
@@ -147,7 +148,7 @@ class _FusedRetrieve:
             if exc is not None:
                 f.set_exception(exc)
             else:
-                f.set_result(self.r._to_results(hits[i][:kq], th))
+                f.set_result(res[i])
 
     def _post(self, loop, batch, ran, exc=None):
         if loop.is_closed():
@@ -250,6 +251,7 @@ class VectorRetriever(BaseRetriever):
         if os.environ.get("HIPRAG_FUSED_RETRIEVE", "1") == "0":  # (A/B switch: the reference's two awaits)
             return False
         return (self.reranker is None and callable(getattr(self.vector_store, "search_device_sync", None))
+                and callable(getattr(self.vector_store, "_assemble_results", None))
                 and callable(getattr(self.embedder, "encode_queries", None))
                 and hasattr(self.embedder, "_fwd_lock") and getattr(self.embedder, "fused_retrieve", True))
 

@@ -83,6 +83,29 @@ def _assemble_py(C, rec_l, meta_l, score_l, per_q, embs, untrack=False):
         i += cnt
     return out
 
+
+def _assemble_results_py(C, R, rec_l, meta_l, score_l, per_q, embs, ks, ths, untrack=False):
+    """The per-query RetrievalResult lists of a batch's gathered hits for calls with top_k ks[q] and similarity
+    threshold ths[q] (VectorRetriever._to_results over _assemble_py's pairs cut to top_k); _hostfast.assemble_results
+    is the same in C (`untrack` only applies there)."""
+    out, i = [], 0
+    for q, cnt in enumerate(per_q):
+        res, pos, kq, th = [], 0, ks[q], ths[q]
+        for j in range(i, i + cnt):
+            r = rec_l[j]
+            if r is None or pos >= kq:
+                continue
+            pos += 1
+            if th > 0.0 and not score_l[j] >= th:
+                continue
+            m = meta_l[j]
+            res.append(R(C(r[0], m.get("document_id", ""), r[2], m.get("chunk_index", 0), dict(m),
+                           None if embs is None else embs[j]), score_l[j], pos))
+        out.append(res)
+        i += cnt
+    return out
+
+
 logger = logging.getLogger(__name__)
 
 _METRIC = {"cosine": "cosine", "dot": "ip", "euclidean": "l2"}
@@ -824,15 +847,13 @@ class HipVectorStore(BaseVectorStore):
         finally:
             self._lock.release()
 
-    def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
-        """(Chunk, score) lists of a finished batch.  Runs on the event loop while the next launch is in
-        flight, so it is the host's per-hit cost under load: the hits' host records are gathered for the
-        whole batch at once (object-array fancy indexing instead of a Python lookup per row and field); each hit is
-        a slotted Chunk (two tracked objects per hit with its tuple) with a fresh metadata dict, as Chroma returns."""
+    def _gather(self, ran):
+        """The host lists of a finished batch's hits -- (rec_l, meta_l, score_l, per_q, embs) -- or None when the store
+        was cleared since the search ran (its rows are gone).  The hits' host records are gathered for the whole batch
+        at once (object-array fancy indexing instead of a Python lookup per row and field)."""
         raw, (recs, metas, epoch) = ran
-        n = len(prep[0])
-        if raw is None or epoch != self._epoch:  # cleared since the search ran: its rows are gone
-            return [[] for _ in range(n)]
+        if raw is None or epoch != self._epoch:
+            return None
         scores, rows = raw
         # the tables the search ran against (append-only; a row deleted since then reads None, dropped)
         # rows the index returned but the tables do not hold yet (an add racing a native launch) are
@@ -848,13 +869,32 @@ class HipVectorStore(BaseVectorStore):
             keep = [i for i, r in enumerate(rec_l) if r is not None]
             with self._lock:
                 if epoch != self._epoch:
-                    return [[] for _ in range(n)]
+                    return None
                 e = self._embeddings(hit_rows[keep].tolist())
             embs = [None] * len(rec_l)
             for j, i in enumerate(keep):
                 embs[i] = e[j].tolist()
-        return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, rec_l, meta_l, score_l, per_q, embs,
-                                                                               self.untracked_results)
+        return rec_l, meta_l, score_l, per_q, embs
+
+    def _assemble(self, prep, ran) -> list[list[tuple[Chunk, float]]]:
+        """(Chunk, score) lists of a finished batch.  Runs on the event loop while the next launch is in
+        flight, so it is the host's per-hit cost under load: each hit is a slotted Chunk (two tracked objects per hit
+        with its tuple) with a fresh metadata dict, as Chroma returns."""
+        g = self._gather(ran)
+        if g is None:
+            return [[] for _ in range(len(prep[0]))]
+        return (_hostfast.assemble if _hostfast is not None else _assemble_py)(Chunk, *g, self.untracked_results)
+
+    def _assemble_results(self, ran, ks: list[int], ths: list[float], result_cls) -> list[list]:
+        """A finished batch as the retriever's per-call results (result_cls(chunk, score, rank): top_k ks[q], threshold
+        ths[q], ranks before the threshold -- base_retriever.py:66-80 without a reranker), built in one pass without
+        the (Chunk, score) pairs: one tracked object fewer per hit for the cycle collector, and no Chunk for a hit past
+        its call's top_k."""
+        g = self._gather(ran)
+        if g is None:
+            return [[] for _ in ks]
+        fn = _hostfast.assemble_results if _hostfast is not None else _assemble_results_py
+        return fn(Chunk, result_cls, *g, [int(k) for k in ks], [float(t) for t in ths], self.untracked_results)
 
     async def search(self, query_embedding: list[float], top_k: int = 5, filters: dict[str, Any] | None = None
                      ) -> list[tuple[Chunk, float]]:

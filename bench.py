@@ -694,7 +694,11 @@ def main():
 
     qps = args.steps * B / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-    esz = {"bf16": 2, "f16": 2, "f32": 4}[args.dtype]
+    # corpus bytes per element the FILTER must read: fp32 rows are scanned through their 16-bit shadow (the values
+    # the fp32 kernels rounded every fragment to; the exact rescoring reads fp32 -- hr_internal.hpp rows16) unless
+    # HIPRAG_F32_SHADOW=0
+    f32_shadow = args.dtype == "f32" and os.environ.get("HIPRAG_F32_SHADOW", "1") != "0"
+    esz = 2 if f32_shadow else {"bf16": 2, "f16": 2, "f32": 4}[args.dtype]
     n_max_local = -(-N // G)
     alg_bytes = n_max_local * D * esz  # corpus bytes one filter-scan launch must read (largest shard)
     # FILTER launches per batch (the timed events bracket them all): 65-128 queries are one launch of the 128-query
@@ -736,7 +740,9 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "frac_of_measured_read_ceiling": round(achieved / HBM_READ_CEILING_GBS, 4),
                      "read_ceiling_source": "profiles/r02_stream_ceiling.jsonl", "traffic": None,
-                     "bytes_per_launch": alg_bytes, "avg_launch_ms": round(scan_avg / passes, 4),
+                     "bytes_per_launch": alg_bytes, "scan_bytes_per_element": esz,
+                     **({"scan_rows": "16-bit shadow of the fp32 rows"} if f32_shadow else {}),
+                     "avg_launch_ms": round(scan_avg / passes, 4),
                      "sample_pass_ms": round(sample_avg, 4), "guard_fallback_queries": fallback_queries},
         # host work per step (submit minus its waits for guard flags): at or above ms_per_step the step is host-bound
         "host_ms_per_step": round(1000.0 * (elapsed - host_wait_s) / args.steps, 4),

@@ -965,7 +965,9 @@ def test_wide_filter_vs_oracle(native, dim, dtype, n, B, k):
     The first unmasked search must have launched the 128-query FILTER exactly where the plan takes it."""
     rng = np.random.default_rng(dim + B + n)
     n_parts = (native.kc_for_k(k, dim) + 31) // 32
-    wide_expected = n_parts == 1 or (n_parts <= 7 if dtype == "f32" else (n_parts <= 3 and B <= 128))
+    # (fp32 rows scan their 16-bit shadow and plan as 16-bit rows; HIPRAG_F32_SHADOW=0 keeps the fp32 plan)
+    f32_plan = dtype == "f32" and os.environ.get("HIPRAG_F32_SHADOW", "1") == "0"
+    wide_expected = n_parts == 1 or (n_parts <= 7 if f32_plan else (n_parts <= 3 and B <= 128))
     # (raw inner products of the synthetic rows overflow f16 storage: ip on bf16 / fp32 only; fp32 rows reach the
     # MFMA as f16 for cosine, bf16 for ip)
     for metric in ("cosine", "ip") if dtype != "f16" else ("cosine",):
@@ -1202,3 +1204,57 @@ def test_every_tile_scanned_exactly_once(native):
         assert int(idx.wave_tiles().sum()) == listed
     finally:
         idx.close()
+
+
+# ---------------------------------------------------------------- fp32 corpora: the 16-bit scan shadow
+@pytest.mark.parametrize("metric", ["cosine", "ip", "l2"])
+def test_f32_shadow_incremental_reload_and_off(native, metric, tmp_path, monkeypatch):
+    """fp32 rows are streamed by the approximate passes from a 16-bit shadow (hr_internal.hpp rows16), kept current
+    lazily: searches between adds (a partial last tile re-converted), removals, a save / load (the shadow rebuilt from
+    the loaded rows) and batches of 1 / 40 / 200 queries (k_scan, the 128- and 256-query FILTERs) answer as the
+    oracle does, and as an index built with HIPRAG_F32_SHADOW=0 (the fp32 tiles rounded in the kernels)."""
+    rng = np.random.default_rng({"cosine": 1, "ip": 2, "l2": 3}[metric])
+    dim, n = 512, 12_000
+    x = _embedding_like(rng, n, dim, scale=2.0)
+    stored = R.process_rows(x, metric, "f32")
+    qm = (lambda q: R.process_queries(q, metric)) if metric == "cosine" else (lambda q: q)
+
+    def planted(B, upto):
+        j = rng.choice(upto, B, replace=False)
+        return (x[j] + 0.05 * rng.standard_normal((B, dim)).astype(np.float32)).astype(np.float32)
+
+    def check(idx, q, k, upto, mask=None):
+        s, r = idx.search(q, k, None if mask is None else oracle.mask_from_bool(mask))
+        s_ref, r_ref = oracle.c_search(stored[:upto], "f32", qm(q), k,
+                                       None if mask is None else oracle.mask_from_bool(mask), metric=metric)
+        _check(s, r, s_ref, r_ref)
+        return s, r
+
+    monkeypatch.delenv("HIPRAG_F32_SHADOW", raising=False)
+    idx = native.NativeIndex(dim, "f32", metric)
+    for upto in (5_000, 5_017, n):  # (5,017: the second add lands in the first add's last, partial tile)
+        idx.add(x[idx.size()[0]:upto])
+        check(idx, planted(40, upto), 10, upto)
+    gone = rng.choice(n, 500, replace=False)
+    idx.remove(gone)
+    allowed = np.ones(n, bool)
+    allowed[gone] = False
+    results = {}
+    for B in (1, 40, 200):
+        q = planted(B, n)
+        results[B] = (q, check(idx, q, 10, n, allowed))
+    p = str(tmp_path / "f32.hri")
+    idx.save(p)
+    idx2 = native.NativeIndex.load(p, dim=dim, dtype="f32", metric=metric)
+    for B, (q, (s, r)) in results.items():
+        s2, r2 = idx2.search(q, 10)
+        np.testing.assert_array_equal(r2, r)
+        np.testing.assert_array_equal(s2, s)
+    monkeypatch.setenv("HIPRAG_F32_SHADOW", "0")
+    off = native.NativeIndex(dim, "f32", metric)
+    off.add(x)
+    off.remove(gone)
+    for B, (q, (s, r)) in results.items():
+        s3, r3 = off.search(q, 10)
+        np.testing.assert_array_equal(r3, r)
+        np.testing.assert_array_equal(s3, s)

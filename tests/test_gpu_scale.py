@@ -14,6 +14,8 @@
 Bar: ids identical (score desc, row asc), scores equal to the oracle's fp64 canonical scores cast
 to fp32 (so within the north_star's 1e-5).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -306,9 +308,15 @@ def test_c3_10M_f32_vs_oracle(c3_f32, k):
     """The drop-in store's default dtype (fp32 rows, the reference's: faiss_store.py:98, :148-154; Chroma
     float32) at the headline size, 40.96 GB: fp32 rows reach the MFMA as f16 and rely on the exactness guard,
     whose window is widest here (isotropic queries over 10M rows).  B = 64 runs k_scan; B = 128 the fp32
-    128-query FILTER (asserted through hr_index_wide_launches, row parts at k = 100).  Identical to the oracle's
+    128-query FILTER where the plan takes it (asserted through hr_index_wide_launches).  Identical to the oracle's
     exact fp32 answer; the guard counters are printed."""
+    from hiprag import _native
+
     idx, q, s_ref, r_ref, *_ = c3_f32
+    # the 128-query FILTER takes up to 3 row parts on 16-bit rows -- fp32 rows scan their 16-bit shadow and plan
+    # alike -- and up to 7 on fp32 rows streamed as such (HIPRAG_F32_SHADOW=0)
+    n_parts = (_native.kc_for_k(k, 1024) + 31) // 32
+    wide_ok = n_parts <= (7 if os.environ.get("HIPRAG_F32_SHADOW", "1") == "0" else 3)
     for B in (64, 128):
         before, w0 = idx.stats(), idx.wide_launches()
         if B == 64:
@@ -319,7 +327,7 @@ def test_c3_10M_f32_vs_oracle(c3_f32, k):
         after, w1 = idx.stats(), idx.wide_launches()
         print(f"\nC3 10Mx1024 f32 k={k} B={B}: 128-query FILTER launches {w1 - w0}, guard failures "
               f"{after['guard_failures'] - before['guard_failures']}, exhaustive {after['exhaustive'] - before['exhaustive']}")
-        assert (w1 - w0 > 0) == (B == 128)
+        assert (w1 - w0 > 0) == (B == 128 and wide_ok)
         _check(s[:64], r[:64], s_ref[:64, :k], r_ref[:64, :k])    # planted
         _check(s[64:], r[64:], s_ref[64:, :k], r_ref[64:, :k])    # isotropic
 

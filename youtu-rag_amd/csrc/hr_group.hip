@@ -1027,6 +1027,7 @@ int group_load_into(hr_index* g, FILE* f, int64_t n, int64_t n_live, double max_
             const int64_t l0 = T0 / G + (T0 % G > s ? 1 : 0);
             if (int rc = set_device(sh)) return rc;
             HIP_TRY(hipMemcpy(sh->rows + (size_t)l0 * tb, sb[(size_t)s].data(), sb[(size_t)s].size(), hipMemcpyHostToDevice));
+            shadow_stale(sh, l0);
         }
     }
     std::vector<uint32_t> lw((size_t)tiles);

@@ -83,6 +83,11 @@ extern "C" int hr_index_create(int dim, int dtype, int metric, int n_dev, const 
     h->dtype = dtype;
     h->metric = metric;
     h->device = dev;
+    {
+        const char* e = std::getenv("HIPRAG_F32_SHADOW");
+        h->shadow = dtype == F32 && !(e && e[0] == '0');
+        h->shadow_lo = INT64_MAX;
+    }
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&h->norm_bits, sizeof(unsigned long long));
@@ -125,6 +130,18 @@ int index_grow(hr_index* h, int64_t need_rows) {
     if (h->xnorm) {
         HIP_TRY(hipStreamSynchronize(h->stream));
         HIP_TRY(hipFree(h->xnorm));
+    }
+    if (h->shadow) {  // the 16-bit shadow grows with the rows (its converted tiles carried over)
+        const size_t tb16 = (size_t)h->S * 1024;
+        uint8_t* n16 = nullptr;
+        HIP_TRY(hipMalloc(&n16, (size_t)(new_cap / 32) * tb16));
+        HIP_TRY(hipMemsetAsync(n16, 0, (size_t)(new_cap / 32) * tb16, h->stream));
+        if (h->rows16) {
+            HIP_TRY(hipMemcpyAsync(n16, h->rows16, (size_t)(h->cap / 32) * tb16, hipMemcpyDeviceToDevice, h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            HIP_TRY(hipFree(h->rows16));
+        }
+        h->rows16 = n16;
     }
     h->rows = nr;
     h->live = nl;
@@ -208,6 +225,7 @@ static int add_impl(hr_index* h, const float* rows, uint64_t seed, int64_t gen_b
         if (rc) return rc;
     }
     h->n = r0 + n;
+    shadow_stale(h, r0 / 32);
     if (int rc = index_update_row_norms(h, r0, n)) return rc;
     if (int rc = mark_live(h, r0, n)) return rc;
     if (int rc = finish_add(h)) return rc;
@@ -280,6 +298,7 @@ extern "C" int hr_index_add_device_at(hr_index* h, const float* rows_dev, int64_
         if (rc) return rc;
         hipLaunchKernelGGL(k_mark_live, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, dest_dev, n, h->live);
         HIP_TRY(hipGetLastError());
+        shadow_stale(h, 0);  // (rows placed anywhere)
     }
     h->n = n_rows_after;
     const int64_t words = (h->n + 31) / 32;
@@ -409,15 +428,16 @@ static int make_plan(const hr_index* h, int B, Plan* p) {
     // k-steps) form groups only at the dims the 128-query FILTER takes (below); elsewhere they keep one group.
     constexpr int max_groups = 4;
     // (fp32 rows form groups only where the 128-query FILTER takes them: its eight-wave form reads fp32 rows)
-    p->NG = (QB == 2 && (h->dtype != F32 || wide_filter_ok(h->dtype, h->S))) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
+    const int sdt = scan_dtype(h);
+    p->NG = (QB == 2 && (sdt != F32 || wide_filter_ok(sdt, h->S))) ? std::max(1, std::min(max_groups, (B + 63) / 64)) : 1;
     // D > 1280 (Youtu-Embedding's 2048 / 2304 dims) leaves LDS for one 32-query block only: a 64-query
     // batch was two corpus passes; 32-query groups share one (2M x 2304: 3.03 -> 1.98 ms/batch)
-    if (QB == 1 && B > 32 && h->dtype != F32) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
+    if (QB == 1 && B > 32 && sdt != F32) p->NG = std::max(1, std::min(max_groups, (B + 31) / 32));
     // the 128-query FILTER (hr_wide.hip) serves query groups in pairs: round the group count up to even
-    if (p->NG > 1 && QB == 2 && wide_filter_ok(h->dtype, h->S)) p->NG = (p->NG + 1) & ~1;
+    if (p->NG > 1 && QB == 2 && wide_filter_ok(sdt, h->S)) p->NG = (p->NG + 1) & ~1;
     p->Bp = p->NG * QB * 32;
     // ring depth: deepest prefetch that compiles without spills (see `make resource`)
-    const int pmax = h->dtype == F32 ? (QB == 2 ? 4 : 8) : 16;
+    const int pmax = sdt == F32 ? (QB == 2 ? 4 : 8) : 16;
     p->P = (h->S % 16 == 0 && pmax >= 16) ? 16 : (h->S % 8 == 0 && pmax >= 8 ? 8 : 4);
     return HR_OK;
 }
@@ -430,10 +450,10 @@ static bool wide_plan(const hr_index* h, const Plan& pl, int np, bool tile_list)
     // (bf16, k = 20 / 50: B = 128 31.9k / 29.6k vs 28.2k / 27.6k QPS, but B = 256 32.4k / 29.8k vs 33.0k / 32.2k,
     // and k = 100's 5 parts FILTER in 5.0 vs 4.5 ms: the appends of its slower-rising thresholds cost more than
     // the L2 re-reads of the groups; profiles/r03_wide_parts_*)
-    const bool f32 = h->dtype == F32;
-    const int max_parts = std::min(f32 ? 7 : 3, wide_max_parts(h->dtype));
+    const bool f32 = scan_dtype(h) == F32;
+    const int max_parts = std::min(f32 ? 7 : 3, wide_max_parts(scan_dtype(h)));
     const bool parts_ok = np <= max_parts && (f32 || pl.NG == 2);
-    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) && wide_filter_ok(h->dtype, h->S);
+    return pl.NG >= 2 && pl.QB == 2 && !tile_list && (np == 1 || parts_ok) && wide_filter_ok(scan_dtype(h), h->S);
 }
 
 // dynamic tail of a FILTER over W waves: the last 10 % of the units go out in 2-unit runs from the counter, but
@@ -521,7 +541,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
         if (wide_plan(h, pl, a.np, a.tile_list != nullptr) && a.use_groups) {
             // 129-256 queries (four groups), one row part: ONE pass of the 256-query FILTER (hr_q256.hip) instead of
             // two of the 128-query one
-            if (pl.NG == 4 && a.np == 1 && h->q256 && q256_filter_ok(h->dtype, h->S)) {
+            if (pl.NG == 4 && a.np == 1 && h->q256 && q256_filter_ok(scan_dtype(h), h->S)) {
                 const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (a.n_units + 7) / 8));
                 const int64_t W = (int64_t)blocks * 4;  // waves: one candidate region per (group, wave)
                 HIP_TRY(sc.pbuf.ensure((size_t)4 * 64 * W * kCapW * sizeof(float2)));
@@ -582,7 +602,7 @@ static int launch_scan_p(hr_index* h, Scratch& sc, int cus, const Plan& pl, cons
 
 static int launch_scan(hr_index* h, Scratch& sc, int cus, const Plan& pl, const ScanArgs& a, int mode,
                        hipStream_t st) {
-    return dispatch_dt(h->dtype, [&](auto dt) -> int {
+    return dispatch_dt(scan_dtype(h), [&](auto dt) -> int {
         constexpr int DT = decltype(dt)::value;
         auto go = [&](auto mt) -> int {
             constexpr int MT = decltype(mt)::value;
@@ -675,7 +695,7 @@ static void persist_free(hr_index* h) {
 static bool persist_wanted(hr_index* h, const Plan& pl, int np, bool early, const uint64_t* mask_dev, int64_t n_tiles) {
     const int mode = h->ps ? h->ps->mode : 1;
     if (mode == 0 || !early || mask_dev || np != 1 || pl.NG != 1 || pl.QB != 2 || h->stripe_G != 1) return false;
-    if (!(h->dtype != F32 ? pl.P == 16 : pl.P == 4)) return false;
+    if (!(scan_dtype(h) != F32 ? pl.P == 16 : pl.P == 4)) return false;
     return mode == 2 || (n_tiles >= 128 * 1024 && n_tiles <= 160 * 1024);
 }
 
@@ -745,6 +765,47 @@ static int persist_configure(hr_index* h, const Plan& pl) {
     return HR_OK;
 }
 
+// fp32 tiles [t0, t1) -> the 16-bit shadow: k-step chunk c of a tile, lane l -> the 8 elements XFrag<MT, F32> forms
+// from bytes l*16 of the chunk's two KiB halves, rounded to MT the same way (packed hardware RNE)
+template <int MT>
+__global__ __launch_bounds__(256) void k_shadow(const uint8_t* __restrict__ rows, uint8_t* __restrict__ rows16, int S,
+                                                int64_t t0, int64_t t1) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (tile - t0) * S * 64 + chunk * 64 + lane
+    const int64_t per_tile = (int64_t)S * 64;
+    if (i >= (t1 - t0) * per_tile) return;
+    const int64_t t = t0 + i / per_tile, c = (i % per_tile) >> 6;
+    const int lane = (int)(i & 63);
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    typedef float f32x8 __attribute__((ext_vector_type(8)));
+    const uint8_t* src = rows + (t * S + c) * 2048 + lane * 16;
+    const f32x4 fa = *(const f32x4*)src, fb = *(const f32x4*)(src + 1024);
+    const f32x8 f = __builtin_shufflevector(fa, fb, 0, 1, 2, 3, 4, 5, 6, 7);
+    u32x4 o;
+    if constexpr (MT == BF16) o = __builtin_bit_cast(u32x4, __builtin_convertvector(f, bf16x8));
+    else o = __builtin_bit_cast(u32x4, __builtin_convertvector(f, f16x8));
+    *(u32x4*)(rows16 + (t * S + c) * 1024 + lane * 16) = o;
+}
+
+// bring the shadow up to the rows (h->stream, synchronous; never inside a capture: the graph path calls it first)
+int shadow_update(hr_index* h) {
+    if (!h->rows16 || h->shadow_lo == INT64_MAX) return HR_OK;
+    const int64_t t1 = (h->n + 31) / 32, t0 = std::min(h->shadow_lo, t1);
+    if (t1 > t0) {
+        if (int rc = set_device(h)) return rc;
+        const int64_t work = (t1 - t0) * h->S * 64;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, h->stream, h->rows, h->rows16, h->S,
+                               t0, t1);
+        };
+        if (mfma_type(h) == BF16) go(k_shadow<BF16>);
+        else go(k_shadow<F16>);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    h->shadow_lo = INT64_MAX;
+    return HR_OK;
+}
+
 // error-bound constants for the approximate (MFMA) scores, see DESIGN.md "Exactness guard"
 static double acc_gamma(const hr_index* h) { return (double)(h->dpad + 64) * std::ldexp(1.0, -23); }
 static double storage_u(const hr_index* h) {
@@ -766,6 +827,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
                        const double* kth_dev_host /* mode 1: host array of kth, B */, int mode, int cap_out,
                        Cand* cand_out, double* bound_out, hipStream_t st, hipStream_t st_tail,
                        hipEvent_t q_ready = nullptr) {
+    if (int rc = shadow_update(h)) return rc;
     Plan pl;
     if (int rc = make_plan(h, B, &pl)) return rc;
     const int Bp = pl.Bp;
@@ -943,7 +1005,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     }
 
     ScanArgs a{};
-    a.rows = h->rows;
+    a.rows = scan_rows(h);
     a.xnorm = h->metric == L2 ? h->xnorm : nullptr;
     a.live = h->live;
     a.mask = (const uint32_t*)mask_dev;
@@ -1065,7 +1127,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
             HIP_TRY(hipEventRecord(ps.posted[pslot], sp));
             HIP_TRY(hipStreamWaitEvent(ps.pst, ps.posted[pslot], 0));
             ps.launched = true;  // (before the launch: a quiesce after a failed launch still waits on the stream)
-            if (int rc = launch_persist(mfma_type(h), h->dtype, pl.P, ps.nwg, pa, scan_lds_bytes(h, pl.QB), ps.pst))
+            if (int rc = launch_persist(mfma_type(h), scan_dtype(h), pl.P, ps.nwg, pa, scan_lds_bytes(h, pl.QB), ps.pst))
                 return rc;
             ps.active = true;
             sc.wtiles_valid = false;
@@ -1270,6 +1332,7 @@ static int search_device_impl(hr_index* h, const float* q_dev, int B, int k, con
 // small search -- ~10 launches, 6 copies, 2 waits -- was most of its latency on small collections.
 // Returns HR_E_UNSUPPORTED when the normal path must run instead (a shape's first use, a failed capture).
 static int sync_graph_search(hr_index* h, const float* q, int B, int k, float* scores_out, int64_t* rows_out) {
+    if (int rc = shadow_update(h)) return rc;  // (a replay reads the shadow as it is now)
     hipStream_t st = h->stream;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t qb = (size_t)B * h->dim * 4, sb = (size_t)B * k * 4, rb = (size_t)B * k * 8;
@@ -2056,6 +2119,7 @@ extern "C" int hr_index_load(const char* path, int n_dev, const int* dev_ids, hr
     h->n = hd.n;
     h->n_live = hd.n_live;
     h->max_norm2 = hd.max_norm2;
+    shadow_stale(h, 0);
     if (int rc2 = index_finish_load(h)) {
         hr_index_destroy(h);
         return rc2;
@@ -2085,6 +2149,7 @@ extern "C" void hr_index_destroy(hr_index* h) {
     persist_free(h);  // every persistent FILTER instance exits before the rows go
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rows) (void)hipFree(h->rows);
+    if (h->rows16) (void)hipFree(h->rows16);
     if (h->live) (void)hipFree(h->live);
     if (h->xnorm) (void)hipFree(h->xnorm);
     if (h->norm_bits) (void)hipFree(h->norm_bits);

@@ -135,6 +135,14 @@ struct hr_index {
     int64_t n = 0, cap = 0, n_live = 0;
     double max_norm2 = 0.0;
     uint8_t* rows = nullptr;        // tiled corpus
+    // fp32 corpora: a 16-bit copy of the rows in the MFMA type (mfma_type), tiled as a 16-bit corpus, that the
+    // approximate passes (SAMPLE, FILTER, collect) stream instead of the fp32 tiles -- the values they round every
+    // fragment to anyway, at half the bytes; the exact rescoring and exhaustive passes keep reading the fp32 rows.
+    // Maintained lazily: row writers lower shadow_lo (first stale tile) and the next search converts [shadow_lo,
+    // tiles).  HIPRAG_F32_SHADOW=0 at create: none (the fp32 tiles are streamed and rounded in the kernels).
+    uint8_t* rows16 = nullptr;
+    bool shadow = false;
+    int64_t shadow_lo = 0;
     uint32_t* live = nullptr;       // one word per tile
     float* xnorm = nullptr;         // euclidean only: fp32 |x|^2 per stored row (approximate scan score)
     std::vector<uint32_t> live_host;
@@ -324,4 +332,15 @@ inline int dispatch_dt(int dt, F&& f) {
 inline int mfma_type(const hr_index* h) {
     return (h->dtype == F16 || (h->dtype == F32 && h->metric == COSINE)) ? F16 : BF16;
 }
+
+// what the approximate passes stream: the 16-bit shadow of an fp32 corpus (as a corpus of the MFMA type), else the
+// stored rows.  The exactness guard's storage term (storage_u) stays the fp32 one: the shadow holds exactly the
+// RNE-rounded values the fp32 kernels would form on the fly.
+inline int scan_dtype(const hr_index* h) { return h->rows16 ? mfma_type(h) : h->dtype; }
+inline const uint8_t* scan_rows(const hr_index* h) { return h->rows16 ? h->rows16 : h->rows; }
+// a row writer touched tiles from t0 on (INT64_MAX: the shadow is current)
+inline void shadow_stale(hr_index* h, int64_t t0) {
+    if (h->shadow && t0 < h->shadow_lo) h->shadow_lo = t0 < 0 ? 0 : t0;
+}
+int shadow_update(hr_index* h);
 

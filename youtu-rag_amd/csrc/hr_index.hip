@@ -134,14 +134,24 @@ int index_grow(hr_index* h, int64_t need_rows) {
     if (h->shadow) {  // the 16-bit shadow grows with the rows (its converted tiles carried over)
         const size_t tb16 = (size_t)h->S * 1024;
         uint8_t* n16 = nullptr;
-        HIP_TRY(hipMalloc(&n16, (size_t)(new_cap / 32) * tb16));
-        HIP_TRY(hipMemsetAsync(n16, 0, (size_t)(new_cap / 32) * tb16, h->stream));
-        if (h->rows16) {
-            HIP_TRY(hipMemcpyAsync(n16, h->rows16, (size_t)(h->cap / 32) * tb16, hipMemcpyDeviceToDevice, h->stream));
+        if (hipMalloc(&n16, (size_t)(new_cap / 32) * tb16) != hipSuccess) {
+            // no room for it beside the fp32 rows (a corpus of more than ~2/3 of the device): the index goes on
+            // without a shadow, scanning the fp32 tiles as before (plans follow scan_dtype)
+            (void)hipGetLastError();
             HIP_TRY(hipStreamSynchronize(h->stream));
-            HIP_TRY(hipFree(h->rows16));
+            if (h->rows16) HIP_TRY(hipFree(h->rows16));
+            h->rows16 = nullptr;
+            h->shadow = false;
+            h->shadow_lo = INT64_MAX;
+        } else {
+            HIP_TRY(hipMemsetAsync(n16, 0, (size_t)(new_cap / 32) * tb16, h->stream));
+            if (h->rows16) {
+                HIP_TRY(hipMemcpyAsync(n16, h->rows16, (size_t)(h->cap / 32) * tb16, hipMemcpyDeviceToDevice, h->stream));
+                HIP_TRY(hipStreamSynchronize(h->stream));
+                HIP_TRY(hipFree(h->rows16));
+            }
+            h->rows16 = n16;
         }
-        h->rows16 = n16;
     }
     h->rows = nr;
     h->live = nl;

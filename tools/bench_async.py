@@ -22,17 +22,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "youtu-rag_amd"), REPO]
 
 
-def build_store(n: int, max_batch: int, idx=None):
+def build_store(n: int, max_batch: int, idx=None, dtype: str = "bf16"):
     from hiprag import _native
     from hiprag.rag import HipVectorStore, VectorStoreConfig
 
     D = 1024
     if idx is None:
-        idx = _native.NativeIndex(D, "bf16", "cosine")
+        idx = _native.NativeIndex(D, dtype, "cosine")
         idx.reserve(n)
         idx.add_synthetic(0, 0, n)
     cfg = VectorStoreConfig(backend="hip", collection_name="bench", persist_directory="/tmp/hiprag_bench_async",
-                            index_params={"dtype": "bf16", "persist": False, "max_batch": max_batch})
+                            index_params={"dtype": dtype, "persist": False, "max_batch": max_batch})
     st = HipVectorStore(cfg, index_factory=lambda d: idx)
     st._ensure_index(D)
     recs = []
@@ -78,6 +78,7 @@ def main():
     p.add_argument("--gc-freeze", default="0", help="0/1 list: gc.freeze() after building the store (A/B)")
     p.add_argument("--seconds", type=float, default=3.0)
     p.add_argument("--k", type=int, default=10)
+    p.add_argument("--dtype", default="bf16", help="stored rows: bf16, or f32 (the store's default, the reference's)")
     p.add_argument("--native-async", default="1", help="0/1 list: event-loop native launches (1) or worker threads (0)")
     p.add_argument("--torch", type=int, default=1,
                    help="import torch first: a serving process's heap (the in-process embedder), ~170k tracked objects "
@@ -108,7 +109,7 @@ def main():
     q, _ = synth.planted_queries(0, args.rows, 1024, 2048, qseed=11)
     queries = [np.asarray(x, np.float32) for x in q]
     t0 = time.perf_counter()
-    st, _ = build_store(args.rows, 64)
+    st, _ = build_store(args.rows, 64, dtype=args.dtype)
     print(f"# store of {args.rows} rows in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     gc.collect()
@@ -139,7 +140,7 @@ def main():
                     with open(f"{args.profile}.{C}_{mb}", "w") as f:
                         pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(30)
                 a = np.asarray(lat) * 1e3
-                print(json.dumps({"rows": args.rows, "max_batch": mb, "depth": depth, "gc_freeze": fz,
+                print(json.dumps({"rows": args.rows, "dtype": args.dtype, "max_batch": mb, "depth": depth, "gc_freeze": fz,
                                   "native_async": na, "native_launches": st._batcher.native_launches - nat0,
                                   "clients": C,
                                   "queries": len(lat), "qps": round(len(lat) / wall, 1),

@@ -264,4 +264,16 @@ def test_fused_retrieve_matches_two_step_path(cpu_emb, tmp_path):
     assert all(r.chunk.metadata["grp"] == "g1" for r in got[-1])
     high = run(ret.retrieve(qs[1][0], top_k=5, similarity_threshold=0.99))  # threshold filtering after the ranks
     assert all(r.score >= 0.99 for r in high)
+    # one cohort, different thresholds and top_k per call: each call's hits are the two-step path's, ranks counted
+    # before its own threshold drops any (base_retriever.py:66-72)
+    mixed = [(qs[2][0], 6, 0.0), (qs[2][0], 6, 0.5), (qs[3][0], 2, 0.3), (qs[4][0], 7, -1.0)]
+
+    async def fused_mixed():  # (concurrent calls on one loop: formed into one cohort by the next loop iteration)
+        return await asyncio.gather(*[ret.retrieve(q, top_k=k, similarity_threshold=t) for q, k, t in mixed])
+
+    got_m = run(fused_mixed())
+    for (q, k, t), res in zip(mixed, got_m):
+        want = run(two.retrieve(q, top_k=k, similarity_threshold=t))
+        assert [(r.chunk.id, r.rank) for r in res] == [(r.chunk.id, r.rank) for r in want]
+    assert len(got_m[1]) <= len(got_m[0]) and [r.rank for r in got_m[0]] == list(range(1, 7))
     ret._fused.close()

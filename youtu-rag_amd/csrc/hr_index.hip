@@ -411,7 +411,9 @@ extern "C" int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* met
 // ---------------------------------------------------------------- search pieces
 // A/B knobs of the scan plan, read once (timing studies; the defaults are the measured choices):
 // HIPRAG_TAIL_CUS (32), HIPRAG_SAMPLE_MIN (1024: sampled tiles of a shard <= 80k tiles), HIPRAG_DYN_PCT (10),
-// HIPRAG_REFRESH_EVERY (4)
+// HIPRAG_REFRESH_EVERY (0 = by shard size: group-maxima refreshes every 8 tiles on shards of <= 48k tiles, every 4
+// above -- 1.25M x 1024: 0.403-0.406 against 0.410-0.418 ms/step; 1M x 768 unchanged; 10M x 1024: 2.97-3.03 against
+// 2.94-2.95 ms, three alternating repeats each, profiles/r06_refresh_every_ab.jsonl)
 static int knob(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
@@ -419,7 +421,8 @@ static int knob(const char* name, int dflt) {
 static const int kTailCus = knob("HIPRAG_TAIL_CUS", 32);
 static const int kSampleMin = knob("HIPRAG_SAMPLE_MIN", 1024);
 static const int kDynPct = knob("HIPRAG_DYN_PCT", 10);
-static const int kRefreshEvery = std::max(1, knob("HIPRAG_REFRESH_EVERY", 4));
+static const int kRefreshEvery = std::max(0, knob("HIPRAG_REFRESH_EVERY", 0));
+static int refresh_every(int64_t n_tiles) { return kRefreshEvery ? kRefreshEvery : (n_tiles <= 48 * 1024 ? 8 : 4); }
 
 struct Plan {
     int QB, Bp, P;
@@ -1041,7 +1044,7 @@ static int shard_chunk(hr_index* h, const float* q_dev, int B, int kc, int kj, c
     // positions, not tiles) parts keep contiguous per-wave ranges, as does the SAMPLE pass.
     a.strided = 1;
     a.teams = tl_ptr ? 0 : 1;
-    a.refresh_every = kRefreshEvery;
+    a.refresh_every = refresh_every(n_tiles);
     // refresh loads issued before the tile's k-loop (ScanArgs::early_refresh): on small shards (the dual
     // FILTER streams' range, <= 5.1M rows) 1.25M rows 0.425 -> 0.421 ms/step; at 10M rows 2.99-3.03 ->
     // 3.05-3.07 ms (two alternating repeats on one box), so big shards keep the epilogue loads ...

@@ -411,9 +411,10 @@ extern "C" int hr_index_info(hr_index* h, int* dim_out, int* dtype_out, int* met
 // ---------------------------------------------------------------- search pieces
 // A/B knobs of the scan plan, read once (timing studies; the defaults are the measured choices):
 // HIPRAG_TAIL_CUS (32), HIPRAG_SAMPLE_MIN (1024: sampled tiles of a shard <= 80k tiles), HIPRAG_DYN_PCT (10),
-// HIPRAG_REFRESH_EVERY (0 = by shard size: group-maxima refreshes every 8 tiles on shards of <= 48k tiles, every 4
-// above -- 1.25M x 1024: 0.403-0.406 against 0.410-0.418 ms/step; 1M x 768 unchanged; 10M x 1024: 2.97-3.03 against
-// 2.94-2.95 ms, three alternating repeats each, profiles/r06_refresh_every_ab.jsonl)
+// HIPRAG_REFRESH_EVERY (0 = by shard size: group-maxima refreshes every 8 tiles on shards of <= 160k tiles, every 4
+// above -- 1.25M x 1024: 0.403-0.406 against 0.410-0.418 ms/step; 5M: 1.494-1.497 against 1.516-1.519; 1M x 768 and
+// 2.5M unchanged; 10M x 1024: 2.97-3.03 against 2.94-2.95 ms; three alternating repeats each,
+// profiles/r06_refresh_every_ab.jsonl)
 static int knob(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
@@ -422,7 +423,7 @@ static const int kTailCus = knob("HIPRAG_TAIL_CUS", 32);
 static const int kSampleMin = knob("HIPRAG_SAMPLE_MIN", 1024);
 static const int kDynPct = knob("HIPRAG_DYN_PCT", 10);
 static const int kRefreshEvery = std::max(0, knob("HIPRAG_REFRESH_EVERY", 0));
-static int refresh_every(int64_t n_tiles) { return kRefreshEvery ? kRefreshEvery : (n_tiles <= 48 * 1024 ? 8 : 4); }
+static int refresh_every(int64_t n_tiles) { return kRefreshEvery ? kRefreshEvery : (n_tiles <= 160 * 1024 ? 8 : 4); }
 
 struct Plan {
     int QB, Bp, P;
